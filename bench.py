@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE metric: GiB/s of the device-resident ncclSum reduction.
+
+Workload (BASELINE.json configs[1]): one step = one
+call of the hot path, nbxReduceMulti (the reduceCopy replacement), folding
+8 fp32 inputs of 256 MiB (67,108,864 elements) into one 256 MiB output on the
+GPU — 2.25 GiB of algorithmic HBM traffic per step, inputs resident in HBM
+before timing starts.
+
+N GPUs (one process per GPU, torch.distributed.run): every rank reduces its
+own 8 x 256 MiB shard (the path shards by chunk; no data-path collective), so
+scaling is weak and value = N x 2.25 GiB / max-over-ranks step time.
+
+Extra JSON fields:
+  roofline     — the dominant kernel's algorithmic bytes per launch / its mean
+                 launch duration (HIP events on the launch stream) vs the
+                 8 TB/s HBM3E peak; `traffic` = HBM bytes per launch from the
+                 committed rocprofv3 PMC pass (profiles/), or null.
+  cpu_baseline — the oracle's C restatement (oracle/reduce_oracle.c, a port of
+                 the reference semantics) timed on this box's host cores on a
+                 bounded sample of the same workload (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+N_SRCS = 8
+COUNT = 64 << 20                    # fp32 elements per 256 MiB input
+ELT = 4
+ALG_BYTES = (N_SRCS + 1) * COUNT * ELT   # (nSrcs + nDsts) x count x sizeof(T), SURVEY §8(d)
+HBM_PEAK_GBS = 8000.0               # MI355X HBM3E spec peak, MI355X_MICROARCH.md
+METRIC = "GiB/s device-resident ncclSum reduce, 256 MiB fp32, 1/2/4/8 MI355X (% HBM peak)"
+
+
+def _load_package():
+    from __graft_entry__ import _load_package as lp
+    return lp()
+
+
+def _dist_init():
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local) if backend == "nccl" else None)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(value: float, world: int) -> float:
+    """Max of a host float over ranks (the contract's max-over-ranks timing)."""
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _pmc_traffic():
+    """HBM bytes per launch of the f32 sum 8-src kernel from the committed PMC
+    summary (profiles/pmc_latest.json, written by scripts/pmc_traffic.py from
+    separate rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 note)."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") == "config_b_f32_sum_8x256MiB":
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(seconds: float = 1.5):
+    """Oracle (C port of the reference semantics) on host cores, same workload
+    shape, bounded sample. Returns the cpu_baseline JSON object."""
+    import numpy as np
+    from oracle import oracle   # checker / baseline only
+    oracle.build()
+    threads = int(os.environ.get("NBX_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    rng = np.random.default_rng(1234)
+    srcs = [rng.uniform(-1, 1, COUNT).astype(np.float32) for _ in range(N_SRCS)]
+    out = [np.empty(COUNT, np.float32)]
+    oracle.reduce_multi(srcs, 7, 0, threads=threads, out=out)   # warm (page-in)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        oracle.reduce_multi(srcs, 7, 0, threads=threads, out=out)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 2:
+            break
+    per = el / n
+    return {"value": round(ALG_BYTES / per / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{n} passes of the full config-B workload (8 x 256 MiB fp32 -> 256 MiB), "
+                      f"{el:.2f} s wall x {threads} threads, oracle/reduce_oracle.c (gcc -O3)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5)
+    ap.add_argument("--check", action="store_true", help="verify step output against the oracle (sampled)")
+    args = ap.parse_args()
+
+    import torch
+    world, rank, local = _dist_init()
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    nbx = _load_package()
+    nbx.load_library()
+    dev = torch.device("cuda", local)
+
+    # inputs resident in HBM before timing: seeded uniform[-1,1) per rank
+    g = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
+    srcs = [torch.rand(COUNT, device=dev, generator=g).mul_(2).sub_(1) for _ in range(N_SRCS)]
+    out = torch.empty(COUNT, device=dev)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    op = nbx.host_to_dev_redop(nbx.ncclRedOp.ncclSum, nbx.ncclDataType.ncclFloat32, 1)
+    dptr = [out.data_ptr()]
+    sptr = [t.data_ptr() for t in srcs]
+    f32 = int(nbx.ncclDataType.ncclFloat32)
+
+    def step():
+        nbx.reduce_multi(dptr, sptr, COUNT, f32, op, 0, False, sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        step()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    _barrier(world)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(wall, world)
+    ms_per_step = wall * 1e3 / args.steps
+    kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    kern_avg_ms = sum(kern_ms) / len(kern_ms)
+    value = world * ALG_BYTES / (wall / args.steps) / 2**30
+
+    if args.check:
+        import numpy as np
+        idx = torch.randint(0, COUNT, (1 << 16,), device=dev)
+        ref = srcs[0][idx].clone()
+        for s in srcs[1:]:
+            ref = ref + s[idx]
+        assert torch.equal(out[idx], ref), "bench output differs from the left-fold reference"
+
+    achieved = ALG_BYTES / (kern_avg_ms * 1e-3) / 1e9
+    traffic = _pmc_traffic()
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded uniform[-1,1) per rank, resident in HBM)",
+        "config": {"workload": "config B: 8-input fp32 ncclSum reduce (nbxReduceMulti), 256 MiB per input, "
+                               "device-resident; N ranks = N independent shards",
+                   "n_srcs": N_SRCS, "count_per_input": COUNT, "bytes_per_step_per_gpu": ALG_BYTES,
+                   "parallelism": f"shard{world}"},
+        "pct_hbm_peak": round(100.0 * (ALG_BYTES / (wall / args.steps)) / (HBM_PEAK_GBS * 1e9), 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "kReducePacks<FnSumF<TyF32>, NSRC=8>", "kernel_avg_ms": round(kern_avg_ms, 5),
+                     "alg_bytes_per_launch": ALG_BYTES},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del srcs, out
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

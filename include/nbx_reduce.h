@@ -1,0 +1,92 @@
+/*
+ * nbx_reduce.h — internal C ABI of the MI355X reduction core.
+ *
+ * This is the hot path the library is built around: NCCL's device-side
+ * multi-source element-wise reduction ("ReduceOrCopyMulti"),
+ *   reduceCopy / reduceCopyPacks   /root/reference/src/device/common_kernel.h:28-239
+ *   functors                       /root/reference/src/device/reduce_kernel.h:34-526
+ *   one-rank launch                /root/reference/src/device/onerank.cu:48-79
+ *   host op encoding               /root/reference/src/enqueue.cc:1436-1512
+ * exposed as plain C so that the NCCL API layer, a multi-GPU sharder, a test
+ * harness or an emulator can call it with raw device pointers.
+ *
+ * Semantics of nbxReduceMulti (identical to reduceCopy, common_kernel.h:79-158):
+ *   for every element i in [0, count):
+ *     acc = pre_0(srcs[0][i])
+ *     for s = 1 .. nSrcs-1:  acc = Fn(acc, pre_s(srcs[s][i]))    (ordered left fold)
+ *     if postOp:             acc = post(acc)
+ *     for d in dsts:         dsts[d][i] = acc
+ *   where pre_s is the PreMulSum pre-multiply for s < nPreOpSrcs (identity
+ *   otherwise) and post is the SumPostDiv integer divide.
+ */
+#ifndef NBX_REDUCE_H_
+#define NBX_REDUCE_H_
+
+#include "nccl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device reduction opcode — /root/reference/src/include/device.h:26-30 (same order). */
+typedef enum {
+  nbxDevSum = 0,
+  nbxDevProd = 1,
+  nbxDevMinMax = 2,
+  nbxDevPreMulSum = 3,
+  nbxDevSumPostDiv = 4,
+  nbxNumDevRedOps = 5
+} nbxDevRedOp_t;
+
+/* Full device op — /root/reference/src/include/device.h:31-36 (ncclDevRedOpFull).
+ * scalarArg: MinMax xormask, PreMulSum scalar bits (element type, low bytes),
+ * SumPostDiv divisor. If scalarArgIsPtr, scalarArg is a device address of the
+ * PreMulSum scalar, dereferenced by the kernel while it runs (ncclScalarDevice,
+ * common.h:100-119 / onerank.cu:32-42). */
+typedef struct {
+  int32_t op;             /* nbxDevRedOp_t */
+  int32_t scalarArgIsPtr; /* bool */
+  uint64_t scalarArg;
+} nbxDevRedOpFull;
+
+#define NBX_MAX_SRCS 32   /* > 8 sources run as ordered multi-pass folds */
+#define NBX_MAX_DSTS 2
+
+/* Host-side op encoding: replaces hostToDevRedOp, enqueue.cc:1436-1512, for
+ * the built-in ops (Sum/Prod/Max/Min/Avg). nRanks feeds ncclAvg. */
+ncclResult_t nbxHostToDevRedOp(nbxDevRedOpFull* out, ncclRedOp_t op,
+                               ncclDataType_t datatype, int nRanks);
+
+/* The reduction core: replaces reduceCopy<...>(...) (common_kernel.h:183-239)
+ * plus its kernel shell (onerank.cu:14-45, common.h:121-210).
+ * Stream-ordered and asynchronous; returns once the kernel is enqueued.
+ * count == 0 is a no-op. Any pointer alignment is accepted (16-B packs when
+ * the pointers share one alignment, element packs otherwise — common_kernel.h:209-238).
+ * Errors: ncclInvalidArgument for nSrcs outside [1, NBX_MAX_SRCS], nDsts
+ * outside [1, NBX_MAX_DSTS], a NULL pointer with count > 0, a bad datatype,
+ * op or op/type combination (SumPostDiv on floats: reduce_kernel.h:506-509);
+ * ncclUnhandledCudaError if the launch fails. */
+ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
+                            const void* const* srcs, int nSrcs,
+                            size_t count, ncclDataType_t datatype,
+                            nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
+                            ncclStream_t stream);
+
+/* Launch knobs (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues, tuning.cc:12,
+ * connect.cc:314): blocksPerCU caps the grid at CUs x blocksPerCU workgroups
+ * (0 = default 8, env NBX_BLOCKS_PER_CU); policy 0 = default cache policy,
+ * 1 = nontemporal loads/stores. */
+ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int policy);
+ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* policy);
+
+/* Number of (datatype, device op) kernel sets compiled in (for the ABI test). */
+int nbxKernelCount(void);
+
+/* Version of the core ABI (bumped on incompatible changes). */
+int nbxAbiVersion(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NBX_REDUCE_H_ */

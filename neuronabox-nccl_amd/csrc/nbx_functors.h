@@ -1,0 +1,321 @@
+// nbx_functors.h — per-element reduction functors for gfx950 (CDNA4).
+//
+// MI355X-native restatement of the reference functors
+//   FuncSum / FuncProd / FuncMinMax     /root/reference/src/device/reduce_kernel.h:34-49, 147-170
+//   half/bf16 specialisations           reduce_kernel.h:236-269
+//   FuncPreMulSum (+ Apply_PreOp)       reduce_kernel.h:360-484
+//   FuncSumPostDiv (+ Apply_PostOp)     reduce_kernel.h:489-526
+// The reference expresses them as recursive BytePack templates over PTX; here
+// a functor works on one 16-byte pack held in a u32x4 (one dwordx4 per lane,
+// 1 KiB per wave64 instruction) and on single elements for tails.
+//
+// Numerics (each is bit-identical to the reference's float round trip,
+// because fp32 carries p = 24 >= 2p+2 bits for f16/bf16/fp8 — double rounding
+// is innocuous and every op is correctly rounded):
+//   f16  : native v_add_f16 / v_mul_f16 (RNE), packed by the compiler.
+//   bf16 : widen (shift), fp32 op, v_cvt_pk_bf16_f32 (RNE, NaN stays NaN).
+//   fp8  : v_cvt_pk_f32_{fp8,bf8} widen, fp32 op, RNE narrow (software, see
+//          fp8 note below). Not in the reference: this build's definition.
+//   f32/f64 : native IEEE ops; denormals preserved (.amdhsa_float_denorm_mode 3);
+//          build with -ffp-contract=off so x*s + acc is never fused.
+//   min/max (floats): NaN operand yields the other operand, ties return the
+//          second operand — the oracle's pinned fminf/fmaxf rule.
+//   integers: signed Sum/Prod/PreMulSum/MinMax run on the unsigned pattern
+//          (/root/reference/src/device/generate.py:125-133).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nbx {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+template <class E>
+union PackU {
+  u32x4 v;
+  E e[16 / sizeof(E)];
+};
+
+// -------------------------------------------------------------------------
+// Element-type traits: storage Elt, compute type C, widen / narrow.
+
+struct TyF32 {
+  using Elt = uint32_t; using C = float;
+  __device__ static C wide(Elt e) { return __uint_as_float(e); }
+  __device__ static Elt narrow(C c) { return __float_as_uint(c); }
+};
+struct TyF64 {
+  using Elt = uint64_t; using C = double;
+  __device__ static C wide(Elt e) { return __longlong_as_double((long long)e); }
+  __device__ static Elt narrow(C c) { return (Elt)__double_as_longlong(c); }
+};
+struct TyF16 {
+  using Elt = uint16_t; using C = _Float16;
+  __device__ static C wide(Elt e) { return __builtin_bit_cast(_Float16, e); }
+  __device__ static Elt narrow(C c) { return __builtin_bit_cast(uint16_t, c); }
+};
+struct TyBF16 {
+  using Elt = uint16_t; using C = float;
+  __device__ static C wide(Elt e) { return __uint_as_float((uint32_t)e << 16); }
+  __device__ static Elt narrow(C c) { return __builtin_bit_cast(uint16_t, (__bf16)c); }
+};
+
+// fp8 narrowing. OCP e4m3fn / e5m2, round-to-nearest-even, overflow -> NaN
+// (e4m3fn, which has no infinity) / -> +-inf (e5m2). Written in integer ops
+// on the fp32 bits so the result does not depend on the hardware converter's
+// clamp/saturation mode; widening uses the exact hardware converter.
+template <int E, int M, bool FN>
+__device__ __forceinline__ uint32_t f32ToSmall(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const uint32_t sign = (u >> 31) << (E + M);
+  const uint32_t a = u & 0x7fffffffu;
+  constexpr uint32_t expAllOnes = ((1u << E) - 1u) << M;
+  constexpr uint32_t nanCode = FN ? (expAllOnes | ((1u << M) - 1u)) : (expAllOnes | (1u << (M - 1)));
+  constexpr uint32_t infCode = expAllOnes;
+  constexpr uint32_t maxFinite = FN ? (expAllOnes | ((1u << M) - 2u))
+                                    : ((expAllOnes - (1u << M)) | ((1u << M) - 1u));
+  constexpr int bias = (1 << (E - 1)) - 1;
+  constexpr int emin = 1 - bias;
+  const int e = (int)(a >> 23) - 127;
+  const int et = e < emin ? emin : e;
+  int shift = (23 - M) + (et - e);
+  shift = shift > 31 ? 31 : shift;
+  const uint32_t mant = (a & 0x7fffffu) | 0x800000u;
+  uint32_t q = mant >> shift;
+  const uint32_t rem = mant & ((1u << shift) - 1u);
+  const uint32_t half = 1u << (shift - 1);
+  q += (rem > half || (rem == half && (q & 1u))) ? 1u : 0u;
+  uint32_t enc = (uint32_t)((et + bias - 1) << M) + q;
+  enc = enc > maxFinite ? (FN ? nanCode : infCode) : enc;
+  enc = (a >> 23) == 0 ? 0u : enc;                       // fp32 zero/denormal -> 0
+  enc = a >= 0x7f800000u ? (a == 0x7f800000u && !FN ? infCode : nanCode) : enc;
+  return sign | enc;
+}
+
+struct TyE4M3 {
+  using Elt = uint8_t; using C = float;
+  __device__ static C wide(Elt e) { return __builtin_amdgcn_cvt_pk_f32_fp8((int)e, false)[0]; }
+  __device__ static Elt narrow(C c) { return (Elt)f32ToSmall<4, 3, true>(c); }
+  // 4 codes in a dword <-> 4 floats
+  __device__ static void wide4(uint32_t w, float (&f)[4]) {
+    auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
+    auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = hi[0]; f[3] = hi[1];
+  }
+};
+struct TyE5M2 {
+  using Elt = uint8_t; using C = float;
+  __device__ static C wide(Elt e) { return __builtin_amdgcn_cvt_pk_f32_bf8((int)e, false)[0]; }
+  __device__ static Elt narrow(C c) { return (Elt)f32ToSmall<5, 2, false>(c); }
+  __device__ static void wide4(uint32_t w, float (&f)[4]) {
+    auto lo = __builtin_amdgcn_cvt_pk_f32_bf8((int)w, false);
+    auto hi = __builtin_amdgcn_cvt_pk_f32_bf8((int)w, true);
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = hi[0]; f[3] = hi[1];
+  }
+};
+
+template <class C>
+__device__ __forceinline__ bool isNan(C x) { return x != x; }
+
+// -------------------------------------------------------------------------
+// Generic pack helpers built from an element functor.
+
+template <class Fn>
+__device__ __forceinline__ u32x4 packRed(const Fn& fn, u32x4 a, u32x4 b) {
+  using E = typename Fn::Elt;
+  PackU<E> x, y;
+  x.v = a; y.v = b;
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(E)); i++) x.e[i] = fn.red(x.e[i], y.e[i]);
+  return x.v;
+}
+template <class Fn>
+__device__ __forceinline__ u32x4 packPre(const Fn& fn, u32x4 a) {
+  using E = typename Fn::Elt;
+  PackU<E> x;
+  x.v = a;
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(E)); i++) x.e[i] = fn.pre(x.e[i]);
+  return x.v;
+}
+template <class Fn>
+__device__ __forceinline__ u32x4 packPost(const Fn& fn, u32x4 a) {
+  using E = typename Fn::Elt;
+  PackU<E> x;
+  x.v = a;
+#pragma unroll
+  for (int i = 0; i < (int)(16 / sizeof(E)); i++) x.e[i] = fn.post(x.e[i]);
+  return x.v;
+}
+
+// Base: identity pre/post, generic pack ops. Derived functors override.
+template <class D, class E>
+struct FnBase {
+  using Elt = E;
+  static constexpr bool kHasPre = false;
+  static constexpr bool kHasPost = false;
+  __device__ E pre(E a) const { return a; }
+  __device__ E post(E a) const { return a; }
+  __device__ u32x4 redPack(u32x4 a, u32x4 b) const { return packRed(*static_cast<const D*>(this), a, b); }
+  __device__ u32x4 prePack(u32x4 a) const { return packPre(*static_cast<const D*>(this), a); }
+  __device__ u32x4 postPack(u32x4 a) const { return packPost(*static_cast<const D*>(this), a); }
+};
+
+// -------------------------------------------------------------------------
+// Integer functors (E = uint8_t / uint32_t / uint64_t storage; signed types
+// share them, generate.py:125-133).
+
+template <class E>
+struct FnSumInt : FnBase<FnSumInt<E>, E> {
+  __device__ explicit FnSumInt(uint64_t) {}
+  __device__ E red(E a, E b) const { return (E)(a + b); }
+  __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
+    if constexpr (sizeof(E) == 1) {
+      // bytewise modular add: carries stopped at byte boundaries (SWAR,
+      // same result as reduce_kernel.h:173-183)
+      const u32x4 lo7 = (u32x4)(0x7f7f7f7fu);
+      const u32x4 hi1 = (u32x4)(0x80808080u);
+      return ((a & lo7) + (b & lo7)) ^ ((a ^ b) & hi1);
+    } else if constexpr (sizeof(E) == 4) {
+      return a + b;
+    } else {
+      return packRed(*this, a, b);
+    }
+  }
+};
+
+template <class E>
+struct FnProdInt : FnBase<FnProdInt<E>, E> {
+  __device__ explicit FnProdInt(uint64_t) {}
+  __device__ E red(E a, E b) const { return (E)(a * b); }
+};
+
+template <class E>
+struct FnMinMaxInt : FnBase<FnMinMaxInt<E>, E> {
+  E xormask;  // reduce_kernel.h:43-46
+  __device__ explicit FnMinMaxInt(uint64_t arg) : xormask((E)arg) {}
+  __device__ E red(E a, E b) const { return ((E)(a ^ xormask) < (E)(b ^ xormask)) ? a : b; }
+};
+
+template <class E>
+struct FnPreMulSumInt : FnBase<FnPreMulSumInt<E>, E> {
+  static constexpr bool kHasPre = true;
+  E scalar;  // reduce_kernel.h:360-369
+  __device__ explicit FnPreMulSumInt(uint64_t arg) : scalar((E)arg) {}
+  __device__ E red(E a, E b) const { return (E)(a + b); }
+  __device__ E pre(E a) const { return (E)(a * scalar); }
+};
+
+// SumPostDiv: S is the signed/unsigned view used by `T / int` (reduce_kernel.h:524).
+template <class E, class S>
+struct FnSumPostDiv : FnBase<FnSumPostDiv<E, S>, E> {
+  static constexpr bool kHasPost = true;
+  int divisor;  // reduce_kernel.h:502
+  __device__ explicit FnSumPostDiv(uint64_t arg) : divisor((int)arg) {}
+  __device__ E red(E a, E b) const { return (E)(a + b); }
+  __device__ E post(E a) const { return (E)((S)a / divisor); }
+};
+// unsigned 32-bit: uint32 / int converts the int to unsigned.
+template <>
+__device__ inline uint32_t FnSumPostDiv<uint32_t, uint32_t>::post(uint32_t a) const {
+  return a / (uint32_t)divisor;
+}
+template <>
+__device__ inline uint64_t FnSumPostDiv<uint64_t, uint64_t>::post(uint64_t a) const {
+  return a / (uint64_t)(int64_t)divisor;
+}
+template <>
+__device__ inline uint64_t FnSumPostDiv<uint64_t, int64_t>::post(uint64_t a) const {
+  return (uint64_t)((int64_t)a / (int64_t)divisor);
+}
+
+// -------------------------------------------------------------------------
+// Floating-point functors over a type trait Ty.
+
+template <class Ty>
+struct FnSumF : FnBase<FnSumF<Ty>, typename Ty::Elt> {
+  using E = typename Ty::Elt;
+  __device__ explicit FnSumF(uint64_t) {}
+  __device__ E red(E a, E b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
+};
+template <class Ty>
+struct FnProdF : FnBase<FnProdF<Ty>, typename Ty::Elt> {
+  using E = typename Ty::Elt;
+  __device__ explicit FnProdF(uint64_t) {}
+  __device__ E red(E a, E b) const { return Ty::narrow(Ty::wide(a) * Ty::wide(b)); }
+};
+template <class Ty>
+struct FnMinMaxF : FnBase<FnMinMaxF<Ty>, typename Ty::Elt> {
+  using E = typename Ty::Elt;
+  bool isMin;  // reduce_kernel.h:47: (opArg & 1) == 0
+  __device__ explicit FnMinMaxF(uint64_t arg) : isMin((arg & 1ull) == 0ull) {}
+  __device__ E red(E a, E b) const {
+    auto x = Ty::wide(a);
+    auto y = Ty::wide(b);
+    bool pickA = isMin ? (x < y || isNan(y)) : (x > y || isNan(y));
+    return pickA ? a : b;   // narrowing a widened value is exact: keep the bits
+  }
+};
+template <class Ty>
+struct FnPreMulSumF : FnBase<FnPreMulSumF<Ty>, typename Ty::Elt> {
+  using E = typename Ty::Elt;
+  static constexpr bool kHasPre = true;
+  typename Ty::C scalar;  // reduce_kernel.h:360-413 (scalar of the element type)
+  __device__ explicit FnPreMulSumF(uint64_t arg) : scalar(Ty::wide((E)arg)) {}
+  __device__ E red(E a, E b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
+  __device__ E pre(E a) const { return Ty::narrow(Ty::wide(a) * scalar); }
+};
+
+// fp8: 4 codes per dword — widen a dword with two v_cvt_pk_f32_* and narrow
+// each lane result.
+template <class Ty, class Op>
+__device__ __forceinline__ u32x4 fp8PackMap2(u32x4 a, u32x4 b, Op op) {
+  u32x4 r;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    float fa[4], fb[4];
+    Ty::wide4(a[w], fa);
+    Ty::wide4(b[w], fb);
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) o |= (uint32_t)Ty::narrow(op(fa[k], fb[k])) << (8 * k);
+    r[w] = o;
+  }
+  return r;
+}
+
+template <class Ty>
+struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
+  __device__ explicit FnSumF8(uint64_t) {}
+  __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
+  __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
+    return fp8PackMap2<Ty>(a, b, [](float x, float y) { return x + y; });
+  }
+};
+template <class Ty>
+struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
+  __device__ explicit FnProdF8(uint64_t) {}
+  __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) * Ty::wide(b)); }
+  __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
+    return fp8PackMap2<Ty>(a, b, [](float x, float y) { return x * y; });
+  }
+};
+template <class Ty>
+struct FnPreMulSumF8 : FnBase<FnPreMulSumF8<Ty>, uint8_t> {
+  static constexpr bool kHasPre = true;
+  float scalar;
+  __device__ explicit FnPreMulSumF8(uint64_t arg) : scalar(Ty::wide((uint8_t)arg)) {}
+  __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
+  __device__ uint8_t pre(uint8_t a) const { return Ty::narrow(Ty::wide(a) * scalar); }
+  __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
+    return fp8PackMap2<Ty>(a, b, [](float x, float y) { return x + y; });
+  }
+  __device__ u32x4 prePack(u32x4 a) const {
+    const float s = scalar;
+    return fp8PackMap2<Ty>(a, a, [s](float x, float) { return x * s; });
+  }
+};
+
+}  // namespace nbx

@@ -1,0 +1,37 @@
+// nbx_kargs.h — kernel argument block and launch-table entry, shared by the
+// device instantiation units and the host launcher (no device code here, so
+// host .cc files compile as plain C++).
+#pragma once
+#include <stdint.h>
+
+namespace nbx {
+
+constexpr int kBlock = 256;      // workgroup = 4 wave64
+constexpr int kMaxKSrcs = 8;     // sources per kernel pass
+
+struct KArgs {
+  const void* src[kMaxKSrcs];
+  void* dst[2];
+  uint64_t nElts;     // total elements
+  uint64_t nPacks;    // 16-B packs in the aligned body (starts at headElts)
+  uint64_t arg;       // ncclDevRedOpFull.scalarArg (by value)
+  const void* argPtr; // device scalar (ncclScalarDevice) or nullptr
+  uint32_t preMask;   // bit s set: apply the PreMulSum pre-op to source s
+  int32_t nSrcs;
+  int32_t nDsts;
+  int32_t postOp;
+  int32_t headElts;   // elements before the 16-B aligned body
+  int32_t policy;     // cache policy (0 = default, 1 = nontemporal)
+};
+
+// Launch table for one functor (kernel entry points as host handles).
+
+struct KernelSet {
+  const void* packs[2][kMaxKSrcs];  // [policy][nSrcs-1]
+  const void* elts;
+  int unroll[kMaxKSrcs];         // packs per lane per source per tile
+  int eltBytes;
+  int valid;
+};
+
+}  // namespace nbx

@@ -1,0 +1,186 @@
+// nbx_kernels.h — the multi-source reduce-copy kernels for gfx950.
+//
+// MI355X-native replacement for reduceCopy / reduceCopyPacks
+// (/root/reference/src/device/common_kernel.h:28-239) and the one-rank kernel
+// shell (/root/reference/src/device/onerank.cu:14-45).
+//
+// Design (not a translation of the warp-32 hunk loop):
+//   * One wave64 instruction moves 1 KiB contiguous (64 lanes x 16-B dwordx4);
+//     a 256-thread workgroup owns a tile of U x 256 packs and issues all
+//     NSRC x U loads of a tile before folding, so every lane keeps
+//     NSRC*U*16 B in flight — the HBM-latency cover this load-bound loop
+//     needs (no LDS: an element-wise fold has no reuse to stage).
+//   * NSRC is a compile-time constant (1..8): sources are folded in order,
+//     acc = pre(src0); acc = Fn(acc, pre(src_s)), in registers — the
+//     reference's left fold (common_kernel.h:79-131), hence bit-exact.
+//   * Grid-stride over tiles with a capped grid (>= 8 workgroups per CU on
+//     256 CUs), a guarded last tile, and the <16-B head/tail elements of a
+//     shared misalignment done by one wave of the last workgroup.
+//   * Pointers that do not share one alignment modulo 16 take the element
+//     kernel (common_kernel.h:229-238's sizeof(T) packs).
+#pragma once
+#include <utility>
+#include "nbx_functors.h"
+#include "nbx_kargs.h"
+
+namespace nbx {
+
+
+
+
+// Device-resident scalar: read the element's bytes while the kernel runs
+// (reference: common.h:100-119 / onerank.cu:32-42 dereference by alignment;
+// reading exactly sizeof(T) yields the same scalar bits).
+template <class Fn>
+__device__ __forceinline__ uint64_t loadArg(const KArgs& a) {
+  if (a.argPtr != nullptr) return (uint64_t) * (const typename Fn::Elt*)a.argPtr;
+  return a.arg;
+}
+
+template <int POLICY>
+__device__ __forceinline__ u32x4 ldPack(const u32x4* p) {
+  if constexpr (POLICY == 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int POLICY>
+__device__ __forceinline__ void stPack(u32x4* p, u32x4 v) {
+  if constexpr (POLICY == 1) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// One element, any source count <= kMaxKSrcs (unrolled with a uniform guard
+// so the kernel-argument pointer array is never indexed dynamically).
+template <class Fn>
+__device__ __forceinline__ void reduceElt(const Fn& fn, const KArgs& a, int nSrcs, uint64_t i) {
+  using E = typename Fn::Elt;
+  E acc = ((const E*)a.src[0])[i];
+  if constexpr (Fn::kHasPre) if (a.preMask & 1u) acc = fn.pre(acc);
+#pragma unroll
+  for (int s = 1; s < kMaxKSrcs; s++) {
+    if (s < nSrcs) {
+      E v = ((const E*)a.src[s])[i];
+      if constexpr (Fn::kHasPre) if ((a.preMask >> s) & 1u) v = fn.pre(v);
+      acc = fn.red(acc, v);
+    }
+  }
+  if constexpr (Fn::kHasPost) if (a.postOp) acc = fn.post(acc);
+  ((E*)a.dst[0])[i] = acc;
+  if (a.nDsts > 1) ((E*)a.dst[1])[i] = acc;
+}
+
+template <class Fn, int NSRC, int U, int POLICY>
+__global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
+  using E = typename Fn::Elt;
+  constexpr int EPP = 16 / (int)sizeof(E);
+  const Fn fn(loadArg<Fn>(a));
+  const uint64_t headBytes = (uint64_t)a.headElts * sizeof(E);
+  const u32x4* src[NSRC];
+#pragma unroll
+  for (int s = 0; s < NSRC; s++) src[s] = (const u32x4*)((const char*)a.src[s] + headBytes);
+  u32x4* dst0 = (u32x4*)((char*)a.dst[0] + headBytes);
+  u32x4* dst1 = (u32x4*)((char*)a.dst[1] + headBytes);
+  const bool two = a.nDsts > 1;
+  const bool doPost = Fn::kHasPost && a.postOp;
+  const uint32_t preMask = a.preMask;
+  const uint64_t n = a.nPacks;
+  constexpr uint64_t kTile = (uint64_t)U * kBlock;
+  const uint64_t stride = (uint64_t)gridDim.x * kTile;
+
+  for (uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x; p < n; p += stride) {
+    u32x4 v[NSRC][U];
+    if (p + (uint64_t)(U - 1) * kBlock < n) {
+      // full tile: issue every load first, then fold
+#pragma unroll
+      for (int s = 0; s < NSRC; s++)
+#pragma unroll
+        for (int u = 0; u < U; u++) v[s][u] = ldPack<POLICY>(src[s] + p + u * kBlock);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        u32x4 acc = v[0][u];
+        if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
+#pragma unroll
+        for (int s = 1; s < NSRC; s++) {
+          u32x4 t = v[s][u];
+          if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
+          acc = fn.redPack(acc, t);
+        }
+        if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
+        stPack<POLICY>(dst0 + p + u * kBlock, acc);
+        if (two) stPack<POLICY>(dst1 + p + u * kBlock, acc);
+      }
+    } else {
+      // last, partial tile
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t q = p + (uint64_t)u * kBlock;
+        if (q < n) {
+#pragma unroll
+          for (int s = 0; s < NSRC; s++) v[s][u] = ldPack<POLICY>(src[s] + q);
+          u32x4 acc = v[0][u];
+          if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
+#pragma unroll
+          for (int s = 1; s < NSRC; s++) {
+            u32x4 t = v[s][u];
+            if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
+            acc = fn.redPack(acc, t);
+          }
+          if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
+          stPack<POLICY>(dst0 + q, acc);
+          if (two) stPack<POLICY>(dst1 + q, acc);
+        }
+      }
+    }
+  }
+
+  // head (< EPP elements before the aligned body) and tail (< EPP after it)
+  if (blockIdx.x == gridDim.x - 1) {
+    const int head = a.headElts;
+    const uint64_t tailStart = (uint64_t)head + n * EPP;
+    const int tail = (int)(a.nElts - tailStart);
+    const int t = (int)threadIdx.x;
+    if (t < head) reduceElt(fn, a, NSRC, (uint64_t)t);
+    else if (t < head + tail) reduceElt(fn, a, NSRC, tailStart + (uint64_t)(t - head));
+  }
+}
+
+// Element kernel: pointers with different alignments modulo 16.
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
+  const Fn fn(loadArg<Fn>(a));
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < a.nElts; i += stride)
+    reduceElt(fn, a, a.nSrcs, i);
+}
+
+// ---------------------------------------------------------------------------
+// Launch table for one functor.
+
+
+
+// Loads in flight per lane per tile ~ 8 x 16 B, whatever the source count.
+template <int NSRC>
+constexpr int unrollFor() { return NSRC >= 8 ? 1 : (NSRC >= 4 ? 2 : (NSRC >= 2 ? 4 : 8)); }
+
+template <class Fn, int... I>
+KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
+  KernelSet ks{};
+  const void* p0[] = {(const void*)&kReducePacks<Fn, I + 1, unrollFor<I + 1>(), 0>...};
+  const void* p1[] = {(const void*)&kReducePacks<Fn, I + 1, unrollFor<I + 1>(), 1>...};
+  int un[] = {unrollFor<I + 1>()...};
+  for (int i = 0; i < kMaxKSrcs; i++) {
+    ks.packs[0][i] = p0[i];
+    ks.packs[1][i] = p1[i];
+    ks.unroll[i] = un[i];
+  }
+  ks.elts = (const void*)&kReduceElts<Fn>;
+  ks.eltBytes = (int)sizeof(typename Fn::Elt);
+  ks.valid = 1;
+  return ks;
+}
+
+template <class Fn>
+KernelSet makeKernelSet() {
+  return makeKernelSetImpl<Fn>(std::make_integer_sequence<int, kMaxKSrcs>{});
+}
+
+}  // namespace nbx

@@ -1,0 +1,320 @@
+// nbx_reduce.cc — host side of the reduction core: argument checks, pointer
+// alignment analysis, multi-pass folding for > 8 sources, grid sizing and the
+// kernel launch. Exposes the C ABI of include/nbx_reduce.h.
+//
+// Reference behaviour mirrored:
+//   * alignment fallback — reduceCopy checks every pointer for 16-B alignment
+//     and otherwise runs sizeof(T) packs (common_kernel.h:209-238). Here the
+//     fast kernel also accepts pointers that share ONE misalignment modulo 16
+//     (peeling < 16 B of head elements), so only genuinely mixed alignments
+//     take the element kernel.
+//   * opArg: by value, or a device pointer dereferenced by the kernel
+//     (ncclScalarDevice; common.h:100-119, onerank.cu:32-42).
+//   * PreOp on sources s < nPreOpSrcs, postOp after the fold
+//     (common_kernel.h:79-137).
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/nbx_reduce.h"
+#include "nbx_registry.h"
+
+using namespace nbx;
+
+namespace {
+
+KernelTable g_table;
+std::once_flag g_tableOnce;
+
+void buildTable() {
+  std::memset(&g_table, 0, sizeof(g_table));
+  fillInt8(g_table);
+  fillInt32(g_table);
+  fillInt64(g_table);
+  fillF16(g_table);
+  fillBF16(g_table);
+  fillF32(g_table);
+  fillF64(g_table);
+  fillFp8(g_table);
+}
+
+const KernelTable& table() {
+  std::call_once(g_tableOnce, buildTable);
+  return g_table;
+}
+
+// Launch configuration (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues).
+std::atomic<int> g_maxBlocksPerCU{0};   // 0 = default
+std::atomic<int> g_policy{0};            // 0 = default cache policy, 1 = nontemporal
+
+int envInt(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cuCount[kMaxDevices];
+
+int cuCount(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return 256;
+  int c = g_cuCount[dev].load(std::memory_order_relaxed);
+  if (c > 0) return c;
+  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+  g_cuCount[dev].store(c, std::memory_order_relaxed);
+  return c;
+}
+
+int maxBlocksPerCU() {
+  int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  return envInt("NBX_BLOCKS_PER_CU", 8);
+}
+
+bool isFloatType(int dt) {
+  return dt == ncclFloat16 || dt == ncclFloat32 || dt == ncclFloat64 || dt == ncclBfloat16 ||
+         dt == ncclFloat8e4m3 || dt == ncclFloat8e5m2;
+}
+
+int typeSize(int dt) {
+  switch (dt) {
+    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return -1;
+  }
+}
+
+bool overlaps(const void* a, const void* b, size_t bytes) {
+  uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+  return x < y + bytes && y < x + bytes;
+}
+
+// One kernel pass over <= kMaxKSrcs sources.
+ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const void* const* srcs,
+                        int nSrcs, size_t count, const nbxDevRedOpFull& op, uint32_t preMask,
+                        int postOp, hipStream_t stream) {
+  KArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int s = 0; s < nSrcs; s++) a.src[s] = srcs[s];
+  for (int d = 0; d < nDsts; d++) a.dst[d] = dsts[d];
+  a.dst[1] = nDsts > 1 ? dsts[1] : dsts[0];
+  a.nElts = count;
+  a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+  a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+  a.preMask = preMask;
+  a.nSrcs = nSrcs;
+  a.nDsts = nDsts;
+  a.postOp = postOp;
+  a.policy = g_policy.load(std::memory_order_relaxed);
+
+  const int eb = ks.eltBytes;
+  const int epp = 16 / eb;
+  // shared misalignment modulo 16?
+  const unsigned mis = (unsigned)((uintptr_t)srcs[0] & 15u);
+  bool shared = true;
+  for (int s = 1; s < nSrcs; s++) shared &= (((uintptr_t)srcs[s] & 15u) == mis);
+  for (int d = 0; d < nDsts; d++) shared &= (((uintptr_t)dsts[d] & 15u) == mis);
+
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const int cus = cuCount(dev);
+  void* args[] = {&a};
+  hipError_t err;
+  if (shared) {
+    size_t head = mis ? (size_t)((16u - mis) / (unsigned)eb) : 0;
+    if (head > count) head = count;
+    const size_t nPacks = (count - head) / (size_t)epp;
+    a.headElts = (int)head;
+    a.nPacks = nPacks;
+    const int unroll = ks.unroll[nSrcs - 1];
+    const size_t tile = (size_t)unroll * kBlock;
+    size_t tiles = (nPacks + tile - 1) / tile;
+    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU();
+    size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
+    if (grid == 0) grid = 1;
+    const int pol = a.policy == 1 ? 1 : 0;
+    err = hipLaunchKernel((const void*)ks.packs[pol][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args, 0,
+                          stream);
+  } else {
+    size_t blocks = (count + kBlock - 1) / kBlock;
+    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU();
+    size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
+    err = hipLaunchKernel((const void*)ks.elts, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
+  }
+  if (err != hipSuccess) {
+    std::fprintf(stderr, "nbx: kernel launch failed: %s\n", hipGetErrorString(err));
+    return ncclUnhandledCudaError;
+  }
+  return ncclSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) ncclResult_t nbxHostToDevRedOp(nbxDevRedOpFull* out, ncclRedOp_t op,
+                                                                       ncclDataType_t datatype, int nRanks) {
+  // enqueue.cc:1436-1512 for the built-in ops.
+  if (out == nullptr) return ncclInvalidArgument;
+  const int sz = typeSize((int)datatype);
+  if (sz < 0) return ncclInvalidArgument;
+  const int nbits = 8 * sz;
+  const uint64_t allBits = ~0ull >> (64 - nbits);
+  const uint64_t signBit = allBits ^ (allBits >> 1);
+  out->scalarArgIsPtr = 0;
+  out->scalarArg = 0;
+  switch ((int)op) {
+    case ncclSum: out->op = nbxDevSum; return ncclSuccess;
+    case ncclProd: out->op = nbxDevProd; return ncclSuccess;
+    case ncclMin:
+    case ncclMax:
+      out->op = nbxDevMinMax;
+      if (datatype == ncclInt8 || datatype == ncclInt32 || datatype == ncclInt64) out->scalarArg ^= signBit;
+      out->scalarArg ^= ((int)op == ncclMax) ? allBits : 0;
+      return ncclSuccess;
+    case ncclAvg: {
+      if (nRanks < 1) return ncclInvalidArgument;
+      if (!isFloatType((int)datatype)) {
+        out->op = nbxDevSumPostDiv;
+        out->scalarArg = (uint64_t)nRanks;
+        return ncclSuccess;
+      }
+      out->op = nbxDevPreMulSum;
+      const float f = (float)(1.0 / nRanks);
+      uint32_t fb;
+      std::memcpy(&fb, &f, 4);
+      switch ((int)datatype) {
+        case ncclFloat16: {  // __float2half(float(1.0/n)) — enqueue.cc:1483
+          _Float16 h = (_Float16)f;
+          uint16_t hb;
+          std::memcpy(&hb, &h, 2);
+          out->scalarArg = hb;
+          break;
+        }
+        case ncclBfloat16: {  // __float2bfloat16(float(1.0/n)) — enqueue.cc:1488, RNE
+          uint32_t u = fb + 0x7fffu + ((fb >> 16) & 1u);
+          out->scalarArg = (uint16_t)(u >> 16);
+          break;
+        }
+        case ncclFloat32: out->scalarArg = fb; break;
+        case ncclFloat64: {
+          double d = 1.0 / nRanks;
+          std::memcpy(&out->scalarArg, &d, 8);
+          break;
+        }
+        case ncclFloat8e4m3:
+        case ncclFloat8e5m2: {
+          // this build's extension: the element type's RNE encoding of float(1/n)
+          // (e4m3fn: E=4,M=3,bias=7; e5m2: E=5,M=2,bias=15). 1/n <= 1, never overflows.
+          const bool e4 = datatype == ncclFloat8e4m3;
+          const int E = e4 ? 4 : 5, M = e4 ? 3 : 2;
+          const int bias = (1 << (E - 1)) - 1, emin = 1 - bias;
+          const int e = (int)((fb >> 23) & 0xff) - 127;
+          const int et = e < emin ? emin : e;
+          int shift = (23 - M) + (et - e);
+          if (shift > 31) shift = 31;
+          const uint32_t mant = (fb & 0x7fffffu) | 0x800000u;
+          uint32_t q = mant >> shift;
+          const uint32_t rem = mant & ((1u << shift) - 1u), half = 1u << (shift - 1);
+          if (rem > half || (rem == half && (q & 1u))) q++;
+          out->scalarArg = (uint64_t)((uint32_t)((et + bias - 1) << M) + q);
+          break;
+        }
+      }
+      return ncclSuccess;
+    }
+    default: return ncclInvalidArgument;
+  }
+}
+
+__attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
+                                                                    const void* const* srcs, int nSrcs, size_t count,
+                                                                    ncclDataType_t datatype, nbxDevRedOpFull op,
+                                                                    int nPreOpSrcs, int postOp, ncclStream_t stream) {
+  const int dt = (int)datatype;
+  if (dt < 0 || dt >= kNumTypes) return ncclInvalidArgument;
+  if (op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
+  if (nSrcs < 1 || nSrcs > NBX_MAX_SRCS || nDsts < 1 || nDsts > NBX_MAX_DSTS) return ncclInvalidArgument;
+  if (srcs == nullptr || dsts == nullptr) return ncclInvalidArgument;
+  const KernelSet& ks = table()[dt][op.op];
+  if (!ks.valid) return ncclInvalidArgument;   // e.g. SumPostDiv on floats
+  if (op.op == nbxDevSumPostDiv && !op.scalarArgIsPtr && (int)op.scalarArg == 0) return ncclInvalidArgument;
+  if (count == 0) return ncclSuccess;
+  const int eb = ks.eltBytes;
+  for (int s = 0; s < nSrcs; s++)
+    if (srcs[s] == nullptr || ((uintptr_t)srcs[s] % (uintptr_t)eb) != 0) return ncclInvalidArgument;
+  for (int d = 0; d < nDsts; d++)
+    if (dsts[d] == nullptr || ((uintptr_t)dsts[d] % (uintptr_t)eb) != 0) return ncclInvalidArgument;
+  if (op.scalarArgIsPtr && op.scalarArg == 0) return ncclInvalidArgument;
+  if (nPreOpSrcs < 0) nPreOpSrcs = 0;
+  hipStream_t st = (hipStream_t)stream;
+  const bool pre = op.op == nbxDevPreMulSum;
+  const int post = (op.op == nbxDevSumPostDiv && postOp) ? 1 : 0;
+
+  if (nSrcs <= kMaxKSrcs) {
+    uint32_t mask = 0;
+    if (pre)
+      for (int s = 0; s < nSrcs; s++)
+        if (s < nPreOpSrcs) mask |= 1u << s;
+    return launchPass(ks, dsts, nDsts, srcs, nSrcs, count, op, mask, post, st);
+  }
+
+  // > 8 sources: ordered multi-pass left fold through dsts[0]:
+  //   pass 0: dsts[0] = fold(srcs[0..8)); pass k: dsts[0] = fold(dsts[0], next <= 7 srcs).
+  // dsts[0] must not alias a source consumed in a later pass.
+  const size_t bytes = count * (size_t)eb;
+  for (int s = kMaxKSrcs; s < nSrcs; s++)
+    if (overlaps(dsts[0], srcs[s], bytes)) return ncclInvalidArgument;
+  uint32_t mask = 0;
+  if (pre)
+    for (int s = 0; s < kMaxKSrcs; s++)
+      if (s < nPreOpSrcs) mask |= 1u << s;
+  ncclResult_t r = launchPass(ks, dsts, 1, srcs, kMaxKSrcs, count, op, mask, 0, st);
+  if (r != ncclSuccess) return r;
+  int next = kMaxKSrcs;
+  while (next < nSrcs) {
+    const void* ps[kMaxKSrcs];
+    ps[0] = dsts[0];
+    int n = 1;
+    uint32_t m = 0;
+    while (n < kMaxKSrcs && next < nSrcs) {
+      if (pre && next < nPreOpSrcs) m |= 1u << n;
+      ps[n++] = srcs[next++];
+    }
+    const bool last = next >= nSrcs;
+    r = launchPass(ks, dsts, last ? nDsts : 1, ps, n, count, op, m, last ? post : 0, st);
+    if (r != ncclSuccess) return r;
+  }
+  return ncclSuccess;
+}
+
+__attribute__((visibility("default"))) ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int policy) {
+  if (blocksPerCU < 0 || blocksPerCU > 64 || policy < 0 || policy > 1) return ncclInvalidArgument;
+  g_maxBlocksPerCU.store(blocksPerCU);
+  g_policy.store(policy);
+  return ncclSuccess;
+}
+
+__attribute__((visibility("default"))) ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* policy) {
+  if (blocksPerCU) *blocksPerCU = maxBlocksPerCU();
+  if (policy) *policy = g_policy.load();
+  return ncclSuccess;
+}
+
+__attribute__((visibility("default"))) int nbxKernelCount(void) {
+  int n = 0;
+  const KernelTable& t = table();
+  for (int ty = 0; ty < kNumTypes; ty++)
+    for (int o = 0; o < kNumDevOps; o++)
+      if (t[ty][o].valid) n++;
+  return n;
+}
+
+__attribute__((visibility("default"))) int nbxAbiVersion(void) { return 1; }
+
+}  // extern "C"

@@ -1,0 +1,748 @@
+// nccl_api.cc — the NCCL-compatible C ABI (include/nccl.h) over the MI355X
+// reduction core (include/nbx_reduce.h).
+//
+// Mirrors the reference's host path for the reducing collectives:
+//   ncclAllReduce / ncclReduceScatter / ncclReduce   src/collectives.cc:29-124
+//   ncclEnqueueCheck / ArgsCheck / PtrCheck           src/enqueue.cc:1613-1646, src/misc/argcheck.cc:28-75
+//   hostToDevRedOp (op -> device op + scalar)         src/enqueue.cc:1436-1512
+//   taskAppend nRanks==1 -> ncclLaunchOneRank          src/enqueue.cc:1564-1566, src/device/onerank.cu:48-79
+//   ncclRedOpCreatePreMulSum / ncclRedOpDestroy       src/enqueue.cc:1648-1717
+//   ncclUserRedOpMangle                               src/include/comm.h:456-467
+//   ncclGetErrorString / ncclGetLastError             src/init.cc:2091-2112
+// and, for nRanks > 1 inside one process (ncclCommInitAll, init.cc:1678-1734),
+// replaces NCCL's ring schedule (all_reduce.h:13-95, reduce_scatter.h:13-66)
+// with a direct one-shot exchange over xGMI peer access: rank r's kernel reads
+// block r of every rank's send buffer (nSrcs = nRanks, the CollNet-direct
+// shape all_reduce.h:318-327), folding in ring order r+1, r+2, ..., r — the
+// order in which NCCL's ring reduce-scatter accumulates block r — then the
+// reduced blocks are gathered peer-to-peer. Cross-device ordering is by HIP
+// events (stream-ordered, asynchronous, graph-capturable), not spin flags.
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <vector>
+
+#include "../../include/nbx_reduce.h"
+
+#define NBX_EXPORT extern "C" __attribute__((visibility("default")))
+// NCCL_API (src/include/core.h:17-32): every entry point plus a p-prefixed alias.
+#define NBX_API(ret, func, ...)                                                     \
+  NBX_EXPORT ret func(__VA_ARGS__);                                                 \
+  NBX_EXPORT __attribute__((alias(#func))) ret p##func(__VA_ARGS__);                \
+  NBX_EXPORT ret func(__VA_ARGS__)
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Logging (NCCL_DEBUG=WARN|INFO, debug.cc:26-147) and last-error string.
+
+char g_lastError[1024] = "";
+std::mutex g_errMu;
+
+int debugLevel() {
+  static int lvl = [] {
+    const char* v = std::getenv("NCCL_DEBUG");
+    if (!v) return 0;
+    if (!strcasecmp(v, "VERSION")) return 1;
+    if (!strcasecmp(v, "WARN")) return 2;
+    if (!strcasecmp(v, "INFO")) return 3;
+    if (!strcasecmp(v, "TRACE")) return 4;
+    return 0;
+  }();
+  return lvl;
+}
+
+void warn(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  {
+    std::lock_guard<std::mutex> g(g_errMu);
+    std::snprintf(g_lastError, sizeof(g_lastError), "%s", buf);
+  }
+  if (debugLevel() >= 2) std::fprintf(stderr, "NCCL WARN %s\n", buf);
+}
+
+void info(const char* fmt, ...) {
+  if (debugLevel() < 3) return;
+  va_list ap;
+  va_start(ap, fmt);
+  std::fprintf(stderr, "NCCL INFO ");
+  std::vfprintf(stderr, fmt, ap);
+  std::fprintf(stderr, "\n");
+  va_end(ap);
+}
+
+#define HIPCHECK(cmd)                                                         \
+  do {                                                                        \
+    hipError_t e_ = (cmd);                                                    \
+    if (e_ != hipSuccess) {                                                   \
+      warn("HIP failure '%s' at %s:%d", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return ncclUnhandledCudaError;                                          \
+    }                                                                         \
+  } while (0)
+#define NCCLCHECK(cmd)                          \
+  do {                                          \
+    ncclResult_t r_ = (cmd);                    \
+    if (r_ != ncclSuccess) return r_;           \
+  } while (0)
+
+int typeSize(ncclDataType_t t) {
+  switch ((int)t) {
+    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Communicator.
+
+constexpr uint64_t kCommMagic = 0x4e42584343434f4dull;  // "NBXCCCOM"
+constexpr char kIdMagic[8] = {'N', 'B', 'X', 'U', 'I', 'D', '0', '1'};
+
+struct UserRedOp {   // comm.h ncclUserRedOp
+  int freeNext;      // -1 = allocated
+  ncclDataType_t datatype;
+  nbxDevRedOpFull opFull;
+};
+
+struct Clique;
+
+}  // namespace
+
+struct ncclComm {
+  uint64_t magic = kCommMagic;
+  int nRanks = 1;
+  int rank = 0;
+  int device = 0;
+  int blocking = 1;
+  bool checkPointers = false;
+  std::atomic<int> asyncError{ncclSuccess};
+  std::mutex opsMu;
+  std::vector<UserRedOp> userOps;
+  int freeHead = 0;
+  std::shared_ptr<Clique> clique;  // nRanks > 1 (single process)
+};
+
+namespace {
+
+// In-process clique (ncclCommInitAll): per-rank streams are the caller's; the
+// clique owns the events used to order the exchange across devices.
+struct Clique {
+  int n = 0;
+  std::vector<ncclComm*> comms;
+  std::vector<int> devs;
+  std::vector<hipEvent_t> evEnter, evReduced, evDone;   // one per rank
+  std::mutex mu;
+};
+
+ncclResult_t commCheck(ncclComm* comm, const char* opName) {
+  // PtrCheck(comm) — argcheck.cc:28-34
+  if (comm == nullptr) {
+    warn("%s : comm argument is NULL", opName);
+    return ncclInvalidArgument;
+  }
+  if (comm->magic != kCommMagic) {
+    warn("%s : comm %p is not a valid communicator", opName, (void*)comm);
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+// comm.h:456-467
+ncclRedOp_t userRedOpMangle(ncclComm* comm, ncclRedOp_t op) {
+  if ((int)op < (int)ncclNumOps) return op;
+  uint64_t h = reinterpret_cast<uint64_t>(comm);
+  h ^= h >> 32;
+  h *= 0x9e3779b97f4a7c13ull;
+  h >>= 32;
+  h &= (uint64_t)ncclMaxRedOp;
+  int op1 = (int)h ^ (int)op;
+  // builtin values are preserved, so their preimage is too
+  return op1 < (int)ncclNumOps ? op : (ncclRedOp_t)op1;
+}
+
+class DevGuard {
+ public:
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&old_) != hipSuccess) old_ = -1;
+    if (old_ != dev) (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    if (old_ >= 0) (void)hipSetDevice(old_);
+  }
+
+ private:
+  int old_ = -1;
+};
+
+// hostToDevRedOp — enqueue.cc:1436-1512, including the user-op branch.
+ncclResult_t hostToDevRedOp(nbxDevRedOpFull* opFull, ncclRedOp_t op, ncclDataType_t dt, ncclComm* comm) {
+  if ((int)op < (int)ncclNumOps) return nbxHostToDevRedOp(opFull, op, dt, comm->nRanks);
+  int ix = (int)userRedOpMangle(comm, op) - (int)ncclNumOps;
+  std::lock_guard<std::mutex> g(comm->opsMu);
+  if (ix < 0 || ix >= (int)comm->userOps.size() || comm->userOps[ix].freeNext != -1) {
+    warn("reduction operation %d unknown to this communicator", (int)op);
+    return ncclInvalidArgument;
+  }
+  const UserRedOp& u = comm->userOps[ix];
+  if (dt != u.datatype) {
+    warn("Data type supplied to user-created ncclRedOp_t does not match type given to reduction operation");
+    return ncclInvalidArgument;
+  }
+  *opFull = u.opFull;
+  return ncclSuccess;
+}
+
+// ArgsCheck — argcheck.cc:36-75 (pointer checks only under NCCL_CHECK_POINTERS=1,
+// as in the reference; NULL buffers with count > 0 are always rejected here).
+ncclResult_t argsCheck(ncclComm* comm, const char* opName, const void* sendbuff, const void* recvbuff,
+                       size_t count, ncclDataType_t dt, ncclRedOp_t op, int root, bool isReduce) {
+  if (root < 0 || root >= comm->nRanks) {
+    warn("%s : invalid root %d (root should be in the 0..%d range)", opName, root, comm->nRanks);
+    return ncclInvalidArgument;
+  }
+  if ((int)dt < 0 || (int)dt >= (int)ncclNumTypes) {
+    warn("%s : invalid type %d", opName, (int)dt);
+    return ncclInvalidArgument;
+  }
+  if ((int)op < 0 || (int)ncclMaxRedOp < (int)op) {
+    warn("%s : invalid reduction operation %d", opName, (int)op);
+    return ncclInvalidArgument;
+  }
+  if ((int)op >= (int)ncclNumOps) {
+    int ix = (int)userRedOpMangle(comm, op) - (int)ncclNumOps;
+    std::lock_guard<std::mutex> g(comm->opsMu);
+    if (ix < 0 || ix >= (int)comm->userOps.size() || comm->userOps[ix].freeNext != -1) {
+      warn("%s : reduction operation %d unknown to this communicator", opName, (int)op);
+      return ncclInvalidArgument;
+    }
+  }
+  if (count > 0) {
+    if (sendbuff == nullptr) {
+      warn("%s : sendbuff argument is NULL", opName);
+      return ncclInvalidArgument;
+    }
+    if (recvbuff == nullptr && (!isReduce || comm->rank == root)) {
+      warn("%s : recvbuff argument is NULL", opName);
+      return ncclInvalidArgument;
+    }
+  }
+  if (comm->checkPointers && count > 0) {
+    const void* ptrs[2] = {sendbuff, recvbuff};
+    const char* names[2] = {"sendbuff", "recvbuff"};
+    for (int i = 0; i < 2; i++) {
+      if (i == 1 && isReduce && comm->rank != root) continue;
+      hipPointerAttribute_t attr;
+      if (hipPointerGetAttributes(&attr, ptrs[i]) != hipSuccess || attr.devicePointer == nullptr) {
+        warn("%s : %s %p is not a valid pointer", opName, names[i], ptrs[i]);
+        return ncclInvalidArgument;
+      }
+      if (attr.type == hipMemoryTypeDevice && attr.device != comm->device) {
+        warn("%s : %s allocated on device %d mismatchs with NCCL device %d", opName, names[i], attr.device,
+             comm->device);
+        return ncclInvalidArgument;
+      }
+    }
+  }
+  return ncclSuccess;
+}
+
+// ncclLaunchOneRank — onerank.cu:48-79: PreMulSum -> kernel (pre-op on the one
+// source, postOp=true); every other op -> D2D copy, or nothing when in place.
+ncclResult_t launchOneRank(void* dst, const void* src, size_t count, const nbxDevRedOpFull& op,
+                           ncclDataType_t dt, hipStream_t stream) {
+  if (count == 0) return ncclSuccess;
+  if (op.op != nbxDevPreMulSum) {
+    if (dst != src) HIPCHECK(hipMemcpyAsync(dst, src, count * (size_t)typeSize(dt), hipMemcpyDeviceToDevice, stream));
+    return ncclSuccess;
+  }
+  void* dsts[1] = {dst};
+  const void* srcs[1] = {src};
+  return nbxReduceMulti(dsts, 1, srcs, 1, count, dt, op, /*nPreOpSrcs=*/1, /*postOp=*/1, (ncclStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------
+// Group semantics (group.cc:82-103 depth is thread-local). One-rank
+// collectives launch at enqueue, as in the reference (taskAppend returns after
+// ncclLaunchOneRank); in-process multi-rank collectives are queued and run
+// when every rank has enqueued its part and the outermost group ends.
+
+thread_local int t_groupDepth = 0;
+
+enum CollKind { kAllReduce, kReduceScatter, kReduce };
+
+struct PendingColl {
+  CollKind kind;
+  const void* send;
+  void* recv;
+  size_t count;   // AllReduce/Reduce: count; ReduceScatter: recvcount
+  ncclDataType_t dt;
+  nbxDevRedOpFull op;
+  int root;
+  hipStream_t stream;
+};
+
+struct CliquePending {
+  std::vector<std::vector<PendingColl>> perRank;   // FIFO per rank
+};
+
+std::mutex g_pendMu;
+std::vector<std::pair<Clique*, CliquePending>> g_pending;
+
+CliquePending& pendingFor(Clique* c) {
+  for (auto& p : g_pending)
+    if (p.first == c) return p.second;
+  g_pending.push_back({c, CliquePending{}});
+  g_pending.back().second.perRank.resize(c->n);
+  return g_pending.back().second;
+}
+
+// Element range of block b when `count` is split over n ranks, aligned so
+// every block starts on a 16-byte boundary relative to the buffer.
+void blockRange(size_t count, int eb, int n, int b, size_t* off, size_t* len) {
+  const size_t epp = (size_t)(16 / eb);
+  size_t per = (count + (size_t)n - 1) / (size_t)n;
+  per = (per + epp - 1) / epp * epp;
+  size_t lo = per * (size_t)b;
+  if (lo > count) lo = count;
+  size_t hi = lo + per;
+  if (hi > count) hi = count;
+  *off = lo;
+  *len = hi - lo;
+}
+
+// Run one collective across every rank of an in-process clique.
+ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
+  const int n = c->n;
+  const PendingColl& p0 = parts[0];
+  for (int r = 1; r < n; r++) {
+    if (parts[r].kind != p0.kind || parts[r].count != p0.count || parts[r].dt != p0.dt ||
+        parts[r].root != p0.root || parts[r].op.op != p0.op.op) {
+      warn("collective mismatch across ranks of the clique");
+      return ncclInvalidUsage;
+    }
+  }
+  const int eb = typeSize(p0.dt);
+  // 1. enter: every rank's stream reaches the collective
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    HIPCHECK(hipEventRecord(c->evEnter[r], parts[r].stream));
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    for (int j = 0; j < n; j++)
+      if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evEnter[j], 0));
+  }
+  // 2. reduce: rank r folds block r of every send buffer in ring order r+1..r
+  const size_t total = p0.kind == kReduceScatter ? p0.count * (size_t)n : p0.count;
+  const int postOp = 1;   // the fold is complete in one pass: apply SumPostDiv here
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    size_t off, len;
+    if (p0.kind == kReduceScatter) {
+      off = (size_t)r * p0.count;
+      len = p0.count;
+    } else {
+      blockRange(total, eb, n, r, &off, &len);
+    }
+    if (len == 0) continue;
+    std::vector<const void*> srcs(n);
+    for (int k = 0; k < n; k++) {
+      int j = (r + 1 + k) % n;
+      srcs[k] = (const char*)parts[j].send + off * (size_t)eb;
+    }
+    void* dst;
+    if (p0.kind == kReduceScatter) dst = parts[r].recv;
+    else if (p0.kind == kReduce) dst = (char*)parts[p0.root].recv + off * (size_t)eb;
+    else dst = (char*)parts[r].recv + off * (size_t)eb;
+    void* dsts[1] = {dst};
+    nbxDevRedOpFull op = parts[r].op;
+    NCCLCHECK(nbxReduceMulti(dsts, 1, srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n, postOp,
+                             (ncclStream_t)parts[r].stream));
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    HIPCHECK(hipEventRecord(c->evReduced[r], parts[r].stream));
+  }
+  // 3. gather (AllReduce only): rank r pulls block j from rank j's recv buffer
+  if (p0.kind == kAllReduce) {
+    for (int r = 0; r < n; r++) {
+      DevGuard g(c->devs[r]);
+      for (int j = 0; j < n; j++)
+        if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evReduced[j], 0));
+      for (int j = 0; j < n; j++) {
+        if (j == r) continue;
+        size_t off, len;
+        blockRange(total, eb, n, j, &off, &len);
+        if (len == 0) continue;
+        char* d = (char*)parts[r].recv + off * (size_t)eb;
+        const char* s = (const char*)parts[j].recv + off * (size_t)eb;
+        if (c->devs[j] == c->devs[r])
+          HIPCHECK(hipMemcpyAsync(d, s, len * (size_t)eb, hipMemcpyDeviceToDevice, parts[r].stream));
+        else
+          HIPCHECK(hipMemcpyPeerAsync(d, c->devs[r], s, c->devs[j], len * (size_t)eb, parts[r].stream));
+      }
+      HIPCHECK(hipEventRecord(c->evDone[r], parts[r].stream));
+    }
+  } else {
+    for (int r = 0; r < n; r++) {
+      DevGuard g(c->devs[r]);
+      HIPCHECK(hipEventRecord(c->evDone[r], parts[r].stream));
+    }
+  }
+  // 4. leave: no rank reuses its buffers before every peer is done with them
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    for (int j = 0; j < n; j++)
+      if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evDone[j], 0));
+  }
+  return ncclSuccess;
+}
+
+// Launch every complete collective queued for every clique (called when the
+// outermost group ends, or immediately outside a group).
+ncclResult_t flushPending() {
+  std::lock_guard<std::mutex> g(g_pendMu);
+  for (auto& cp : g_pending) {
+    Clique* c = cp.first;
+    auto& pr = cp.second.perRank;
+    for (;;) {
+      bool ready = true;
+      for (int r = 0; r < c->n; r++) ready &= !pr[r].empty();
+      if (!ready) break;
+      std::vector<PendingColl> parts(c->n);
+      for (int r = 0; r < c->n; r++) {
+        parts[r] = pr[r].front();
+        pr[r].erase(pr[r].begin());
+      }
+      NCCLCHECK(runCliqueColl(c, parts));
+    }
+  }
+  return ncclSuccess;
+}
+
+// ncclEnqueueCheck + taskAppend for the reducing collectives.
+ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff, void* recvbuff, size_t count,
+                         ncclDataType_t dt, ncclRedOp_t op, int root, ncclComm* comm, hipStream_t stream) {
+  NCCLCHECK(commCheck(comm, opName));
+  NCCLCHECK(argsCheck(comm, opName, sendbuff, recvbuff, count, dt, op, root, kind == kReduce));
+  info("%s: sendbuff %p recvbuff %p count %zu datatype %d op %d root %d comm %p [nranks=%d] stream %p", opName,
+       sendbuff, (void*)recvbuff, count, (int)dt, (int)op, root, (void*)comm, comm->nRanks, (void*)stream);
+  nbxDevRedOpFull opFull;
+  NCCLCHECK(hostToDevRedOp(&opFull, op, dt, comm));   // op state copied at enqueue (enqueue.cc:1557-1562)
+  if (comm->nRanks == 1) {
+    DevGuard g(comm->device);
+    ncclResult_t r = launchOneRank(recvbuff, sendbuff, count, opFull, dt, stream);
+    if (r != ncclSuccess) comm->asyncError.store(r);
+    return r;
+  }
+  {
+    std::lock_guard<std::mutex> g(g_pendMu);
+    CliquePending& cp = pendingFor(comm->clique.get());
+    cp.perRank[comm->rank].push_back(PendingColl{kind, sendbuff, recvbuff, count, dt, opFull, root, stream});
+  }
+  if (t_groupDepth == 0) return flushPending();
+  return ncclSuccess;
+}
+
+ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclConfig_t* config) {
+  ncclComm* c = new (std::nothrow) ncclComm();
+  if (c == nullptr) return ncclSystemError;
+  c->nRanks = nRanks;
+  c->rank = rank;
+  c->device = dev;
+  const char* cp = std::getenv("NCCL_CHECK_POINTERS");
+  c->checkPointers = cp && std::atoi(cp) != 0;
+  if (config && config->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = config->blocking;
+  *out = c;
+  return ncclSuccess;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Public C ABI
+
+NBX_API(ncclResult_t, ncclGetVersion, int* version) {
+  if (version == nullptr) return ncclInvalidArgument;
+  *version = NCCL_VERSION_CODE;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclGetUniqueId, ncclUniqueId* out) {
+  if (out == nullptr) return ncclInvalidArgument;
+  std::memset(out, 0, sizeof(*out));
+  std::memcpy(out->internal, kIdMagic, sizeof(kIdMagic));
+  std::random_device rd;
+  uint64_t key = ((uint64_t)rd() << 32) ^ rd();
+  std::memcpy(out->internal + 8, &key, sizeof(key));
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank,
+        ncclConfig_t* config) {
+  if (newcomm == nullptr) return ncclInvalidArgument;
+  if (nranks < 1 || myrank < 0 || myrank >= nranks) {
+    warn("Invalid rank requested : %d/%d", myrank, nranks);
+    return ncclInvalidArgument;
+  }
+  if (config && (config->magic != 0xcafebeef || config->size != sizeof(ncclConfig_t))) {
+    warn("ncclCommInitRankConfig : config is not initialized with NCCL_CONFIG_INITIALIZER");
+    return ncclInvalidArgument;
+  }
+  if (std::memcmp(commId.internal, kIdMagic, sizeof(kIdMagic)) != 0) {
+    warn("ncclCommInitRank : unique id was not produced by ncclGetUniqueId");
+    return ncclInvalidArgument;
+  }
+  if (nranks > 1) {
+    // Multi-process bootstrap (bootstrap.cc) is not part of this build's hot path;
+    // multi-rank communicators come from ncclCommInitAll (single process).
+    warn("ncclCommInitRank : nranks > 1 across processes is not supported; use ncclCommInitAll");
+    return ncclInvalidUsage;
+  }
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  return newComm(newcomm, 1, 0, dev, config);
+}
+
+NBX_API(ncclResult_t, ncclCommInitRank, ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
+  return ncclCommInitRankConfig(newcomm, nranks, commId, myrank, nullptr);
+}
+
+NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* devlist) {
+  // init.cc:1678-1734. Several ranks may share one device (emulation / testing).
+  if (comms == nullptr || ndev < 1) {
+    warn("ncclCommInitAll : invalid arguments");
+    return ncclInvalidArgument;
+  }
+  int nDevices = 0;
+  HIPCHECK(hipGetDeviceCount(&nDevices));
+  std::vector<int> devs(ndev);
+  for (int i = 0; i < ndev; i++) {
+    devs[i] = devlist ? devlist[i] : i;
+    if (devs[i] < 0 || devs[i] >= nDevices) {
+      warn("ncclCommInitAll : invalid device %d", devs[i]);
+      return ncclInvalidArgument;
+    }
+  }
+  if (ndev == 1) {
+    DevGuard g(devs[0]);
+    return newComm(&comms[0], 1, 0, devs[0], nullptr);
+  }
+  auto clique = std::make_shared<Clique>();
+  clique->n = ndev;
+  clique->devs = devs;
+  clique->evEnter.resize(ndev);
+  clique->evReduced.resize(ndev);
+  clique->evDone.resize(ndev);
+  for (int r = 0; r < ndev; r++) {
+    DevGuard g(devs[r]);
+    for (int j = 0; j < ndev; j++) {
+      if (devs[j] == devs[r]) continue;
+      int can = 0;
+      HIPCHECK(hipDeviceCanAccessPeer(&can, devs[r], devs[j]));
+      if (!can) {
+        warn("ncclCommInitAll : device %d cannot access peer %d", devs[r], devs[j]);
+        return ncclUnhandledCudaError;
+      }
+      hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+      (void)hipGetLastError();
+    }
+    HIPCHECK(hipEventCreateWithFlags(&clique->evEnter[r], hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&clique->evReduced[r], hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&clique->evDone[r], hipEventDisableTiming));
+  }
+  for (int r = 0; r < ndev; r++) {
+    NCCLCHECK(newComm(&comms[r], ndev, r, devs[r], nullptr));
+    comms[r]->clique = clique;
+  }
+  clique->comms.assign(comms, comms + ndev);
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommFinalize, ncclComm_t comm) {
+  NCCLCHECK(commCheck(comm, "ncclCommFinalize"));
+  return flushPending();
+}
+
+static ncclResult_t commFree(ncclComm* comm) {
+  std::shared_ptr<Clique> c = comm->clique;
+  comm->magic = 0;
+  if (c) {
+    std::lock_guard<std::mutex> g(c->mu);
+    int r = comm->rank;
+    if (r >= 0 && r < c->n) {
+      c->comms[r] = nullptr;
+      DevGuard dg(c->devs[r]);
+      (void)hipEventDestroy(c->evEnter[r]);
+      (void)hipEventDestroy(c->evReduced[r]);
+      (void)hipEventDestroy(c->evDone[r]);
+    }
+  }
+  delete comm;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommDestroy, ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;   // init.cc: NULL comm is a no-op
+  NCCLCHECK(commCheck(comm, "ncclCommDestroy"));
+  return commFree(comm);
+}
+
+NBX_API(ncclResult_t, ncclCommAbort, ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;
+  NCCLCHECK(commCheck(comm, "ncclCommAbort"));
+  return commFree(comm);
+}
+
+NBX_API(const char*, ncclGetErrorString, ncclResult_t code) {
+  switch (code) {   // init.cc:2091-2104
+    case ncclSuccess: return "no error";
+    case ncclUnhandledCudaError: return "unhandled cuda error (run with NCCL_DEBUG=INFO for details)";
+    case ncclSystemError: return "unhandled system error (run with NCCL_DEBUG=INFO for details)";
+    case ncclInternalError: return "internal error - please report this issue to the NCCL developers";
+    case ncclInvalidArgument: return "invalid argument (run with NCCL_DEBUG=WARN for details)";
+    case ncclInvalidUsage: return "invalid usage (run with NCCL_DEBUG=WARN for details)";
+    case ncclRemoteError: return "remote process exited or there was a network error";
+    case ncclInProgress: return "NCCL operation in progress";
+    default: return "unknown result code";
+  }
+}
+
+NBX_API(const char*, ncclGetLastError, ncclComm_t comm) {
+  (void)comm;
+  return g_lastError;
+}
+
+NBX_API(ncclResult_t, ncclCommGetAsyncError, ncclComm_t comm, ncclResult_t* asyncError) {
+  NCCLCHECK(commCheck(comm, "ncclGetAsyncError"));
+  if (asyncError == nullptr) return ncclInvalidArgument;
+  *asyncError = (ncclResult_t)comm->asyncError.load();
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommCount, const ncclComm_t comm, int* count) {
+  NCCLCHECK(commCheck(comm, "CommCount"));
+  if (count == nullptr) return ncclInvalidArgument;
+  *count = comm->nRanks;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommCuDevice, const ncclComm_t comm, int* devid) {
+  NCCLCHECK(commCheck(comm, "CommCuDevice"));
+  if (devid == nullptr) return ncclInvalidArgument;
+  *devid = comm->device;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommUserRank, const ncclComm_t comm, int* rank) {
+  NCCLCHECK(commCheck(comm, "CommUserRank"));
+  if (rank == nullptr) return ncclInvalidArgument;
+  *rank = comm->rank;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclRedOpCreatePreMulSum, ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,
+        ncclScalarResidence_t residence, ncclComm_t comm) {
+  // enqueue.cc:1648-1685
+  NCCLCHECK(commCheck(comm, "ncclRedOpCreatePreMulSum"));
+  if (op == nullptr || scalar == nullptr) return ncclInvalidArgument;
+  const int sz = typeSize(datatype);
+  if (sz < 0) return ncclInvalidArgument;
+  std::lock_guard<std::mutex> g(comm->opsMu);
+  if (comm->freeHead == (int)comm->userOps.size()) {
+    int cap = 2 * (int)comm->userOps.size();
+    if (cap < 4) cap = 4;
+    int old = (int)comm->userOps.size();
+    comm->userOps.resize(cap);
+    for (int ix = old; ix < cap; ix++) comm->userOps[ix].freeNext = ix + 1;
+  }
+  int ix = comm->freeHead;
+  UserRedOp& u = comm->userOps[ix];
+  comm->freeHead = u.freeNext;
+  u.freeNext = -1;
+  u.datatype = datatype;
+  u.opFull.op = nbxDevPreMulSum;
+  if (residence == ncclScalarHostImmediate) {
+    u.opFull.scalarArgIsPtr = 0;
+    u.opFull.scalarArg = 0;
+    std::memcpy(&u.opFull.scalarArg, scalar, (size_t)sz);
+  } else {
+    u.opFull.scalarArgIsPtr = 1;
+    u.opFull.scalarArg = reinterpret_cast<uint64_t>(scalar);
+  }
+  *op = userRedOpMangle(comm, (ncclRedOp_t)((int)ncclNumOps + ix));
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclRedOpDestroy, ncclRedOp_t op, ncclComm_t comm) {
+  // enqueue.cc:1687-1717
+  if (0 <= (int)op && (int)op < (int)ncclNumOps) {
+    warn("ncclRedOpDestroy : operator is a NCCL builtin.");
+    return ncclInvalidArgument;
+  }
+  if ((int)op < 0 || (int)ncclMaxRedOp < (int)op) {
+    warn("ncclRedOpDestroy :  operator is garbage.");
+    return ncclInvalidArgument;
+  }
+  if (comm == nullptr) {
+    warn("ncclRedOpDestroy : invalid communicator passed.");
+    return ncclInvalidArgument;
+  }
+  NCCLCHECK(commCheck(comm, "ncclRedOpDestroy"));
+  int ix = (int)userRedOpMangle(comm, op) - (int)ncclNumOps;
+  std::lock_guard<std::mutex> g(comm->opsMu);
+  if (ix < 0 || ix >= (int)comm->userOps.size() || comm->userOps[ix].freeNext != -1) {
+    warn("ncclRedOpDestroy : operator unknown to this communicator.");
+    return ncclInvalidArgument;
+  }
+  comm->userOps[ix].freeNext = comm->freeHead;
+  comm->freeHead = ix;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclAllReduce, const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+        ncclRedOp_t op, ncclComm_t comm, ncclStream_t stream) {
+  return enqueueColl(kAllReduce, "AllReduce", sendbuff, recvbuff, count, datatype, op, 0, comm,
+                     (hipStream_t)stream);
+}
+
+NBX_API(ncclResult_t, ncclReduceScatter, const void* sendbuff, void* recvbuff, size_t recvcount,
+        ncclDataType_t datatype, ncclRedOp_t op, ncclComm_t comm, ncclStream_t stream) {
+  return enqueueColl(kReduceScatter, "ReduceScatter", sendbuff, recvbuff, recvcount, datatype, op, 0, comm,
+                     (hipStream_t)stream);
+}
+
+NBX_API(ncclResult_t, ncclReduce, const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+        ncclRedOp_t op, int root, ncclComm_t comm, ncclStream_t stream) {
+  return enqueueColl(kReduce, "Reduce", sendbuff, recvbuff, count, datatype, op, root, comm,
+                     (hipStream_t)stream);
+}
+
+NBX_API(ncclResult_t, ncclGroupStart) {
+  t_groupDepth++;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclGroupEnd) {
+  if (t_groupDepth == 0) {
+    warn("ncclGroupEnd: not in a group call.");
+    return ncclInvalidUsage;
+  }
+  if (--t_groupDepth > 0) return ncclSuccess;
+  return flushPending();
+}
