@@ -74,10 +74,10 @@ ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
 
 /* Launch knobs (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues, tuning.cc:12,
  * connect.cc:314): blocksPerCU caps the grid at CUs x blocksPerCU workgroups
- * (0 = default 8, env NBX_BLOCKS_PER_CU); policy 0 = default cache policy,
- * 1 = nontemporal loads/stores. */
-ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int policy);
-ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* policy);
+ * (0 = default: 1 for big tiles, 8 for small; env NBX_BLOCKS_PER_CU);
+ * variant 0 = auto tile choice, 1 = force small tiles, 2 = force big tiles. */
+ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int variant);
+ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* variant);
 
 /* Number of (datatype, device op) kernel sets compiled in (for the ABI test). */
 int nbxKernelCount(void);

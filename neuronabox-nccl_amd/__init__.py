@@ -231,8 +231,8 @@ def host_to_dev_redop(op: int, dtype: int, nranks: int) -> DevRedOpFull:
     return out
 
 
-def set_launch_config(blocks_per_cu: int = 0, policy: int = 0) -> None:
-    _check(load_library().nbxSetLaunchConfig(int(blocks_per_cu), int(policy)), "nbxSetLaunchConfig")
+def set_launch_config(blocks_per_cu: int = 0, variant: int = 0) -> None:
+    _check(load_library().nbxSetLaunchConfig(int(blocks_per_cu), int(variant)), "nbxSetLaunchConfig")
 
 
 def get_launch_config() -> tuple:

@@ -14,8 +14,12 @@
 // is innocuous and every op is correctly rounded):
 //   f16  : native v_add_f16 / v_mul_f16 (RNE), packed by the compiler.
 //   bf16 : widen (shift), fp32 op, v_cvt_pk_bf16_f32 (RNE, NaN stays NaN).
-//   fp8  : v_cvt_pk_f32_{fp8,bf8} widen, fp32 op, RNE narrow (software, see
-//          fp8 note below). Not in the reference: this build's definition.
+//   fp8  : v_cvt_pk_f32_{fp8,bf8} widen, fp32 op, v_cvt_pk_{fp8,bf8}_f32 narrow
+//          (RNE; overflow -> NaN for e4m3fn, -> inf for e5m2). The hardware
+//          narrowing was checked equal to the software definition f32ToSmall
+//          on all 2^32 fp32 inputs (scripts/probe_fp8_cvt.hip,
+//          profiles/r1/probe_fp8_cvt.txt). Not in the reference: this build's
+//          definition.
 //   f32/f64 : native IEEE ops; denormals preserved (.amdhsa_float_denorm_mode 3);
 //          build with -ffp-contract=off so x*s + acc is never fused.
 //   min/max (floats): NaN operand yields the other operand, ties return the
@@ -62,10 +66,10 @@ struct TyBF16 {
   __device__ static Elt narrow(C c) { return __builtin_bit_cast(uint16_t, (__bf16)c); }
 };
 
-// fp8 narrowing. OCP e4m3fn / e5m2, round-to-nearest-even, overflow -> NaN
-// (e4m3fn, which has no infinity) / -> +-inf (e5m2). Written in integer ops
-// on the fp32 bits so the result does not depend on the hardware converter's
-// clamp/saturation mode; widening uses the exact hardware converter.
+// fp8 narrowing, specification form: OCP e4m3fn / e5m2, round-to-nearest-even,
+// overflow -> NaN (e4m3fn, which has no infinity) / -> +-inf (e5m2). Kernels
+// use the hardware converter, which equals this function bit for bit (up to
+// the NaN code) on every fp32 input; kept as the executable specification.
 template <int E, int M, bool FN>
 __device__ __forceinline__ uint32_t f32ToSmall(float x) {
   const uint32_t u = __float_as_uint(x);
@@ -97,7 +101,12 @@ __device__ __forceinline__ uint32_t f32ToSmall(float x) {
 struct TyE4M3 {
   using Elt = uint8_t; using C = float;
   __device__ static C wide(Elt e) { return __builtin_amdgcn_cvt_pk_f32_fp8((int)e, false)[0]; }
-  __device__ static Elt narrow(C c) { return (Elt)f32ToSmall<4, 3, true>(c); }
+  __device__ static Elt narrow(C c) { return (Elt)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xff); }
+  // two results into bytes {0,1} (hi = false) or {2,3} (hi = true) of `old`
+  __device__ static uint32_t narrow2(float x, float y, uint32_t old, bool hi) {
+    return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x, y, (int)old, true)
+              : (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x, y, (int)old, false);
+  }
   // 4 codes in a dword <-> 4 floats
   __device__ static void wide4(uint32_t w, float (&f)[4]) {
     auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
@@ -108,7 +117,11 @@ struct TyE4M3 {
 struct TyE5M2 {
   using Elt = uint8_t; using C = float;
   __device__ static C wide(Elt e) { return __builtin_amdgcn_cvt_pk_f32_bf8((int)e, false)[0]; }
-  __device__ static Elt narrow(C c) { return (Elt)f32ToSmall<5, 2, false>(c); }
+  __device__ static Elt narrow(C c) { return (Elt)(__builtin_amdgcn_cvt_pk_bf8_f32(c, c, 0, false) & 0xff); }
+  __device__ static uint32_t narrow2(float x, float y, uint32_t old, bool hi) {
+    return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(x, y, (int)old, true)
+              : (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(x, y, (int)old, false);
+  }
   __device__ static void wide4(uint32_t w, float (&f)[4]) {
     auto lo = __builtin_amdgcn_cvt_pk_f32_bf8((int)w, false);
     auto hi = __builtin_amdgcn_cvt_pk_f32_bf8((int)w, true);
@@ -156,6 +169,9 @@ struct FnBase {
   using Elt = E;
   static constexpr bool kHasPre = false;
   static constexpr bool kHasPost = false;
+  // cap on the big-tile unroll: VALU-heavy functors gain nothing from more
+  // loads in flight and only grow code size
+  static constexpr int kUnrollCap = 16;
   __device__ E pre(E a) const { return a; }
   __device__ E post(E a) const { return a; }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const { return packRed(*static_cast<const D*>(this), a, b); }
@@ -188,12 +204,14 @@ struct FnSumInt : FnBase<FnSumInt<E>, E> {
 
 template <class E>
 struct FnProdInt : FnBase<FnProdInt<E>, E> {
+  static constexpr int kUnrollCap = sizeof(E) == 1 ? 4 : 16;
   __device__ explicit FnProdInt(uint64_t) {}
   __device__ E red(E a, E b) const { return (E)(a * b); }
 };
 
 template <class E>
 struct FnMinMaxInt : FnBase<FnMinMaxInt<E>, E> {
+  static constexpr int kUnrollCap = sizeof(E) == 1 ? 4 : 16;
   E xormask;  // reduce_kernel.h:43-46
   __device__ explicit FnMinMaxInt(uint64_t arg) : xormask((E)arg) {}
   __device__ E red(E a, E b) const { return ((E)(a ^ xormask) < (E)(b ^ xormask)) ? a : b; }
@@ -248,6 +266,7 @@ struct FnProdF : FnBase<FnProdF<Ty>, typename Ty::Elt> {
 };
 template <class Ty>
 struct FnMinMaxF : FnBase<FnMinMaxF<Ty>, typename Ty::Elt> {
+  static constexpr int kUnrollCap = sizeof(typename Ty::Elt) == 1 ? 4 : 16;
   using E = typename Ty::Elt;
   bool isMin;  // reduce_kernel.h:47: (opArg & 1) == 0
   __device__ explicit FnMinMaxF(uint64_t arg) : isMin((arg & 1ull) == 0ull) {}
@@ -278,16 +297,15 @@ __device__ __forceinline__ u32x4 fp8PackMap2(u32x4 a, u32x4 b, Op op) {
     float fa[4], fb[4];
     Ty::wide4(a[w], fa);
     Ty::wide4(b[w], fb);
-    uint32_t o = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) o |= (uint32_t)Ty::narrow(op(fa[k], fb[k])) << (8 * k);
-    r[w] = o;
+    uint32_t o = Ty::narrow2(op(fa[0], fb[0]), op(fa[1], fb[1]), 0u, false);
+    r[w] = Ty::narrow2(op(fa[2], fb[2]), op(fa[3], fb[3]), o, true);
   }
   return r;
 }
 
 template <class Ty>
 struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
+  static constexpr int kUnrollCap = 4;
   __device__ explicit FnSumF8(uint64_t) {}
   __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
@@ -296,6 +314,7 @@ struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
 };
 template <class Ty>
 struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
+  static constexpr int kUnrollCap = 4;
   __device__ explicit FnProdF8(uint64_t) {}
   __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) * Ty::wide(b)); }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
@@ -304,6 +323,7 @@ struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
 };
 template <class Ty>
 struct FnPreMulSumF8 : FnBase<FnPreMulSumF8<Ty>, uint8_t> {
+  static constexpr int kUnrollCap = 4;
   static constexpr bool kHasPre = true;
   float scalar;
   __device__ explicit FnPreMulSumF8(uint64_t arg) : scalar(Ty::wide((uint8_t)arg)) {}

@@ -21,15 +21,15 @@ struct KArgs {
   int32_t nDsts;
   int32_t postOp;
   int32_t headElts;   // elements before the 16-B aligned body
-  int32_t policy;     // cache policy (0 = default, 1 = nontemporal)
+  int32_t variant;    // 0 = small tile (U = 1), 1 = big tile
 };
 
 // Launch table for one functor (kernel entry points as host handles).
 
 struct KernelSet {
-  const void* packs[2][kMaxKSrcs];  // [policy][nSrcs-1]
+  const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
-  int unroll[kMaxKSrcs];         // packs per lane per source per tile
+  int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;
   int valid;
 };

@@ -37,16 +37,12 @@ __device__ __forceinline__ uint64_t loadArg(const KArgs& a) {
   return a.arg;
 }
 
-template <int POLICY>
-__device__ __forceinline__ u32x4 ldPack(const u32x4* p) {
-  if constexpr (POLICY == 1) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-template <int POLICY>
-__device__ __forceinline__ void stPack(u32x4* p, u32x4 v) {
-  if constexpr (POLICY == 1) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
+// Streaming loads carry the nontemporal hint (global_load_dwordx4 ... nt):
+// measured on MI355X (scripts/sweep_variants.hip, profiles/) the 8:1
+// read:write fold runs ~20 % faster with nt loads, while nt STORES cost
+// ~7 % (write-only ceiling 6.8 TB/s plain vs 5.3 TB/s nt), so stores stay plain.
+__device__ __forceinline__ u32x4 ldPack(const u32x4* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void stPack(u32x4* p, u32x4 v) { *p = v; }
 
 // One element, any source count <= kMaxKSrcs (unrolled with a uniform guard
 // so the kernel-argument pointer array is never indexed dynamically).
@@ -68,7 +64,7 @@ __device__ __forceinline__ void reduceElt(const Fn& fn, const KArgs& a, int nSrc
   if (a.nDsts > 1) ((E*)a.dst[1])[i] = acc;
 }
 
-template <class Fn, int NSRC, int U, int POLICY>
+template <class Fn, int NSRC, int U>
 __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
@@ -93,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
 #pragma unroll
       for (int s = 0; s < NSRC; s++)
 #pragma unroll
-        for (int u = 0; u < U; u++) v[s][u] = ldPack<POLICY>(src[s] + p + u * kBlock);
+        for (int u = 0; u < U; u++) v[s][u] = ldPack(src[s] + p + u * kBlock);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         u32x4 acc = v[0][u];
@@ -105,8 +101,8 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
           acc = fn.redPack(acc, t);
         }
         if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
-        stPack<POLICY>(dst0 + p + u * kBlock, acc);
-        if (two) stPack<POLICY>(dst1 + p + u * kBlock, acc);
+        stPack(dst0 + p + u * kBlock, acc);
+        if (two) stPack(dst1 + p + u * kBlock, acc);
       }
     } else {
       // last, partial tile
@@ -115,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
         const uint64_t q = p + (uint64_t)u * kBlock;
         if (q < n) {
 #pragma unroll
-          for (int s = 0; s < NSRC; s++) v[s][u] = ldPack<POLICY>(src[s] + q);
+          for (int s = 0; s < NSRC; s++) v[s][u] = ldPack(src[s] + q);
           u32x4 acc = v[0][u];
           if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
 #pragma unroll
@@ -125,8 +121,8 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
             acc = fn.redPack(acc, t);
           }
           if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
-          stPack<POLICY>(dst0 + q, acc);
-          if (two) stPack<POLICY>(dst1 + q, acc);
+          stPack(dst0 + q, acc);
+          if (two) stPack(dst1 + q, acc);
         }
       }
     }
@@ -157,19 +153,25 @@ __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
 
 
 
-// Loads in flight per lane per tile ~ 8 x 16 B, whatever the source count.
-template <int NSRC>
-constexpr int unrollFor() { return NSRC >= 8 ? 1 : (NSRC >= 4 ? 2 : (NSRC >= 2 ? 4 : 8)); }
+// Two tile shapes per source count. BIG keeps ~32 dwordx4 loads (512 B) in
+// flight per lane and runs one 256-thread workgroup per CU (the best 8:1
+// shape measured: 6.1-6.2 TB/s); SMALL (U = 1) gives small buckets enough
+// workgroups to cover 256 CUs.
+template <int NSRC, int CAP>
+constexpr int bigUnroll() {
+  constexpr int u = NSRC >= 5 ? 4 : (NSRC >= 3 ? 8 : 16);
+  return u < CAP ? u : CAP;
+}
 
 template <class Fn, int... I>
 KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   KernelSet ks{};
-  const void* p0[] = {(const void*)&kReducePacks<Fn, I + 1, unrollFor<I + 1>(), 0>...};
-  const void* p1[] = {(const void*)&kReducePacks<Fn, I + 1, unrollFor<I + 1>(), 1>...};
-  int un[] = {unrollFor<I + 1>()...};
+  const void* big[] = {(const void*)&kReducePacks<Fn, I + 1, bigUnroll<I + 1, Fn::kUnrollCap>()>...};
+  const void* small[] = {(const void*)&kReducePacks<Fn, I + 1, 1>...};
+  int un[] = {bigUnroll<I + 1, Fn::kUnrollCap>()...};
   for (int i = 0; i < kMaxKSrcs; i++) {
-    ks.packs[0][i] = p0[i];
-    ks.packs[1][i] = p1[i];
+    ks.packs[0][i] = small[i];
+    ks.packs[1][i] = big[i];
     ks.unroll[i] = un[i];
   }
   ks.elts = (const void*)&kReduceElts<Fn>;

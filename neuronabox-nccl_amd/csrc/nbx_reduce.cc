@@ -48,8 +48,8 @@ const KernelTable& table() {
 }
 
 // Launch configuration (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues).
-std::atomic<int> g_maxBlocksPerCU{0};   // 0 = default
-std::atomic<int> g_policy{0};            // 0 = default cache policy, 1 = nontemporal
+std::atomic<int> g_maxBlocksPerCU{0};   // 0 = default per variant
+std::atomic<int> g_variant{0};          // 0 = auto, 1 = force small tile, 2 = force big tile
 
 int envInt(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -68,10 +68,18 @@ int cuCount(int dev) {
   return c;
 }
 
-int maxBlocksPerCU() {
+// Workgroups per CU: big tiles keep ~32 dwordx4 loads in flight per lane
+// slot — one 256-thread workgroup per CU (4 waves, ~128 KiB in flight per CU)
+// when nSrcs x U >= 32, proportionally more when the unroll is capped; small
+// tiles up to 8.
+int maxBlocksPerCU(bool big, int loadsPerLane) {
   int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
   if (v > 0) return v;
-  return envInt("NBX_BLOCKS_PER_CU", 8);
+  static const int envBig = envInt("NBX_BLOCKS_PER_CU", 0);
+  if (envBig > 0) return envBig;
+  if (!big) return 8;
+  int b = (32 + loadsPerLane - 1) / loadsPerLane;
+  return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
 
 bool isFloatType(int dt) {
@@ -110,7 +118,6 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
   a.nSrcs = nSrcs;
   a.nDsts = nDsts;
   a.postOp = postOp;
-  a.policy = g_policy.load(std::memory_order_relaxed);
 
   const int eb = ks.eltBytes;
   const int epp = 16 / eb;
@@ -131,18 +138,22 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     const size_t nPacks = (count - head) / (size_t)epp;
     a.headElts = (int)head;
     a.nPacks = nPacks;
-    const int unroll = ks.unroll[nSrcs - 1];
-    const size_t tile = (size_t)unroll * kBlock;
-    size_t tiles = (nPacks + tile - 1) / tile;
-    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU();
+    // big tiles once every CU gets at least one; small tiles below that
+    const size_t bigTile = (size_t)ks.unroll[nSrcs - 1] * kBlock;
+    const size_t bigTiles = (nPacks + bigTile - 1) / bigTile;
+    const int force = g_variant.load(std::memory_order_relaxed);
+    const bool big = force == 2 || (force == 0 && bigTiles >= (size_t)cus);
+    const size_t tile = big ? bigTile : (size_t)kBlock;
+    const size_t tiles = (nPacks + tile - 1) / tile;
+    const size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(big, nSrcs * (big ? ks.unroll[nSrcs - 1] : 1));
     size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
     if (grid == 0) grid = 1;
-    const int pol = a.policy == 1 ? 1 : 0;
-    err = hipLaunchKernel((const void*)ks.packs[pol][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args, 0,
-                          stream);
+    a.variant = big ? 1 : 0;
+    err = hipLaunchKernel((const void*)ks.packs[big ? 1 : 0][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args,
+                          0, stream);
   } else {
     size_t blocks = (count + kBlock - 1) / kBlock;
-    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU();
+    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs);
     size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
     err = hipLaunchKernel((const void*)ks.elts, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
   }
@@ -293,16 +304,16 @@ __attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* 
   return ncclSuccess;
 }
 
-__attribute__((visibility("default"))) ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int policy) {
-  if (blocksPerCU < 0 || blocksPerCU > 64 || policy < 0 || policy > 1) return ncclInvalidArgument;
+__attribute__((visibility("default"))) ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int variant) {
+  if (blocksPerCU < 0 || blocksPerCU > 64 || variant < 0 || variant > 2) return ncclInvalidArgument;
   g_maxBlocksPerCU.store(blocksPerCU);
-  g_policy.store(policy);
+  g_variant.store(variant);
   return ncclSuccess;
 }
 
-__attribute__((visibility("default"))) ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* policy) {
-  if (blocksPerCU) *blocksPerCU = maxBlocksPerCU();
-  if (policy) *policy = g_policy.load();
+__attribute__((visibility("default"))) ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* variant) {
+  if (blocksPerCU) *blocksPerCU = g_maxBlocksPerCU.load();
+  if (variant) *variant = g_variant.load();
   return ncclSuccess;
 }
 

@@ -35,4 +35,5 @@ if [ "${SKIP_PROF:-0}" != "1" ]; then
     python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_write_bench.json" 2> "$OUT/pmc_write.err"
   stop_if_fatal $? pmc_write
 fi
+python3 "$ROOT/scripts/pmc_traffic.py" "$OUT" "$OUT/summary" > "$OUT/pmc_summary.json" 2>&1 || true
 echo done | tee -a "$OUT/steps.log"

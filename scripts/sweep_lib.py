@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Measurements through the product C ABI (libnbxccl.so), one process, on the
+GPU box. Not the bench: feeds DESIGN.md and the launch-default choice.
+
+  knobs   config B (8 x 256 MiB fp32 sum) under launch settings, interleaved rounds
+  sweep   config C: fp16 / bf16 (and fp32, fp8) sum, nSrcs in {2, 8}, 1..64 MiB per input
+  e2e     host-staged path: pinned host -> hipMemcpy H2D -> reduce -> D2H (BASELINE asks for it)
+  small   latency of small buckets (4 KiB .. 1 MiB), nSrcs 2
+
+Prints one JSON object per line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def gbps(nbytes, ms):
+    return nbytes / (ms * 1e-3) / 1e9
+
+
+def timed(torch, fn, iters, warm=2):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="knobs,sweep,e2e,small")
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from __graft_entry__ import _load_package
+    nbx = _load_package()
+    nbx.load_library()
+    torch.cuda.set_device(0)
+    st = torch.cuda.current_stream().cuda_stream
+    what = set(args.what.split(","))
+
+    def op_for(dt):
+        return nbx.host_to_dev_redop(0, dt, 1)
+
+    if "knobs" in what:
+        n = 64 << 20
+        srcs = [torch.rand(n, device="cuda") for _ in range(8)]
+        out = torch.empty(n, device="cuda")
+        sp = [t.data_ptr() for t in srcs]
+        op = op_for(7)
+        settings = [(0, 0), (1, 2), (2, 2), (4, 2), (8, 1), (4, 1), (16, 1)]
+        res = {s: [] for s in settings}
+        for _ in range(args.rounds):
+            for s in settings:
+                nbx.set_launch_config(*s)
+                res[s].append(timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, 7, op, 0, False, st), 10))
+        nbx.set_launch_config(0, 0)
+        for s, v in res.items():
+            v.sort()
+            print(json.dumps({"what": "knobs", "blocks_per_cu": s[0], "variant": s[1], "med_ms": round(v[len(v) // 2], 4),
+                              "GBps": round(gbps(9 * n * 4, v[len(v) // 2]), 1)}), flush=True)
+        del srcs, out
+
+    if "sweep" in what:
+        for dt, name, tdt in ((6, "fp16", torch.float16), (9, "bf16", torch.bfloat16), (7, "fp32", torch.float32),
+                              (10, "fp8e4m3", torch.uint8)):
+            for nsrc in (2, 8):
+                for mib in (1, 2, 4, 8, 16, 32, 64):
+                    esz = torch.tensor([], dtype=tdt).element_size()
+                    n = (mib << 20) // esz
+                    if tdt == torch.uint8:
+                        srcs = [torch.randint(0, 120, (n,), dtype=torch.uint8, device="cuda") for _ in range(nsrc)]
+                    else:
+                        srcs = [torch.rand(n, device="cuda").to(tdt) for _ in range(nsrc)]
+                    out = torch.empty_like(srcs[0])
+                    sp = [t.data_ptr() for t in srcs]
+                    op = op_for(dt)
+                    iters = max(5, min(200, (256 << 20) // (mib << 20) * 4))
+                    ms = timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, dt, op, 0, False, st), iters)
+                    print(json.dumps({"what": "sweep", "dtype": name, "nsrc": nsrc, "MiB_per_input": mib,
+                                      "ms": round(ms, 5), "GBps": round(gbps((nsrc + 1) * n * esz, ms), 1)}),
+                          flush=True)
+                    del srcs, out
+
+    if "e2e" in what:
+        # host-staged: sources start in pinned host memory (the proxy/net staging
+        # buffers), result returns to pinned host memory
+        for nsrc, mib in ((2, 4), (8, 256), (2, 256)):
+            n = (mib << 20) // 4
+            hs = [torch.rand(n).pin_memory() for _ in range(nsrc)]
+            ho = torch.empty(n).pin_memory()
+            ds = [torch.empty(n, device="cuda") for _ in range(nsrc)]
+            do = torch.empty(n, device="cuda")
+            sp = [t.data_ptr() for t in ds]
+            op = op_for(7)
+
+            def run():
+                for h, d in zip(hs, ds):
+                    d.copy_(h, non_blocking=True)
+                nbx.reduce_multi([do.data_ptr()], sp, n, 7, op, 0, False, st)
+                ho.copy_(do, non_blocking=True)
+
+            ms = timed(torch, run, 5 if mib > 16 else 20)
+            kms = timed(torch, lambda: nbx.reduce_multi([do.data_ptr()], sp, n, 7, op, 0, False, st), 10)
+            alg = (nsrc + 1) * n * 4
+            print(json.dumps({"what": "e2e", "nsrc": nsrc, "MiB_per_input": mib, "e2e_ms": round(ms, 4),
+                              "e2e_alg_GBps": round(gbps(alg, ms), 1), "kernel_ms": round(kms, 4),
+                              "kernel_GBps": round(gbps(alg, kms), 1),
+                              "pcie_bytes": alg}), flush=True)
+            del hs, ho, ds, do
+
+    if "small" in what:
+        for kib in (4, 16, 64, 256, 1024):
+            n = (kib << 10) // 4
+            srcs = [torch.rand(n, device="cuda") for _ in range(2)]
+            out = torch.empty_like(srcs[0])
+            sp = [t.data_ptr() for t in srcs]
+            op = op_for(7)
+            ms = timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, 7, op, 0, False, st), 200, warm=20)
+            print(json.dumps({"what": "small", "KiB_per_input": kib, "us_per_call": round(ms * 1e3, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
