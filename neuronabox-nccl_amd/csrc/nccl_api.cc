@@ -20,10 +20,12 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <exception>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <random>
@@ -71,6 +73,19 @@ void warn(const char* fmt, ...) {
   }
   if (debugLevel() >= 2) std::fprintf(stderr, "NCCL WARN %s\n", buf);
 }
+
+bool traceOn() {
+  static bool on = [] { const char* v = std::getenv("NBX_TRACE"); return v && *v && *v != '0'; }();
+  return on;
+}
+#define NBX_TRACE(...)                                   \
+  do {                                                   \
+    if (traceOn()) {                                     \
+      std::fprintf(stderr, "[nbx] " __VA_ARGS__);        \
+      std::fprintf(stderr, "\n");                        \
+      std::fflush(stderr);                               \
+    }                                                    \
+  } while (0)
 
 void info(const char* fmt, ...) {
   if (debugLevel() < 3) return;
@@ -140,13 +155,32 @@ namespace {
 
 // In-process clique (ncclCommInitAll): per-rank streams are the caller's; the
 // clique owns the events used to order the exchange across devices.
+enum CollKind { kAllReduce, kReduceScatter, kReduce };
+
+struct PendingColl {
+  CollKind kind;
+  const void* send;
+  void* recv;
+  size_t count;   // AllReduce/Reduce: count; ReduceScatter: recvcount
+  ncclDataType_t dt;
+  nbxDevRedOpFull op;
+  int root;
+  hipStream_t stream;
+};
+
 struct Clique {
   int n = 0;
   std::vector<ncclComm*> comms;
   std::vector<int> devs;
   std::vector<hipEvent_t> evEnter, evReduced, evDone;   // one per rank
+  std::vector<std::deque<PendingColl>> pending;         // per-rank FIFO of enqueued parts
   std::mutex mu;
 };
+
+// Live cliques (weak: a clique dies with its last communicator). Guarded by
+// g_pendMu together with every clique's pending queues.
+std::mutex g_pendMu;
+std::vector<std::weak_ptr<Clique>> g_cliques;
 
 ncclResult_t commCheck(ncclComm* comm, const char* opName) {
   // PtrCheck(comm) — argcheck.cc:28-34
@@ -282,34 +316,6 @@ ncclResult_t launchOneRank(void* dst, const void* src, size_t count, const nbxDe
 
 thread_local int t_groupDepth = 0;
 
-enum CollKind { kAllReduce, kReduceScatter, kReduce };
-
-struct PendingColl {
-  CollKind kind;
-  const void* send;
-  void* recv;
-  size_t count;   // AllReduce/Reduce: count; ReduceScatter: recvcount
-  ncclDataType_t dt;
-  nbxDevRedOpFull op;
-  int root;
-  hipStream_t stream;
-};
-
-struct CliquePending {
-  std::vector<std::vector<PendingColl>> perRank;   // FIFO per rank
-};
-
-std::mutex g_pendMu;
-std::vector<std::pair<Clique*, CliquePending>> g_pending;
-
-CliquePending& pendingFor(Clique* c) {
-  for (auto& p : g_pending)
-    if (p.first == c) return p.second;
-  g_pending.push_back({c, CliquePending{}});
-  g_pending.back().second.perRank.resize(c->n);
-  return g_pending.back().second;
-}
-
 // Element range of block b when `count` is split over n ranks, aligned so
 // every block starts on a 16-byte boundary relative to the buffer.
 void blockRange(size_t count, int eb, int n, int b, size_t* off, size_t* len) {
@@ -336,6 +342,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
     }
   }
   const int eb = typeSize(p0.dt);
+  NBX_TRACE("clique coll kind=%d n=%d count=%zu dt=%d op=%d", (int)p0.kind, n, p0.count, (int)p0.dt, p0.op.op);
   // 1. enter: every rank's stream reaches the collective
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
@@ -346,6 +353,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
     for (int j = 0; j < n; j++)
       if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evEnter[j], 0));
   }
+  NBX_TRACE("clique enter events done");
   // 2. reduce: rank r folds block r of every send buffer in ring order r+1..r
   const size_t total = p0.kind == kReduceScatter ? p0.count * (size_t)n : p0.count;
   const int postOp = 1;   // the fold is complete in one pass: apply SumPostDiv here
@@ -370,6 +378,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
     else dst = (char*)parts[r].recv + off * (size_t)eb;
     void* dsts[1] = {dst};
     nbxDevRedOpFull op = parts[r].op;
+    NBX_TRACE("clique reduce rank %d off=%zu len=%zu dst=%p src0=%p", r, off, len, dst, srcs[0]);
     NCCLCHECK(nbxReduceMulti(dsts, 1, srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n, postOp,
                              (ncclStream_t)parts[r].stream));
   }
@@ -377,6 +386,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
     DevGuard g(c->devs[r]);
     HIPCHECK(hipEventRecord(c->evReduced[r], parts[r].stream));
   }
+  NBX_TRACE("clique reduce launched");
   // 3. gather (AllReduce only): rank r pulls block j from rank j's recv buffer
   if (p0.kind == kAllReduce) {
     for (int r = 0; r < n; r++) {
@@ -403,6 +413,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
       HIPCHECK(hipEventRecord(c->evDone[r], parts[r].stream));
     }
   }
+  NBX_TRACE("clique gather enqueued");
   // 4. leave: no rank reuses its buffers before every peer is done with them
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
@@ -414,22 +425,40 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
 
 // Launch every complete collective queued for every clique (called when the
 // outermost group ends, or immediately outside a group).
+ncclResult_t flushPendingImpl();
 ncclResult_t flushPending() {
+  try {
+    return flushPendingImpl();
+  } catch (const std::exception& e) {
+    warn("internal exception: %s", e.what());
+    return ncclInternalError;
+  } catch (...) {
+    warn("internal exception");
+    return ncclInternalError;
+  }
+}
+ncclResult_t flushPendingImpl() {
   std::lock_guard<std::mutex> g(g_pendMu);
-  for (auto& cp : g_pending) {
-    Clique* c = cp.first;
-    auto& pr = cp.second.perRank;
+  for (size_t i = 0; i < g_cliques.size();) {
+    std::shared_ptr<Clique> c = g_cliques[i].lock();
+    if (!c) {   // every communicator of this clique was destroyed
+      g_cliques.erase(g_cliques.begin() + (long)i);
+      continue;
+    }
+    auto& pr = c->pending;
     for (;;) {
       bool ready = true;
       for (int r = 0; r < c->n; r++) ready &= !pr[r].empty();
       if (!ready) break;
-      std::vector<PendingColl> parts(c->n);
+      std::vector<PendingColl> parts;
+      parts.reserve(c->n);
       for (int r = 0; r < c->n; r++) {
-        parts[r] = pr[r].front();
-        pr[r].erase(pr[r].begin());
+        parts.push_back(pr[r].front());
+        pr[r].pop_front();
       }
-      NCCLCHECK(runCliqueColl(c, parts));
+      NCCLCHECK(runCliqueColl(c.get(), parts));
     }
+    i++;
   }
   return ncclSuccess;
 }
@@ -451,8 +480,7 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
   }
   {
     std::lock_guard<std::mutex> g(g_pendMu);
-    CliquePending& cp = pendingFor(comm->clique.get());
-    cp.perRank[comm->rank].push_back(PendingColl{kind, sendbuff, recvbuff, count, dt, opFull, root, stream});
+    comm->clique->pending[comm->rank].push_back(PendingColl{kind, sendbuff, recvbuff, count, dt, opFull, root, stream});
   }
   if (t_groupDepth == 0) return flushPending();
   return ncclSuccess;
@@ -548,6 +576,7 @@ NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* d
   clique->evEnter.resize(ndev);
   clique->evReduced.resize(ndev);
   clique->evDone.resize(ndev);
+  clique->pending.resize(ndev);
   for (int r = 0; r < ndev; r++) {
     DevGuard g(devs[r]);
     for (int j = 0; j < ndev; j++) {
@@ -571,6 +600,10 @@ NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* d
     comms[r]->clique = clique;
   }
   clique->comms.assign(comms, comms + ndev);
+  {
+    std::lock_guard<std::mutex> g(g_pendMu);
+    g_cliques.push_back(clique);
+  }
   return ncclSuccess;
 }
 
@@ -583,8 +616,10 @@ static ncclResult_t commFree(ncclComm* comm) {
   std::shared_ptr<Clique> c = comm->clique;
   comm->magic = 0;
   if (c) {
+    std::lock_guard<std::mutex> gp(g_pendMu);
     std::lock_guard<std::mutex> g(c->mu);
     int r = comm->rank;
+    if (r >= 0 && r < c->n) c->pending[r].clear();
     if (r >= 0 && r < c->n) {
       c->comms[r] = nullptr;
       DevGuard dg(c->devs[r]);

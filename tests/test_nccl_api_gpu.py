@@ -1,0 +1,220 @@
+"""GPU tests of the NCCL API layer (nccl_api.cc) over the reduction core.
+
+World size 1 follows taskAppend -> ncclLaunchOneRank (enqueue.cc:1564-1566,
+onerank.cu:48-79): PreMulSum runs the kernel, every other op is a copy.
+The in-process clique (ncclCommInitAll) is exercised with several ranks that
+share the one GPU of the test box; its documented fold order for block r is
+ranks r+1, r+2, ..., r (NCCL's ring reduce-scatter order).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+F32, F16, I32, BF16, F64, I8, U64 = 7, 6, 2, 9, 8, 0, 5
+
+
+def t_of(torch, a):
+    return torch.from_numpy(a.view(np.uint8).copy()).cuda()
+
+
+def np_of(t, dtype):
+    return t.cpu().numpy().view(dtype)
+
+
+@pytest.fixture
+def comm1(nbx, torch_gpu):
+    c = nbx.Communicator.init_rank(1, nbx.get_unique_id(), 0)
+    yield c
+    c.destroy()
+
+
+def test_comm_queries(nbx, comm1):
+    assert comm1.count() == 1 and comm1.user_rank() == 0 and comm1.device() == 0
+    assert comm1.async_error() == 0
+
+
+@pytest.mark.parametrize("dtype", [I8, I32, U64, F16, F32, F64, BF16, 10])
+@pytest.mark.parametrize("op", [0, 1, 2, 3, 4])
+def test_one_rank_allreduce_semantics(nbx, oracle, torch_gpu, comm1, dtype, op):
+    torch = torch_gpu
+    st = torch.cuda.current_stream().cuda_stream
+    x = oracle.random_inputs(dtype, 1, 5003, seed=dtype * 7 + op)[0]
+    tx = t_of(torch, x)
+    ty = torch.zeros_like(tx)
+    comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, dtype, op, st)
+    torch.cuda.synchronize()
+    devop, arg = oracle.host_to_dev_redop(op, dtype, 1)
+    if devop == 3:   # PreMulSum (float Avg): kernel with pre-op on the one source
+        exp = oracle.reduce_multi([x], dtype, devop, arg, n_pre_op_srcs=1, post_op=True)[0]
+    else:            # copy (onerank.cu:50-55)
+        exp = x
+    assert np.array_equal(np_of(ty, x.dtype).view(np.uint8), exp.view(np.uint8))
+
+
+def test_one_rank_in_place_and_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, comm1):
+    torch = torch_gpu
+    st = torch.cuda.current_stream().cuda_stream
+    x = oracle.random_inputs(F32, 1, 4096, seed=3)[0]
+    tx = t_of(torch, x)
+    comm1.all_reduce(tx.data_ptr(), tx.data_ptr(), x.size, F32, 0, st)       # in place: no-op
+    ty = torch.zeros_like(tx)
+    comm1.reduce_scatter(tx.data_ptr(), ty.data_ptr(), x.size, F32, 0, st)
+    tz = torch.zeros_like(tx)
+    comm1.reduce(tx.data_ptr(), tz.data_ptr(), x.size, F32, 2, 0, st)
+    torch.cuda.synchronize()
+    for t in (tx, ty, tz):
+        assert np.array_equal(np_of(t, np.float32), x)
+    with pytest.raises(nbx.NcclError) as e:
+        comm1.reduce(tx.data_ptr(), tz.data_ptr(), x.size, F32, 0, 1, st)   # root out of range
+    assert e.value.code == nbx.ncclResult.ncclInvalidArgument
+    with pytest.raises(nbx.NcclError):
+        comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, 12, 0, st)    # bad type
+    with pytest.raises(nbx.NcclError):
+        comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, F32, 77, st)  # unknown op
+
+
+def test_user_premulsum_host_and_device_scalar(nbx, oracle, torch_gpu, comm1):
+    torch = torch_gpu
+    st = torch.cuda.current_stream().cuda_stream
+    x = oracle.random_inputs(F32, 1, 8191, seed=11)[0]
+    tx = t_of(torch, x)
+    ty = torch.zeros_like(tx)
+    s = ctypes.c_float(0.3)
+    op = comm1.redop_create_premulsum(ctypes.addressof(s), F32, nbx.ncclScalarResidence.ncclScalarHostImmediate)
+    assert op >= 5
+    s.value = 9.0   # host-immediate: captured at creation
+    comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, F32, op, st)
+    torch.cuda.synchronize()
+    exp = oracle.reduce_multi([x], F32, 3, int(np.float32(0.3).view(np.uint32)), 1, True)[0]
+    assert np.array_equal(np_of(ty, np.float32), exp)
+    # device-resident scalar: dereferenced while the kernel runs
+    ds = torch.tensor([0.0], dtype=torch.float32, device="cuda")
+    op2 = comm1.redop_create_premulsum(ds.data_ptr(), F32, nbx.ncclScalarResidence.ncclScalarDevice)
+    ds.fill_(-1.75)
+    comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, F32, op2, st)
+    torch.cuda.synchronize()
+    exp2 = oracle.reduce_multi([x], F32, 3, int(np.float32(-1.75).view(np.uint32)), 1, True)[0]
+    assert np.array_equal(np_of(ty, np.float32), exp2)
+    with pytest.raises(nbx.NcclError):   # op created for F32 used with F16
+        comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), 16, F16, op, st)
+    comm1.redop_destroy(op)
+    comm1.redop_destroy(op2)
+    with pytest.raises(nbx.NcclError):
+        comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, F32, op, st)
+    with pytest.raises(nbx.NcclError):
+        comm1.redop_destroy(op)
+
+
+def _ring_order_reduce(oracle, xs, dtype, devop, arg, post, nranks, block_of):
+    """Oracle for the clique: block r folded in rank order r+1, ..., r."""
+    st = oracle.NP_STORAGE[dtype]
+    count = xs[0].size
+    out = np.empty(count, dtype=st)
+    for r in range(nranks):
+        lo, hi = block_of(r)
+        if hi <= lo:
+            continue
+        order = [(r + 1 + k) % nranks for k in range(nranks)]
+        out[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
+                                         n_pre_op_srcs=nranks, post_op=post)[0]
+    return out
+
+
+def _blocks(count, eb, n):
+    epp = 16 // eb
+    per = -(-count // n)
+    per = -(-per // epp) * epp
+    return lambda b: (min(count, per * b), min(count, per * b + per))
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+@pytest.mark.parametrize("dtype,op", [(F32, 0), (F32, 4), (F16, 0), (BF16, 4), (I32, 4), (I32, 2), (F64, 3)])
+def test_clique_allreduce_shared_device(nbx, oracle, torch_gpu, nranks, dtype, op):
+    torch = torch_gpu
+    comms = nbx.Communicator.init_all([0] * nranks)
+    try:
+        assert [c.user_rank() for c in comms] == list(range(nranks))
+        count = 30011
+        xs = oracle.random_inputs(dtype, nranks, count, seed=nranks * 100 + dtype)
+        txs = [t_of(torch, x) for x in xs]
+        tys = [torch.zeros_like(t) for t in txs]
+        streams = [torch.cuda.Stream() for _ in range(nranks)]
+        torch.cuda.synchronize()
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].all_reduce(txs[r].data_ptr(), tys[r].data_ptr(), count, dtype, op, streams[r].cuda_stream)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        devop, arg = oracle.host_to_dev_redop(op, dtype, nranks)
+        eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+        exp = _ring_order_reduce(oracle, xs, dtype, devop, arg, devop == 4, nranks, _blocks(count, eb, nranks))
+        for r in range(nranks):
+            got = np_of(tys[r], exp.dtype)
+            assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), f"rank {r}"
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_clique_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, nranks):
+    torch = torch_gpu
+    comms = nbx.Communicator.init_all([0] * nranks)
+    try:
+        recvcount = 10007
+        xs = oracle.random_inputs(F32, nranks, recvcount * nranks, seed=5)
+        txs = [t_of(torch, x) for x in xs]
+        # in place for rank 1: recvbuff == sendbuff + rank * recvcount
+        outs = [torch.zeros(recvcount * 4, dtype=torch.uint8, device="cuda") for _ in range(nranks)]
+        rptr = [o.data_ptr() for o in outs]
+        rptr[1] = txs[1].data_ptr() + 1 * recvcount * 4
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].reduce_scatter(txs[r].data_ptr(), rptr[r], recvcount, F32, 0, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        exp = _ring_order_reduce(oracle, xs, F32, 0, 0, False, nranks,
+                                 lambda b: (b * recvcount, (b + 1) * recvcount))
+        for r in range(nranks):
+            got = np_of(outs[r], np.float32) if r != 1 else \
+                np_of(txs[1], np.float32)[recvcount:2 * recvcount]
+            assert np.array_equal(got, exp[r * recvcount:(r + 1) * recvcount]), f"rank {r}"
+        # ncclReduce to root 1 (ranks write their reduced block into the root's buffer)
+        count = 20000
+        ys = oracle.random_inputs(I32, nranks, count, seed=9)
+        tys = [t_of(torch, y) for y in ys]
+        root_out = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].reduce(tys[r].data_ptr(), root_out.data_ptr() if r == 1 else 0, count, I32, 4, 1, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        exp = _ring_order_reduce(oracle, ys, I32, 4, nranks, True, nranks, _blocks(count, 4, nranks))
+        assert np.array_equal(np_of(root_out, np.int32), exp)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_graph_capture_one_rank_kernel(nbx, oracle, torch_gpu, comm1):
+    """The launch path does no allocation or sync, so it captures into a graph."""
+    torch = torch_gpu
+    x = oracle.random_inputs(F16, 1, 65536, seed=2)[0]
+    tx = t_of(torch, x)
+    ty = torch.zeros_like(tx)
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    h = np.float16(0.25).view(np.uint16)
+    hs = ctypes.c_uint16(int(h))
+    op = comm1.redop_create_premulsum(ctypes.addressof(hs), F16, nbx.ncclScalarResidence.ncclScalarHostImmediate)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            comm1.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, F16, op, torch.cuda.current_stream().cuda_stream)
+    g.replay()
+    torch.cuda.synchronize()
+    exp = oracle.reduce_multi([x], F16, 3, int(h), 1, True)[0]
+    assert np.array_equal(np_of(ty, np.uint16), exp)
+    comm1.redop_destroy(op)
