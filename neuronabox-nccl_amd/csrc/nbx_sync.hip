@@ -1,0 +1,56 @@
+// nbx_sync.hip — cross-process / cross-device stream barrier for the
+// multi-process communicator (the role of NCCL's waitPeer/postPeer step
+// credits, prims_simple.h:129-185, reduced to one flag per phase).
+//
+// One wave: lane 0 publishes this rank's phase flag with a system-scope
+// release store; lane j polls rank j's flag (IPC-mapped over xGMI) with
+// relaxed system-scope loads and s_sleep backoff until it reaches `seq`, then
+// a system-scope acquire fence. Every spin is bounded: the host abort word
+// (ncclCommAbort) and a wall-clock timeout (s_memrealtime, 100 MHz) both end
+// it and set the host error word, read by ncclCommGetAsyncError.
+// Data written by earlier kernels of the stream is already released at their
+// kernel boundary; the barrier orders the flag after it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nbx {
+
+__global__ __launch_bounds__(64) void kPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlags, int n, int slot,
+                                                   uint64_t seq, const volatile int* abortWord,
+                                                   volatile int* errWord, uint64_t timeoutTicks) {
+  const int lane = (int)threadIdx.x;
+  if (lane == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);   // order prior work of this kernel (none) and the flag
+    __hip_atomic_store(myFlags + slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (lane < n) {
+    const uint64_t* f = peerFlags[lane] + slot;
+    const uint64_t t0 = wall_clock64();
+    uint32_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255u) == 0u) {
+        if (*abortWord != 0) {
+          *errWord = 2;
+          break;
+        }
+        if (wall_clock64() - t0 > timeoutTicks) {
+          *errWord = 1;
+          break;
+        }
+      }
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: drop stale cached peer data
+}
+
+hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t seq,
+                             const int* abortWordDev, int* errWordDev, double timeoutSec, hipStream_t stream) {
+  const uint64_t ticks = (uint64_t)(timeoutSec * 1.0e8);   // wall_clock64 runs at 100 MHz
+  hipLaunchKernelGGL(kPeerBarrier, dim3(1), dim3(64), 0, stream, myFlags, peerFlagsDev, n, slot, seq,
+                     (const volatile int*)abortWordDev, (volatile int*)errWordDev, ticks);
+  return hipGetLastError();
+}
+
+}  // namespace nbx

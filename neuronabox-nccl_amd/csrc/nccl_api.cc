@@ -26,12 +26,18 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
+#include <string>
+#include <unistd.h>
 #include <memory>
 #include <mutex>
 #include <random>
 #include <vector>
 
+#include "../../include/nbx_debug.h"
 #include "../../include/nbx_reduce.h"
+#include "nbx_bootstrap.h"
+#include "nbx_sync.h"
 
 #define NBX_EXPORT extern "C" __attribute__((visibility("default")))
 // NCCL_API (src/include/core.h:17-32): every entry point plus a p-prefixed alias.
@@ -134,6 +140,7 @@ struct UserRedOp {   // comm.h ncclUserRedOp
 };
 
 struct Clique;
+struct MpState;
 
 }  // namespace
 
@@ -149,6 +156,7 @@ struct ncclComm {
   std::vector<UserRedOp> userOps;
   int freeHead = 0;
   std::shared_ptr<Clique> clique;  // nRanks > 1 (single process)
+  MpState* mp = nullptr;           // nRanks > 1 (one process per rank)
 };
 
 namespace {
@@ -463,6 +471,229 @@ ncclResult_t flushPendingImpl() {
   return ncclSuccess;
 }
 
+
+// ---------------------------------------------------------------------------
+// Multi-process communicator (ncclCommInitRank with nranks > 1, one process
+// per rank on one node). Replaces NCCL's bootstrap + P2P transport setup
+// (bootstrap.cc, transport/p2p.cc:190-381) with: a TCP bootstrap for the
+// allgathers, hipIpc handles of the caller's buffers exchanged per call
+// (NCCL calls "may perform inter-CPU synchronization", nccl.h.in:253-261)
+// and cached after the first map, and device flag barriers (nbx_sync.hip)
+// ordering the phases on the caller's stream. The data path is the same
+// one-shot direct exchange as the in-process clique.
+
+enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kNumSlots = 4 };
+
+struct MpState {
+  nbx::Bootstrap* bs = nullptr;
+  uint64_t* flags = nullptr;           // own phase flags (device memory, IPC-exported)
+  uint64_t** peerFlagsDev = nullptr;   // device table: rank -> flags (self = flags)
+  std::vector<void*> peerFlagMaps;     // IPC mappings to close
+  int* hostWords = nullptr;            // pinned: [0] abort, [1] error
+  int* hostWordsDev = nullptr;
+  uint64_t seq = 0;
+  double timeoutSec = 300.0;
+  std::map<std::pair<int, std::string>, void*> maps;   // (peer, ipc handle) -> mapped base
+};
+
+struct MpInitInfo {
+  int32_t pid;
+  int32_t device;
+  hipIpcMemHandle_t flagsHandle;
+};
+
+struct MpCallInfo {
+  uint64_t seq;
+  int32_t kind, dt, op, root;
+  uint64_t count;
+  int32_t hasSend, hasRecv;
+  hipIpcMemHandle_t sendH, recvH;
+  uint64_t sendOff, recvOff;
+};
+
+ncclResult_t ipcHandleOf(const void* p, hipIpcMemHandle_t* h, uint64_t* off) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  HIPCHECK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p));
+  HIPCHECK(hipIpcGetMemHandle(h, (void*)base));
+  *off = (uint64_t)((const char*)p - (const char*)base);
+  return ncclSuccess;
+}
+
+ncclResult_t mapPeer(MpState* mp, int peer, const hipIpcMemHandle_t& h, void** base) {
+  auto key = std::make_pair(peer, std::string((const char*)&h, sizeof(h)));
+  auto it = mp->maps.find(key);
+  if (it != mp->maps.end()) {
+    *base = it->second;
+    return ncclSuccess;
+  }
+  void* p = nullptr;
+  HIPCHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  mp->maps[key] = p;
+  *base = p;
+  return ncclSuccess;
+}
+
+ncclResult_t mpBarrier(ncclComm* comm, int slot, uint64_t seq, hipStream_t stream) {
+  MpState* mp = comm->mp;
+  HIPCHECK(nbx::launchPeerBarrier(mp->flags, mp->peerFlagsDev, comm->nRanks, slot, seq, mp->hostWordsDev,
+                                  mp->hostWordsDev + 1, mp->timeoutSec, stream));
+  return ncclSuccess;
+}
+
+ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
+  MpState* mp = new MpState();
+  c->mp = mp;
+  const char* t = std::getenv("NBX_TIMEOUT_SEC");
+  if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
+  NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
+  HIPCHECK(hipMalloc((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->flags, 0, kNumSlots * sizeof(uint64_t)));
+  HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(mp->hostWords, 0, 64);
+  HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
+  MpInitInfo mine{};
+  mine.pid = (int32_t)getpid();
+  mine.device = c->device;
+  HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
+  std::vector<MpInitInfo> all(c->nRanks);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
+  std::vector<uint64_t*> table(c->nRanks);
+  for (int j = 0; j < c->nRanks; j++) {
+    if (j == c->rank) {
+      table[j] = mp->flags;
+      continue;
+    }
+    if (all[j].device != c->device) {
+      int can = 0;
+      HIPCHECK(hipDeviceCanAccessPeer(&can, c->device, all[j].device));
+      if (can) {
+        hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+        (void)hipGetLastError();
+      }
+    }
+    void* p = nullptr;
+    HIPCHECK(hipIpcOpenMemHandle(&p, all[j].flagsHandle, hipIpcMemLazyEnablePeerAccess));
+    mp->peerFlagMaps.push_back(p);
+    table[j] = (uint64_t*)p;
+  }
+  HIPCHECK(hipMalloc((void**)&mp->peerFlagsDev, c->nRanks * sizeof(uint64_t*)));
+  HIPCHECK(hipMemcpy(mp->peerFlagsDev, table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
+  // everyone has mapped everyone before the first collective
+  int dummy = 0;
+  std::vector<int> sink(c->nRanks);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), sink.data()));
+  info("comm %p rank %d nranks %d device %d: multi-process communicator ready", (void*)c, c->rank, c->nRanks,
+       c->device);
+  return ncclSuccess;
+}
+
+void mpFree(ncclComm* c) {
+  MpState* mp = c->mp;
+  if (!mp) return;
+  DevGuard g(c->device);
+  (void)hipDeviceSynchronize();
+  for (auto& kv : mp->maps) (void)hipIpcCloseMemHandle(kv.second);
+  for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
+  if (mp->peerFlagsDev) (void)hipFree(mp->peerFlagsDev);
+  if (mp->flags) (void)hipFree(mp->flags);
+  if (mp->hostWords) (void)hipHostFree(mp->hostWords);
+  nbx::bootstrapClose(mp->bs);
+  delete mp;
+  c->mp = nullptr;
+}
+
+ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* recv, size_t count, ncclDataType_t dt,
+                       const nbxDevRedOpFull& op, int root, hipStream_t stream) {
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks, me = comm->rank;
+  const int eb = typeSize(dt);
+  const uint64_t seq = ++mp->seq;
+  MpCallInfo mine{};
+  mine.seq = seq;
+  mine.kind = (int32_t)kind;
+  mine.dt = (int32_t)dt;
+  mine.op = op.op;
+  mine.root = root;
+  mine.count = count;
+  mine.hasSend = count > 0 && send != nullptr;
+  mine.hasRecv = count > 0 && recv != nullptr;
+  if (mine.hasSend) NCCLCHECK(ipcHandleOf(send, &mine.sendH, &mine.sendOff));
+  if (mine.hasRecv) NCCLCHECK(ipcHandleOf(recv, &mine.recvH, &mine.recvOff));
+  std::vector<MpCallInfo> all(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
+  for (int j = 0; j < n; j++) {
+    const MpCallInfo& a = all[j];
+    if (a.seq != seq || a.kind != mine.kind || a.dt != mine.dt || a.op != mine.op || a.root != root ||
+        a.count != count) {
+      warn("collective mismatch across ranks (rank %d vs %d)", j, me);
+      return ncclInvalidUsage;
+    }
+  }
+  if (count == 0) return ncclSuccess;
+  std::vector<const char*> sendP(n, nullptr);
+  std::vector<char*> recvP(n, nullptr);
+  for (int j = 0; j < n; j++) {
+    if (j == me) {
+      sendP[j] = (const char*)send;
+      recvP[j] = (char*)recv;
+      continue;
+    }
+    void* b = nullptr;
+    if (all[j].hasSend) {
+      NCCLCHECK(mapPeer(mp, j, all[j].sendH, &b));
+      sendP[j] = (const char*)b + all[j].sendOff;
+    }
+    if (all[j].hasRecv) {
+      NCCLCHECK(mapPeer(mp, j, all[j].recvH, &b));
+      recvP[j] = (char*)b + all[j].recvOff;
+    }
+  }
+  for (int j = 0; j < n; j++)
+    if (!sendP[j] || ((kind != kReduce || j == root) && !recvP[j])) {
+      warn("rank %d passed a NULL buffer", j);
+      return ncclInvalidArgument;
+    }
+  // 1. every rank's stream has reached the collective (its inputs are written)
+  NCCLCHECK(mpBarrier(comm, kSlotEnter, seq, stream));
+  // 2. direct reduce of this rank's block, ring order me+1, ..., me
+  const size_t total = kind == kReduceScatter ? count * (size_t)n : count;
+  size_t off, len;
+  if (kind == kReduceScatter) {
+    off = (size_t)me * count;
+    len = count;
+  } else {
+    blockRange(total, eb, n, me, &off, &len);
+  }
+  if (len > 0) {
+    std::vector<const void*> srcs(n);
+    for (int k = 0; k < n; k++) srcs[k] = sendP[(me + 1 + k) % n] + off * (size_t)eb;
+    void* dst = kind == kReduceScatter ? (void*)recvP[me]
+                : kind == kReduce      ? (void*)(recvP[root] + off * (size_t)eb)
+                                       : (void*)(recvP[me] + off * (size_t)eb);
+    void* dsts[1] = {dst};
+    NCCLCHECK(nbxReduceMulti(dsts, 1, srcs.data(), n, len, dt, op, n, 1, (ncclStream_t)stream));
+  }
+  // 3. AllReduce: gather the peers' reduced blocks
+  if (kind == kAllReduce) {
+    NCCLCHECK(mpBarrier(comm, kSlotReduced, seq, stream));
+    nbxDevRedOpFull copyOp{nbxDevSum, 0, 0};
+    for (int k = 1; k < n; k++) {
+      const int j = (me + k) % n;
+      size_t o, l;
+      blockRange(total, eb, n, j, &o, &l);
+      if (l == 0) continue;
+      void* d[1] = {recvP[me] + o * (size_t)eb};
+      const void* s1[1] = {recvP[j] + o * (size_t)eb};
+      NCCLCHECK(nbxReduceMulti(d, 1, s1, 1, l * (size_t)eb, ncclUint8, copyOp, 0, 0, (ncclStream_t)stream));
+    }
+  }
+  // 4. nobody reuses its buffers while a peer may still read them
+  NCCLCHECK(mpBarrier(comm, kSlotDone, seq, stream));
+  return ncclSuccess;
+}
+
 // ncclEnqueueCheck + taskAppend for the reducing collectives.
 ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff, void* recvbuff, size_t count,
                          ncclDataType_t dt, ncclRedOp_t op, int root, ncclComm* comm, hipStream_t stream) {
@@ -475,6 +706,18 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
   if (comm->nRanks == 1) {
     DevGuard g(comm->device);
     ncclResult_t r = launchOneRank(recvbuff, sendbuff, count, opFull, dt, stream);
+    if (r != ncclSuccess) comm->asyncError.store(r);
+    return r;
+  }
+  if (comm->mp) {
+    DevGuard g(comm->device);
+    ncclResult_t r;
+    try {
+      r = runMpColl(comm, kind, sendbuff, recvbuff, count, dt, opFull, root, stream);
+    } catch (const std::exception& e) {
+      warn("internal exception: %s", e.what());
+      r = ncclInternalError;
+    }
     if (r != ncclSuccess) comm->asyncError.store(r);
     return r;
   }
@@ -512,12 +755,7 @@ NBX_API(ncclResult_t, ncclGetVersion, int* version) {
 
 NBX_API(ncclResult_t, ncclGetUniqueId, ncclUniqueId* out) {
   if (out == nullptr) return ncclInvalidArgument;
-  std::memset(out, 0, sizeof(*out));
-  std::memcpy(out->internal, kIdMagic, sizeof(kIdMagic));
-  std::random_device rd;
-  uint64_t key = ((uint64_t)rd() << 32) ^ rd();
-  std::memcpy(out->internal + 8, &key, sizeof(key));
-  return ncclSuccess;
+  return nbx::bootstrapCreateRoot(out);   // bootstrap.cc: the root listens for the ranks
 }
 
 NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank,
@@ -535,15 +773,29 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
     warn("ncclCommInitRank : unique id was not produced by ncclGetUniqueId");
     return ncclInvalidArgument;
   }
-  if (nranks > 1) {
-    // Multi-process bootstrap (bootstrap.cc) is not part of this build's hot path;
-    // multi-rank communicators come from ncclCommInitAll (single process).
-    warn("ncclCommInitRank : nranks > 1 across processes is not supported; use ncclCommInitAll");
-    return ncclInvalidUsage;
-  }
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
-  return newComm(newcomm, 1, 0, dev, config);
+  if (nranks == 1) return newComm(newcomm, 1, 0, dev, config);
+  if (!nbx::bootstrapIdHasRoot(commId)) {
+    warn("ncclCommInitRank : unique id carries no bootstrap root");
+    return ncclInvalidArgument;
+  }
+  ncclComm* c = nullptr;
+  NCCLCHECK(newComm(&c, nranks, myrank, dev, config));
+  ncclResult_t r;
+  try {
+    r = mpInit(c, commId);
+  } catch (const std::exception& e) {
+    warn("internal exception: %s", e.what());
+    r = ncclInternalError;
+  }
+  if (r != ncclSuccess) {
+    mpFree(c);
+    delete c;
+    return r;
+  }
+  *newcomm = c;
+  return ncclSuccess;
 }
 
 NBX_API(ncclResult_t, ncclCommInitRank, ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
@@ -615,6 +867,7 @@ NBX_API(ncclResult_t, ncclCommFinalize, ncclComm_t comm) {
 static ncclResult_t commFree(ncclComm* comm) {
   std::shared_ptr<Clique> c = comm->clique;
   comm->magic = 0;
+  mpFree(comm);
   if (c) {
     std::lock_guard<std::mutex> gp(g_pendMu);
     std::lock_guard<std::mutex> g(c->mu);
@@ -641,6 +894,7 @@ NBX_API(ncclResult_t, ncclCommDestroy, ncclComm_t comm) {
 NBX_API(ncclResult_t, ncclCommAbort, ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
   NCCLCHECK(commCheck(comm, "ncclCommAbort"));
+  if (comm->mp && comm->mp->hostWords) comm->mp->hostWords[0] = 1;   // ends every spinning barrier
   return commFree(comm);
 }
 
@@ -667,6 +921,8 @@ NBX_API(ncclResult_t, ncclCommGetAsyncError, ncclComm_t comm, ncclResult_t* asyn
   NCCLCHECK(commCheck(comm, "ncclGetAsyncError"));
   if (asyncError == nullptr) return ncclInvalidArgument;
   *asyncError = (ncclResult_t)comm->asyncError.load();
+  if (*asyncError == ncclSuccess && comm->mp && comm->mp->hostWords && comm->mp->hostWords[1] != 0)
+    *asyncError = ncclRemoteError;   // a peer barrier timed out or was aborted
   return ncclSuccess;
 }
 
@@ -780,4 +1036,25 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
   }
   if (--t_groupDepth > 0) return ncclSuccess;
   return flushPending();
+}
+
+NBX_EXPORT ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds) {
+  if (id == nullptr || nranks < 1 || rank < 0 || rank >= nranks || rounds < 0) return ncclInvalidArgument;
+  nbx::Bootstrap* b = nullptr;
+  NCCLCHECK(nbx::bootstrapConnect(*id, rank, nranks, &b));
+  ncclResult_t res = ncclSuccess;
+  for (int r = 0; r < rounds && res == ncclSuccess; r++) {
+    const size_t len = 8 + (size_t)(r * 37) % 4096;
+    std::vector<unsigned char> mine(len), all(len * (size_t)nranks);
+    for (size_t i = 0; i < len; i++) mine[i] = (unsigned char)(rank * 31 + r * 7 + i);
+    res = nbx::bootstrapAllGather(b, mine.data(), len, all.data());
+    for (int j = 0; j < nranks && res == ncclSuccess; j++)
+      for (size_t i = 0; i < len; i++)
+        if (all[(size_t)j * len + i] != (unsigned char)(j * 31 + r * 7 + i)) {
+          res = ncclInternalError;
+          break;
+        }
+  }
+  nbx::bootstrapClose(b);
+  return res;
 }

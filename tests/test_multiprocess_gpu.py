@@ -1,0 +1,119 @@
+"""Multi-process communicators (one process per rank, ncclCommInitRank with
+nranks > 1) on the GPU box. The box has one GPU, so the ranks share device 0:
+this exercises the bootstrap, hipIpc buffer exchange + mapping cache, the
+device flag barriers and the direct reduce/gather data path end to end.
+Results are compared bit-exact with the oracle folding block r in rank order
+r+1, ..., r."""
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # (kind, dtype, op)
+    ("allreduce", 7, 0), ("allreduce", 7, 4), ("allreduce", 6, 0), ("allreduce", 2, 4), ("allreduce", 4, 2),
+    ("reducescatter", 7, 0), ("reducescatter", 9, 4), ("reduce", 7, 0), ("reduce", 2, 4),
+]
+COUNT = 40009
+
+
+def _inputs(oracle, kind, dtype, n, r):
+    cnt = COUNT * n if kind == "reducescatter" else COUNT
+    return oracle.random_inputs(dtype, n, cnt, seed=1000 + 10 * dtype)[r]
+
+
+def _child(uid_bytes, rank, n, q):
+    try:
+        import torch
+        from tests.conftest import load_package
+        from oracle import oracle
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        uid = nbx.ncclUniqueId.from_buffer_copy(uid_bytes)
+        comm = nbx.Communicator.init_rank(n, uid, rank)
+        assert comm.count() == n and comm.user_rank() == rank
+        st = torch.cuda.Stream()
+        out = {}
+        for it in range(2):   # twice: the second round hits the IPC mapping cache
+            for kind, dtype, op in CASES:
+                x = _inputs(oracle, kind, dtype, n, rank)
+                tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+                nbytes = (COUNT if kind == "reducescatter" else x.size) * x.itemsize
+                ty = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                if kind == "allreduce":
+                    comm.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, dtype, op, st.cuda_stream)
+                elif kind == "reducescatter":
+                    comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), COUNT, dtype, op, st.cuda_stream)
+                else:
+                    comm.reduce(tx.data_ptr(), ty.data_ptr() if rank == 1 % n else 0, x.size, dtype, op, 1 % n,
+                                st.cuda_stream)
+                st.synchronize()
+                out[(it, kind, dtype, op)] = ty.cpu().numpy().copy()
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception as e:  # report, never hang the parent
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def _blocks(count, eb, n):
+    epp = 16 // eb
+    per = -(-count // n)
+    per = -(-per // epp) * epp
+    return [(min(count, per * b), min(count, per * b + per)) for b in range(n)]
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multiprocess_collectives(nbx, oracle, n, monkeypatch):
+    # bounded waits everywhere: a failing rank must not strand its peers
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    uid = nbx.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_child, args=(bytes(uid), r, n, q), daemon=True) for r in range(n)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", f"rank {rank}:\n{payload}"
+            res[rank] = payload
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+    for kind, dtype, op in CASES:
+        xs = [_inputs(oracle, kind, dtype, n, r) for r in range(n)]
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        st = oracle.NP_STORAGE[dtype]
+        eb = np.dtype(st).itemsize
+        if kind == "reducescatter":
+            blocks = [(b * COUNT, (b + 1) * COUNT) for b in range(n)]
+        else:
+            blocks = _blocks(xs[0].size, eb, n)
+        full = np.empty(xs[0].size, dtype=st)
+        for r, (lo, hi) in enumerate(blocks):
+            if hi > lo:
+                order = [(r + 1 + k) % n for k in range(n)]
+                full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
+                                                  n_pre_op_srcs=n, post_op=devop == 4)[0]
+        for it in range(2):
+            for r in range(n):
+                got = res[r][(it, kind, dtype, op)].view(st)
+                if kind == "allreduce":
+                    exp = full
+                elif kind == "reducescatter":
+                    exp = full[r * COUNT:(r + 1) * COUNT]
+                else:
+                    if r != 1 % n:
+                        continue
+                    exp = full
+                assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, kind, dtype, op, r)
