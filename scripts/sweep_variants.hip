@@ -93,7 +93,10 @@ struct Variant {
 #define V(NS, B, U, L, S, M, BPC) \
   Variant{#NS "src b" #B " u" #U " ld" #L " st" #S " map" #M " bpc" #BPC, (const void*)&kvar<NS, B, U, L, S, M>, B, U, BPC}
 
+int placement(int rounds);
+
 int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[2]) == "placement") return placement(argc > 1 ? atoi(argv[1]) : 5);
   const uint64_t count = 64ull << 20;   // fp32 per input
   const int rounds = argc > 1 ? atoi(argv[1]) : 5;
   const int iters = 10;
@@ -182,5 +185,62 @@ int main(int argc, char** argv) {
     double med = t[t.size() / 2];
     printf("%-44s %10.4f %10.4f %9.1f\n", v.name.c_str(), med, t[0], bytes / (med * 1e-3) / 1e9);
   }
+  return 0;
+}
+
+// Source placement experiment: one arena, sources `stride` bytes apart.
+int placement(int rounds) {
+  const uint64_t count = 64ull << 20;
+  const uint64_t bytes = count * 4;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const uint64_t extra[] = {0, 4096, 65536 + 1024, (2u << 20) + 8192, 256 * 1024 + 4096 * 3};
+  const int nP = 5;
+  char* arena;
+  const uint64_t arenaBytes = 10 * (bytes + (4u << 20));
+  CK(hipMalloc(&arena, arenaBytes));
+  CK(hipMemset(arena, 0, arenaBytes));
+  std::vector<float*> sep(9);
+  for (int s = 0; s < 9; s++) {
+    CK(hipMalloc(&sep[s], bytes));
+    CK(hipMemset(sep[s], 0, bytes));
+  }
+  std::vector<Variant> vs = {V(8, 256, 4, 1, 0, 0, 1), V(8, 256, 2, 1, 0, 0, 2)};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  // placement -1 = separate allocations
+  std::vector<std::vector<float>> t((nP + 1) * vs.size());
+  for (int rd = 0; rd < rounds; rd++) {
+    for (int pl = -1; pl < nP; pl++) {
+      Args a;
+      for (int s = 0; s < 8; s++)
+        a.src[s] = pl < 0 ? (const f32x4*)sep[s] : (const f32x4*)(arena + s * (bytes + extra[pl]));
+      a.dst = pl < 0 ? (f32x4*)sep[8] : (f32x4*)(arena + 8 * (bytes + extra[pl]));
+      a.nPacks = count / 4;
+      for (size_t vi = 0; vi < vs.size(); vi++) {
+        const Variant& v = vs[vi];
+        uint64_t tile = (uint64_t)v.unroll * v.block;
+        uint64_t grid = std::min<uint64_t>((a.nPacks + tile - 1) / tile, (uint64_t)cus * v.blocksPerCU);
+        void* args[] = {&a};
+        CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.block), args, 0, 0));
+        CK(hipEventRecord(e0, 0));
+        for (int it = 0; it < 10; it++) CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.block), args, 0, 0));
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t[(pl + 1) * vs.size() + vi].push_back(ms / 10);
+      }
+    }
+  }
+  for (int pl = -1; pl < nP; pl++)
+    for (size_t vi = 0; vi < vs.size(); vi++) {
+      auto x = t[(pl + 1) * vs.size() + vi];
+      std::sort(x.begin(), x.end());
+      double med = x[x.size() / 2];
+      printf("placement %-10s extra=%-8llu %-40s med %.4f ms  %.1f GB/s\n", pl < 0 ? "separate" : "arena",
+             pl < 0 ? 0ull : (unsigned long long)extra[pl], vs[vi].name.c_str(), med, 9.0 * bytes / (med * 1e-3) / 1e9);
+    }
   return 0;
 }
