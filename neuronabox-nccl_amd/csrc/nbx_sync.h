@@ -4,6 +4,9 @@
 #include <stdint.h>
 
 namespace nbx {
-hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t seq,
-                             const int* abortWordDev, int* errWordDev, double timeoutSec, hipStream_t stream);
+// Post `postValue` to this rank's flag `slot`; wait until every rank in
+// `waitMask` (bit j = rank j) has flag `slot` >= `waitValue`.
+hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t postValue,
+                             uint64_t waitValue, uint64_t waitMask, const int* abortWordDev, int* errWordDev,
+                             double timeoutSec, hipStream_t stream);
 }  // namespace nbx

@@ -482,7 +482,7 @@ ncclResult_t flushPendingImpl() {
 // ordering the phases on the caller's stream. The data path is the same
 // one-shot direct exchange as the in-process clique.
 
-enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kNumSlots = 4 };
+enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kSlotRing = 3, kNumSlots = 4 };
 
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
@@ -534,11 +534,30 @@ ncclResult_t mapPeer(MpState* mp, int peer, const hipIpcMemHandle_t& h, void** b
   return ncclSuccess;
 }
 
-ncclResult_t mpBarrier(ncclComm* comm, int slot, uint64_t seq, hipStream_t stream) {
+// Post `post` on `slot`, wait for the ranks in `mask` to reach `wait` on it.
+ncclResult_t mpSignalWait(ncclComm* comm, int slot, uint64_t post, uint64_t wait, uint64_t mask, hipStream_t stream) {
   MpState* mp = comm->mp;
-  HIPCHECK(nbx::launchPeerBarrier(mp->flags, mp->peerFlagsDev, comm->nRanks, slot, seq, mp->hostWordsDev,
-                                  mp->hostWordsDev + 1, mp->timeoutSec, stream));
+  HIPCHECK(nbx::launchPeerBarrier(mp->flags, mp->peerFlagsDev, comm->nRanks, slot, post, wait, mask,
+                                  mp->hostWordsDev, mp->hostWordsDev + 1, mp->timeoutSec, stream));
   return ncclSuccess;
+}
+
+ncclResult_t mpBarrier(ncclComm* comm, int slot, uint64_t seq, hipStream_t stream) {
+  const int n = comm->nRanks;
+  const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
+  return mpSignalWait(comm, slot, seq, seq, all, stream);
+}
+
+enum class Algo { Direct, Ring };
+
+// NCCL_ALGO (tuning.cc:254-259): "Ring" selects the ring schedule for
+// AllReduce; anything else (default) the one-shot direct exchange.
+Algo algoFromEnv() {
+  static const Algo a = [] {
+    const char* v = std::getenv("NCCL_ALGO");
+    return (v && strcasecmp(v, "ring") == 0) ? Algo::Ring : Algo::Direct;
+  }();
+  return a;
 }
 
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
@@ -657,9 +676,34 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     }
   // 1. every rank's stream has reached the collective (its inputs are written)
   NCCLCHECK(mpBarrier(comm, kSlotEnter, seq, stream));
-  // 2. direct reduce of this rank's block, ring order me+1, ..., me
   const size_t total = kind == kReduceScatter ? count * (size_t)n : count;
   size_t off, len;
+  if (kind == kAllReduce && n > 2 && algoFromEnv() == Algo::Ring) {
+    // 2'. ring reduce-scatter (all_reduce.h:60-79): chunk c starts at rank c+1 and
+    // visits c+2, ..., c; at step s this rank folds chunk c = me-2-s as
+    // Fn(pre(local), received) — NCCL's operand order (recvReduceSend: srcs[0] is
+    // the local input, srcs[1] the received partial) — into its own recv buffer,
+    // where the right neighbour reads it at step s+1. Step 0 reads the left
+    // neighbour's raw input (its `send`, PreOp applies to both sources); the last
+    // step (c == me) applies postOp. Every rank works on a different chunk at
+    // each step, so all ring links carry 1/n of the data concurrently.
+    const uint64_t base = seq * 64;
+    const int left = (me + n - 1) % n;
+    for (int st = 0; st < n - 1; st++) {
+      const int c = ((me - 2 - st) % n + n) % n;
+      blockRange(total, eb, n, c, &off, &len);
+      if (len > 0) {
+        const void* srcs[2] = {sendP[me] + off * (size_t)eb,
+                               st == 0 ? (const void*)(sendP[left] + off * (size_t)eb)
+                                       : (const void*)(recvP[left] + off * (size_t)eb)};
+        void* dsts[1] = {recvP[me] + off * (size_t)eb};
+        NCCLCHECK(nbxReduceMulti(dsts, 1, srcs, 2, len, dt, op, st == 0 ? 2 : 1, st == n - 2 ? 1 : 0,
+                                 (ncclStream_t)stream));
+      }
+      if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, base + st + 1, base + st + 1, 1ull << left, stream));
+    }
+  } else {
+  // 2. direct reduce of this rank's block, ring order me+1, ..., me
   if (kind == kReduceScatter) {
     off = (size_t)me * count;
     len = count;
@@ -674,6 +718,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
                                        : (void*)(recvP[me] + off * (size_t)eb);
     void* dsts[1] = {dst};
     NCCLCHECK(nbxReduceMulti(dsts, 1, srcs.data(), n, len, dt, op, n, 1, (ncclStream_t)stream));
+  }
   }
   // 3. AllReduce: gather the peers' reduced blocks
   if (kind == kAllReduce) {

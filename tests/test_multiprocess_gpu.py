@@ -67,11 +67,15 @@ def _blocks(count, eb, n):
     return [(min(count, per * b), min(count, per * b + per)) for b in range(n)]
 
 
-@pytest.mark.parametrize("n", [2, 3])
-def test_multiprocess_collectives(nbx, oracle, n, monkeypatch):
+@pytest.mark.parametrize("n,algo", [(2, "direct"), (3, "direct"), (3, "ring"), (4, "ring")])
+def test_multiprocess_collectives(nbx, oracle, n, algo, monkeypatch):
+    """NCCL_ALGO=Ring: NCCL's ring order (chunk c from rank c+1 to c, Fn(local,
+    received)); for the commutative ops tested it is bit-identical to the
+    oracle's left fold in the order c+1, ..., c."""
     # bounded waits everywhere: a failing rank must not strand its peers
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
