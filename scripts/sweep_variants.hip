@@ -94,9 +94,11 @@ struct Variant {
   Variant{#NS "src b" #B " u" #U " ld" #L " st" #S " map" #M " bpc" #BPC, (const void*)&kvar<NS, B, U, L, S, M>, B, U, BPC}
 
 int placement(int rounds);
+int lowsrc(int rounds);
 
 int main(int argc, char** argv) {
   if (argc > 2 && std::string(argv[2]) == "placement") return placement(argc > 1 ? atoi(argv[1]) : 5);
+  if (argc > 2 && std::string(argv[2]) == "lowsrc") return lowsrc(argc > 1 ? atoi(argv[1]) : 5);
   const uint64_t count = 64ull << 20;   // fp32 per input
   const int rounds = argc > 1 ? atoi(argv[1]) : 5;
   const int iters = 10;
@@ -242,5 +244,55 @@ int placement(int rounds) {
       printf("placement %-10s extra=%-8llu %-40s med %.4f ms  %.1f GB/s\n", pl < 0 ? "separate" : "arena",
              pl < 0 ? 0ull : (unsigned long long)extra[pl], vs[vi].name.c_str(), med, 9.0 * bytes / (med * 1e-3) / 1e9);
     }
+  return 0;
+}
+
+// Store policy vs read:write ratio: nSrcs in {1, 2, 3, 4, 8}, plain vs nt stores.
+int lowsrc(int rounds) {
+  const uint64_t count = 64ull << 20;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  std::vector<float*> src(9);
+  for (int s = 0; s < 9; s++) {
+    CK(hipMalloc(&src[s], count * 4));
+    CK(hipMemset(src[s], 0, count * 4));
+  }
+  struct LV { Variant v; int nsrc; };
+  std::vector<LV> vs = {
+      {V(1, 256, 16, 1, 0, 0, 1), 1}, {V(1, 256, 16, 1, 1, 0, 1), 1}, {V(1, 256, 8, 1, 1, 0, 2), 1}, {V(1, 256, 4, 1, 1, 0, 4), 1},
+      {V(2, 256, 16, 1, 0, 0, 1), 2}, {V(2, 256, 16, 1, 1, 0, 1), 2}, {V(2, 256, 8, 1, 1, 0, 2), 2}, {V(2, 256, 4, 1, 1, 0, 4), 2},
+      {V(3, 256, 8, 1, 0, 0, 1), 3},  {V(3, 256, 8, 1, 1, 0, 1), 3},  {V(3, 256, 4, 1, 1, 0, 2), 3},
+      {V(4, 256, 8, 1, 0, 0, 1), 4},  {V(4, 256, 8, 1, 1, 0, 1), 4},  {V(4, 256, 4, 1, 1, 0, 2), 4},
+      {V(8, 256, 4, 1, 0, 0, 1), 8},  {V(8, 256, 4, 1, 1, 0, 1), 8},
+  };
+  Args a;
+  for (int s = 0; s < 8; s++) a.src[s] = (const f32x4*)src[s];
+  a.dst = (f32x4*)src[8];
+  a.nPacks = count / 4;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> t(vs.size());
+  for (int rd = 0; rd < rounds; rd++)
+    for (size_t i = 0; i < vs.size(); i++) {
+      const Variant& v = vs[i].v;
+      uint64_t tile = (uint64_t)v.unroll * v.block;
+      uint64_t grid = std::min<uint64_t>((a.nPacks + tile - 1) / tile, (uint64_t)cus * v.blocksPerCU);
+      void* args[] = {&a};
+      CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.block), args, 0, 0));
+      CK(hipEventRecord(e0, 0));
+      for (int it = 0; it < 10; it++) CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.block), args, 0, 0));
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[i].push_back(ms / 10);
+    }
+  for (size_t i = 0; i < vs.size(); i++) {
+    auto x = t[i];
+    std::sort(x.begin(), x.end());
+    double med = x[x.size() / 2];
+    printf("%-44s med %.4f ms  %.1f GB/s\n", vs[i].v.name.c_str(), med, (vs[i].nsrc + 1.0) * count * 4 / (med * 1e-3) / 1e9);
+  }
   return 0;
 }
