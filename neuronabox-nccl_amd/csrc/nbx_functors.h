@@ -220,6 +220,7 @@ struct FnMinMaxInt : FnBase<FnMinMaxInt<E>, E> {
 template <class E>
 struct FnPreMulSumInt : FnBase<FnPreMulSumInt<E>, E> {
   static constexpr bool kHasPre = true;
+  static constexpr int kUnrollCap = sizeof(E) == 1 ? 4 : 16;
   E scalar;  // reduce_kernel.h:360-369
   __device__ explicit FnPreMulSumInt(uint64_t arg) : scalar((E)arg) {}
   __device__ E red(E a, E b) const { return (E)(a + b); }
@@ -230,6 +231,7 @@ struct FnPreMulSumInt : FnBase<FnPreMulSumInt<E>, E> {
 template <class E, class S>
 struct FnSumPostDiv : FnBase<FnSumPostDiv<E, S>, E> {
   static constexpr bool kHasPost = true;
+  static constexpr int kUnrollCap = sizeof(E) == 1 ? 4 : 16;
   int divisor;  // reduce_kernel.h:502
   __device__ explicit FnSumPostDiv(uint64_t arg) : divisor((int)arg) {}
   __device__ E red(E a, E b) const { return (E)(a + b); }

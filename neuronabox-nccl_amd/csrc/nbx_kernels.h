@@ -64,6 +64,38 @@ __device__ __forceinline__ void reduceElt(const Fn& fn, const KArgs& a, int nSrc
   if (a.nDsts > 1) ((E*)a.dst[1])[i] = acc;
 }
 
+// Fold one tile slice already in registers and store it (all U packs valid).
+template <class Fn, int NSRC, int U>
+__device__ __forceinline__ void foldStore(const Fn& fn, const u32x4 (&v)[NSRC][U], uint32_t preMask, bool doPost,
+                                          u32x4* dst0, u32x4* dst1, bool two, uint64_t p) {
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    u32x4 acc = v[0][u];
+    if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
+#pragma unroll
+    for (int s = 1; s < NSRC; s++) {
+      u32x4 t = v[s][u];
+      if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
+      acc = fn.redPack(acc, t);
+    }
+    if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
+    stPack(dst0 + p + u * kBlock, acc);
+    if (two) stPack(dst1 + p + u * kBlock, acc);
+  }
+}
+
+template <int NSRC, int U>
+__device__ __forceinline__ void loadTile(u32x4 (&v)[NSRC][U], const u32x4* const (&src)[NSRC], uint64_t p) {
+#pragma unroll
+  for (int s = 0; s < NSRC; s++)
+#pragma unroll
+    for (int u = 0; u < U; u++) v[s][u] = ldPack(src[s] + p + u * kBlock);
+}
+
+// Grid-stride loop over tiles; each lane issues all NSRC x U loads of a tile
+// before folding. (A software-pipelined variant — next tile's loads issued
+// before the current tile is stored — measured neutral to -5 % in-process on
+// MI355X, profiles/r1/sweep_lib_r1d.jsonl, and was dropped.)
 template <class Fn, int NSRC, int U>
 __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
   using E = typename Fn::Elt;
@@ -81,48 +113,22 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
   const uint64_t n = a.nPacks;
   constexpr uint64_t kTile = (uint64_t)U * kBlock;
   const uint64_t stride = (uint64_t)gridDim.x * kTile;
-
   for (uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x; p < n; p += stride) {
-    u32x4 v[NSRC][U];
     if (p + (uint64_t)(U - 1) * kBlock < n) {
       // full tile: issue every load first, then fold
-#pragma unroll
-      for (int s = 0; s < NSRC; s++)
-#pragma unroll
-        for (int u = 0; u < U; u++) v[s][u] = ldPack(src[s] + p + u * kBlock);
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        u32x4 acc = v[0][u];
-        if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
-#pragma unroll
-        for (int s = 1; s < NSRC; s++) {
-          u32x4 t = v[s][u];
-          if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
-          acc = fn.redPack(acc, t);
-        }
-        if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
-        stPack(dst0 + p + u * kBlock, acc);
-        if (two) stPack(dst1 + p + u * kBlock, acc);
-      }
+      u32x4 v[NSRC][U];
+      loadTile<NSRC, U>(v, src, p);
+      foldStore<Fn, NSRC, U>(fn, v, preMask, doPost, dst0, dst1, two, p);
     } else {
       // last, partial tile
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const uint64_t q = p + (uint64_t)u * kBlock;
         if (q < n) {
+          u32x4 v1[NSRC][1];
 #pragma unroll
-          for (int s = 0; s < NSRC; s++) v[s][u] = ldPack(src[s] + q);
-          u32x4 acc = v[0][u];
-          if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
-#pragma unroll
-          for (int s = 1; s < NSRC; s++) {
-            u32x4 t = v[s][u];
-            if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
-            acc = fn.redPack(acc, t);
-          }
-          if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
-          stPack(dst0 + q, acc);
-          if (two) stPack(dst1 + q, acc);
+          for (int s = 0; s < NSRC; s++) v1[s][0] = ldPack(src[s] + q);
+          foldStore<Fn, NSRC, 1>(fn, v1, preMask, doPost, dst0, dst1, two, q);
         }
       }
     }
@@ -166,8 +172,8 @@ constexpr int bigUnroll() {
 template <class Fn, int... I>
 KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   KernelSet ks{};
-  const void* big[] = {(const void*)&kReducePacks<Fn, I + 1, bigUnroll<I + 1, Fn::kUnrollCap>()>...};
   const void* small[] = {(const void*)&kReducePacks<Fn, I + 1, 1>...};
+  const void* big[] = {(const void*)&kReducePacks<Fn, I + 1, bigUnroll<I + 1, Fn::kUnrollCap>()>...};
   int un[] = {bigUnroll<I + 1, Fn::kUnrollCap>()...};
   for (int i = 0; i < kMaxKSrcs; i++) {
     ks.packs[0][i] = small[i];

@@ -37,7 +37,7 @@ def timed(torch, fn, iters, warm=2):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", default="knobs,sweep,e2e,small")
+    ap.add_argument("--what", default="knobs,pipe,sweep,e2e,small")
     ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
     import torch
@@ -69,6 +69,27 @@ def main():
             print(json.dumps({"what": "knobs", "blocks_per_cu": s[0], "variant": s[1], "med_ms": round(v[len(v) // 2], 4),
                               "GBps": round(gbps(9 * n * 4, v[len(v) // 2]), 1)}), flush=True)
         del srcs, out
+
+    if "pipe" in what:
+        # in-process A/B of the big-tile kernel: software-pipelined (variant 2) vs not (3)
+        for nsrc in (2, 4, 8):
+            n = 64 << 20
+            srcs = [torch.rand(n, device="cuda") for _ in range(nsrc)]
+            out = torch.empty(n, device="cuda")
+            sp = [t.data_ptr() for t in srcs]
+            op = op_for(7)
+            res = {2: [], 3: []}
+            for _ in range(args.rounds):
+                for v in (2, 3):
+                    nbx.set_launch_config(0, v)
+                    res[v].append(timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, 7, op, 0, False, st), 10))
+            nbx.set_launch_config(0, 0)
+            for v, t in res.items():
+                t.sort()
+                print(json.dumps({"what": "pipe", "nsrc": nsrc, "variant": "pipelined" if v == 2 else "plain",
+                                  "med_ms": round(t[len(t) // 2], 4),
+                                  "GBps": round(gbps((nsrc + 1) * n * 4, t[len(t) // 2]), 1)}), flush=True)
+            del srcs, out
 
     if "sweep" in what:
         for dt, name, tdt in ((6, "fp16", torch.float16), (9, "bf16", torch.bfloat16), (7, "fp32", torch.float32),

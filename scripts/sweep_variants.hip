@@ -84,6 +84,45 @@ __global__ __launch_bounds__(BLOCK) void kvar(Args a) {
   }
 }
 
+// Software-pipelined variant: the next tile's loads are issued before the
+// current tile is folded and stored (loads always in flight per wave).
+template <int NSRC, int U, int SPOL>
+__global__ __launch_bounds__(256) void kpipe(Args a) {
+  const uint64_t n = a.nPacks;
+  constexpr uint64_t tile = (uint64_t)U * 256;
+  const uint64_t stride = (uint64_t)gridDim.x * tile;
+  uint64_t p = (uint64_t)blockIdx.x * tile + threadIdx.x;
+  if (p + (U - 1) * 256 >= n) return;   // sweep sizes: every tile full
+  f32x4 c[NSRC][U], x[NSRC][U];
+#pragma unroll
+  for (int s = 0; s < NSRC; s++)
+#pragma unroll
+    for (int u = 0; u < U; u++) c[s][u] = __builtin_nontemporal_load(a.src[s] + p + u * 256);
+  for (;;) {
+    const uint64_t q = p + stride;
+    const bool more = q + (U - 1) * 256 < n;
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < NSRC; s++)
+#pragma unroll
+        for (int u = 0; u < U; u++) x[s][u] = __builtin_nontemporal_load(a.src[s] + q + u * 256);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      f32x4 acc = c[0][u];
+#pragma unroll
+      for (int s = 1; s < NSRC; s++) acc = acc + c[s][u];
+      st<SPOL>(a.dst + p + u * 256, acc);
+    }
+    if (!more) break;
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) c[s][u] = x[s][u];
+    p = q;
+  }
+}
+
 struct Variant {
   std::string name;
   const void* fn;
@@ -264,6 +303,11 @@ int lowsrc(int rounds) {
       {V(3, 256, 8, 1, 0, 0, 1), 3},  {V(3, 256, 8, 1, 1, 0, 1), 3},  {V(3, 256, 4, 1, 1, 0, 2), 3},
       {V(4, 256, 8, 1, 0, 0, 1), 4},  {V(4, 256, 8, 1, 1, 0, 1), 4},  {V(4, 256, 4, 1, 1, 0, 2), 4},
       {V(8, 256, 4, 1, 0, 0, 1), 8},  {V(8, 256, 4, 1, 1, 0, 1), 8},
+      {Variant{"8src pipelined u4 st0 bpc1", (const void*)&kpipe<8, 4, 0>, 256, 4, 1}, 8},
+      {Variant{"8src pipelined u2 st0 bpc1", (const void*)&kpipe<8, 2, 0>, 256, 2, 1}, 8},
+      {Variant{"8src pipelined u2 st0 bpc2", (const void*)&kpipe<8, 2, 0>, 256, 2, 2}, 8},
+      {Variant{"2src pipelined u8 st1 bpc1", (const void*)&kpipe<2, 8, 1>, 256, 8, 1}, 2},
+      {Variant{"2src pipelined u8 st0 bpc1", (const void*)&kpipe<2, 8, 0>, 256, 8, 1}, 2},
   };
   Args a;
   for (int s = 0; s < 8; s++) a.src[s] = (const f32x4*)src[s];

@@ -1,0 +1,60 @@
+"""Static checks of the gfx950 code object inside libnbxccl.so (CPU only):
+every kernel is present, none uses scratch (a spill or a runtime-indexed
+register array would turn the streaming kernel into a scratch-bound one), and
+register use stays where the launch geometry assumes (<= 512 VGPRs at one
+wave per SIMD for the big tiles)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _kernels(so_path, tmp):
+    fat = os.path.join(tmp, "fat.bin")
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", so_path, os.devnull], check=True)
+    blob = open(fat, "rb").read()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
+    out = []
+    for i, s in enumerate(starts):
+        chunk = blob[s:starts[i + 1] if i + 1 < len(starts) else len(blob)]
+        b = os.path.join(tmp, f"b{i}.bin")
+        e = os.path.join(tmp, f"b{i}.elf")
+        open(b, "wb").write(chunk)
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--unbundle", f"--input={b}",
+                            f"--output={e}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], capture_output=True)
+        if r.returncode != 0 or not os.path.exists(e) or os.path.getsize(e) == 0:
+            continue
+        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", e], capture_output=True, text=True).stdout
+        for m in re.finditer(r"\.name:\s+(\S+).*?\.private_segment_fixed_size:\s+(\d+).*?\.vgpr_count:\s+(\d+)",
+                             notes, re.S):
+            out.append((m.group(1), int(m.group(2)), int(m.group(3))))
+    return out
+
+
+@pytest.fixture(scope="module")
+def kernels(nbx, tmp_path_factory):
+    if not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip("ROCm LLVM tools not present")
+    return _kernels(nbx.library_path(), str(tmp_path_factory.mktemp("co")))
+
+
+def test_all_kernels_present(kernels):
+    names = [k[0] for k in kernels]
+    packs = [n for n in names if "kReducePacks" in n]
+    elts = [n for n in names if "kReduceElts" in n]
+    assert len(elts) == 42                 # one element kernel per distinct functor
+    assert len(packs) == 42 * 16           # 8 source counts x {small, big} tiles
+    assert any("kPeerBarrier" in n for n in names)
+
+
+def test_no_scratch_and_vgpr_budget(kernels):
+    spills = [(n, p) for n, p, v in kernels if p > 0]
+    assert not spills, spills[:5]
+    assert max(v for _, _, v in kernels) <= 512
+    # the config-B kernel keeps ~32 dwordx4 loads in flight in registers
+    k8 = [v for n, p, v in kernels if n == "_ZN3nbx12kReducePacksINS_6FnSumFINS_5TyF32EEELi8ELi4EEEvNS_5KArgsE"]
+    assert k8 and 128 <= k8[0] <= 256
