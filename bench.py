@@ -46,21 +46,24 @@ def _load_package():
 
 
 def _dist_init():
+    """One process per GPU (torch.distributed.run env). The process group is the
+    control plane only (barrier + max-over-ranks): RCCL ("nccl") by default,
+    NBX_BENCH_BACKEND=gloo to keep it on the CPU. NBX_BENCH_DEVICE pins every
+    rank to one device (rehearsing N > 1 on a one-GPU box)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = int(os.environ.get("NBX_BENCH_DEVICE", local))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if torch.cuda.is_available():
-            torch.cuda.set_device(local)
+        backend = os.environ.get("NBX_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local) if backend == "nccl" else None)
-    elif torch.cuda.is_available():
-        torch.cuda.set_device(local)
-    return world, rank, local
+                                device_id=torch.device("cuda", dev) if backend == "nccl" else None)
+    return world, rank, dev
 
 
 def _barrier(world):
