@@ -23,6 +23,12 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
 stop_if_fatal $? bench
+if [ "${REHEARSE:-0}" = "1" ]; then   # N=2 launch path with both ranks on the one GPU
+  NBX_BENCH_DEVICE=0 NBX_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 2 --steps 10 --warmup 2 \
+    > "$OUT/bench_n2_shared.json" 2> "$OUT/bench_n2_shared.err"
+  stop_if_fatal $? bench_n2_rehearsal
+fi
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace -- \
