@@ -375,9 +375,13 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
       blockRange(total, eb, n, r, &off, &len);
     }
     if (len == 0) continue;
+    // fold order: AllReduce / ReduceScatter block r as NCCL's ring accumulates it
+    // (r+1, ..., r); Reduce as NCCL's chain toward the root (root+1, ..., root,
+    // reduce.h:44-67) for every block.
+    const int first = (p0.kind == kReduce ? p0.root : r) + 1;
     std::vector<const void*> srcs(n);
     for (int k = 0; k < n; k++) {
-      int j = (r + 1 + k) % n;
+      int j = (first + k) % n;
       srcs[k] = (const char*)parts[j].send + off * (size_t)eb;
     }
     void* dst;
@@ -703,7 +707,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
       if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, base + st + 1, base + st + 1, 1ull << left, stream));
     }
   } else {
-  // 2. direct reduce of this rank's block, ring order me+1, ..., me
+  // 2. direct reduce of this rank's block
   if (kind == kReduceScatter) {
     off = (size_t)me * count;
     len = count;
@@ -711,8 +715,11 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     blockRange(total, eb, n, me, &off, &len);
   }
   if (len > 0) {
+    // AllReduce / ReduceScatter: ring order me+1, ..., me; Reduce: chain order
+    // root+1, ..., root for every block (reduce.h:44-67)
+    const int first = (kind == kReduce ? root : me) + 1;
     std::vector<const void*> srcs(n);
-    for (int k = 0; k < n; k++) srcs[k] = sendP[(me + 1 + k) % n] + off * (size_t)eb;
+    for (int k = 0; k < n; k++) srcs[k] = sendP[(first + k) % n] + off * (size_t)eb;
     void* dst = kind == kReduceScatter ? (void*)recvP[me]
                 : kind == kReduce      ? (void*)(recvP[root] + off * (size_t)eb)
                                        : (void*)(recvP[me] + off * (size_t)eb);

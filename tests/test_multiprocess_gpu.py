@@ -106,7 +106,8 @@ def test_multiprocess_collectives(nbx, oracle, n, algo, monkeypatch):
         full = np.empty(xs[0].size, dtype=st)
         for r, (lo, hi) in enumerate(blocks):
             if hi > lo:
-                order = [(r + 1 + k) % n for k in range(n)]
+                first = (1 % n if kind == "reduce" else r) + 1   # Reduce: chain order toward root 1 % n
+                order = [(first + k) % n for k in range(n)]
                 full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
                                                   n_pre_op_srcs=n, post_op=devop == 4)[0]
         for it in range(2):

@@ -108,8 +108,9 @@ def test_user_premulsum_host_and_device_scalar(nbx, oracle, torch_gpu, comm1):
         comm1.redop_destroy(op)
 
 
-def _ring_order_reduce(oracle, xs, dtype, devop, arg, post, nranks, block_of):
-    """Oracle for the clique: block r folded in rank order r+1, ..., r."""
+def _ring_order_reduce(oracle, xs, dtype, devop, arg, post, nranks, block_of, root=None):
+    """Oracle for the clique: block r folded in rank order r+1, ..., r
+    (AllReduce / ReduceScatter), or root+1, ..., root for every block (Reduce)."""
     st = oracle.NP_STORAGE[dtype]
     count = xs[0].size
     out = np.empty(count, dtype=st)
@@ -117,7 +118,8 @@ def _ring_order_reduce(oracle, xs, dtype, devop, arg, post, nranks, block_of):
         lo, hi = block_of(r)
         if hi <= lo:
             continue
-        order = [(r + 1 + k) % nranks for k in range(nranks)]
+        first = (r if root is None else root) + 1
+        order = [(first + k) % nranks for k in range(nranks)]
         out[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
                                          n_pre_op_srcs=nranks, post_op=post)[0]
     return out
@@ -192,8 +194,19 @@ def test_clique_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, nranks):
             comms[r].reduce(tys[r].data_ptr(), root_out.data_ptr() if r == 1 else 0, count, I32, 4, 1, 0)
         nbx.group_end()
         torch.cuda.synchronize()
-        exp = _ring_order_reduce(oracle, ys, I32, 4, nranks, True, nranks, _blocks(count, 4, nranks))
+        exp = _ring_order_reduce(oracle, ys, I32, 4, nranks, True, nranks, _blocks(count, 4, nranks), root=1)
         assert np.array_equal(np_of(root_out, np.int32), exp)
+        # float Reduce: the chain order toward the root matters bitwise
+        zs = oracle.random_inputs(F32, nranks, count, seed=19)
+        tzs = [t_of(torch, z) for z in zs]
+        root_f = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].reduce(tzs[r].data_ptr(), root_f.data_ptr() if r == 0 else 0, count, F32, 0, 0, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        exp = _ring_order_reduce(oracle, zs, F32, 0, 0, False, nranks, _blocks(count, 4, nranks), root=0)
+        assert np.array_equal(np_of(root_f, np.float32), exp)
     finally:
         for c in comms:
             c.destroy()
