@@ -72,6 +72,20 @@ ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
                             nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
                             ncclStream_t stream);
 
+/* Host-staged form of nbxReduceMulti: sources and destinations in HOST memory
+ * (pinned for full speed; pageable works), the path NCCL's NET/SHM transports
+ * stage through (host-pinned proxy FIFOs net.cc:735/883, /dev/shm buffers
+ * shm.cc:86-114) — where an emulator's proxy/net buffers live. Data is chunked
+ * (NBX_HOST_CHUNK_BYTES per source, default 16 MiB) through a two-slot device
+ * staging ring so H2D, the reduction and D2H of consecutive chunks overlap.
+ * Ordered after prior work on `stream`; BLOCKING: returns when every host
+ * destination holds the result. Same semantics and errors as nbxReduceMulti. */
+ncclResult_t nbxReduceMultiHost(void* const* hostDsts, int nDsts,
+                                const void* const* hostSrcs, int nSrcs,
+                                size_t count, ncclDataType_t datatype,
+                                nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
+                                ncclStream_t stream);
+
 /* Launch knobs (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues, tuning.cc:12,
  * connect.cc:314): blocksPerCU caps the grid at CUs x blocksPerCU workgroups
  * (0 = default: 1 for big tiles, 8 for small; env NBX_BLOCKS_PER_CU);

@@ -147,6 +147,9 @@ _SIGS = {
     "nbxReduceMulti": [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                        ctypes.c_int, ctypes.c_size_t, ctypes.c_int, DevRedOpFull, ctypes.c_int, ctypes.c_int,
                        ctypes.c_void_p],
+    "nbxReduceMultiHost": [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                           ctypes.c_int, ctypes.c_size_t, ctypes.c_int, DevRedOpFull, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_void_p],
     "nbxSetLaunchConfig": [ctypes.c_int, ctypes.c_int],
     "nbxGetLaunchConfig": [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
     "nbxKernelCount": [],
@@ -254,6 +257,16 @@ def reduce_multi(dsts: Sequence[int], srcs: Sequence[int], count: int, dtype: in
                  n_pre_op_srcs: int = 0, post_op: bool = False, stream: int = 0) -> None:
     """The hot path: ordered left fold of `srcs` into every `dsts` (reduceCopy semantics)."""
     _check(reduce_multi_raw(dsts, srcs, count, dtype, op, n_pre_op_srcs, post_op, stream), "nbxReduceMulti")
+
+
+def reduce_multi_host(dsts: Sequence[int], srcs: Sequence[int], count: int, dtype: int, op: DevRedOpFull,
+                      n_pre_op_srcs: int = 0, post_op: bool = False, stream: int = 0) -> None:
+    """Host-staged reduction (host pointers in and out; blocking)."""
+    d = (ctypes.c_void_p * max(1, len(dsts)))(*[ctypes.c_void_p(int(x)) for x in dsts])
+    s = (ctypes.c_void_p * max(1, len(srcs)))(*[ctypes.c_void_p(int(x)) for x in srcs])
+    _check(load_library().nbxReduceMultiHost(d, len(dsts), s, len(srcs), int(count), int(dtype), op,
+                                             int(n_pre_op_srcs), int(bool(post_op)), ctypes.c_void_p(int(stream))),
+           "nbxReduceMultiHost")
 
 
 class Communicator:

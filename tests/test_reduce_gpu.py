@@ -286,3 +286,26 @@ def test_half_bf16_exhaustive_against_one(nbx, oracle, torch_gpu):
             b = np.random.default_rng(seed).integers(0, 65536, 65536, dtype=np.uint16)
             for devop, arg in ((0, 0), (1, 0), (2, 0), (2, 0xFFFF)):
                 run_case(nbx, oracle, torch_gpu, [a, b], dtype, devop, arg)
+
+
+@pytest.mark.parametrize("dtype,devop", [(7, 0), (6, 0), (9, 3), (2, 4), (10, 0), (8, 2)])
+@pytest.mark.parametrize("count", [1, 1000, (1 << 20) + 13, 5 << 20])
+def test_host_staged_reduce(nbx, oracle, torch_gpu, monkeypatch, dtype, devop, count):
+    """nbxReduceMultiHost: pageable numpy buffers in and out, chunked through the
+    device ring (small chunk size forces many chunks and slot reuse)."""
+    monkeypatch.setenv("NBX_HOST_CHUNK_BYTES", str(256 << 10))
+    rng = np.random.default_rng(count + dtype)
+    nsrc = 3
+    srcs = oracle.random_inputs(dtype, nsrc, count, seed=int(rng.integers(1 << 20)))
+    arg = op_arg(oracle, dtype, devop, rng)
+    npre = 2 if devop == 3 else 0
+    st = oracle.NP_STORAGE[dtype]
+    outs = [np.full(count, 0x5A, dtype=np.uint8 if np.dtype(st).itemsize == 1 else st) for _ in range(2)]
+    outs = [o.view(st) for o in outs]
+    op = nbx.DevRedOpFull()
+    op.op, op.scalarArg = devop, arg
+    nbx.reduce_multi_host([o.ctypes.data for o in outs], [s.ctypes.data for s in srcs], count, dtype, op, npre,
+                          devop == 4, torch_gpu.cuda.current_stream().cuda_stream)
+    exp = oracle.reduce_multi(srcs, dtype, devop, arg, npre, devop == 4, threads=8)[0]
+    for o in outs:
+        assert_same(o, exp, dtype)
