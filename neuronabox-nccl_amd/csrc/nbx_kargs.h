@@ -29,6 +29,7 @@ struct KArgs {
 struct KernelSet {
   const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
+  const void* ll;                   // LL-protocol AllReduce (nbx_ll.h)
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;
   int valid;

@@ -22,6 +22,7 @@
 #include <utility>
 #include "nbx_functors.h"
 #include "nbx_kargs.h"
+#include "nbx_ll.h"
 
 namespace nbx {
 
@@ -181,6 +182,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
     ks.unroll[i] = un[i];
   }
   ks.elts = (const void*)&kReduceElts<Fn>;
+  ks.ll = (const void*)&kLLAllReduce<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.valid = 1;
   return ks;

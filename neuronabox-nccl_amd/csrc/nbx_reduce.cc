@@ -22,6 +22,8 @@
 
 #include "../../include/nbx_reduce.h"
 #include "nbx_registry.h"
+#include "nbx_internal.h"
+#include "nbx_ll_args.h"
 
 using namespace nbx;
 
@@ -165,6 +167,22 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
 }
 
 }  // namespace
+
+namespace nbx {
+ncclResult_t launchLLAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
+  if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
+  const KernelSet& ks = table()[(int)dt][op.op];
+  if (!ks.valid || ks.ll == nullptr) return ncclInvalidArgument;
+  a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+  a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+  size_t grid = (a.nPacks + 255) / 256;
+  if (grid < 1) grid = 1;
+  if (grid > 1024) grid = 1024;
+  void* args[] = {&a};
+  hipError_t e = hipLaunchKernel(ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);
+  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
+}  // namespace nbx
 
 extern "C" {
 

@@ -38,6 +38,8 @@
 #include "../../include/nbx_reduce.h"
 #include "nbx_bootstrap.h"
 #include "nbx_sync.h"
+#include "nbx_internal.h"
+#include "nbx_ll_args.h"
 
 #define NBX_EXPORT extern "C" __attribute__((visibility("default")))
 // NCCL_API (src/include/core.h:17-32): every entry point plus a p-prefixed alias.
@@ -498,13 +500,34 @@ struct MpState {
   uint64_t seq = 0;
   double timeoutSec = 300.0;
   std::map<std::pair<int, std::string>, void*> maps;   // (peer, ipc handle) -> mapped base
+  // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] of 8-byte lines, peers' mapped
+  uint64_t* ll = nullptr;
+  uint64_t** peerLLDev = nullptr;
+  std::vector<void*> peerLLMaps;
+  uint64_t llMaxBytes = 0;
+  uint64_t llSlotLines = 0;
 };
 
 struct MpInitInfo {
   int32_t pid;
   int32_t device;
   hipIpcMemHandle_t flagsHandle;
+  hipIpcMemHandle_t llHandle;
+  uint64_t llMaxBytes;
 };
+
+// NCCL_PROTO (tuning.cc:254-259): "Simple" disables the LL protocol, "LL"
+// forces it for every message that fits the LL buffer; default: LL for
+// AllReduce messages up to NBX_LL_MAX_BYTES (64 KiB).
+int protoFromEnv() {   // 0 auto, 1 LL, 2 Simple
+  static const int p = [] {
+    const char* v = std::getenv("NCCL_PROTO");
+    if (v && strcasecmp(v, "simple") == 0) return 2;
+    if (v && strcasecmp(v, "ll") == 0) return 1;
+    return 0;
+  }();
+  return p;
+}
 
 struct MpCallInfo {
   uint64_t seq;
@@ -575,16 +598,35 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mp->hostWords, 0, 64);
   HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
+  // LL buffer: 2 parities x n sources x 2 lines per 8-byte pack
+  {
+    const char* v = std::getenv("NBX_LL_MAX_BYTES");
+    uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (64u << 10);
+    mx = (mx + 15) & ~(uint64_t)15;
+    if (mx < 1024) mx = 1024;
+    mp->llMaxBytes = mx;
+    mp->llSlotLines = 2 * (mx / 8);
+    const size_t llBytes = 2 * (size_t)c->nRanks * mp->llSlotLines * sizeof(uint64_t);
+    HIPCHECK(hipMalloc((void**)&mp->ll, llBytes));
+    HIPCHECK(hipMemset(mp->ll, 0, llBytes));
+  }
   MpInitInfo mine{};
   mine.pid = (int32_t)getpid();
   mine.device = c->device;
+  mine.llMaxBytes = mp->llMaxBytes;
   HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
+  HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
   std::vector<MpInitInfo> all(c->nRanks);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
-  std::vector<uint64_t*> table(c->nRanks);
+  std::vector<uint64_t*> table(c->nRanks), llTable(c->nRanks);
   for (int j = 0; j < c->nRanks; j++) {
+    if (all[j].llMaxBytes != mp->llMaxBytes) {
+      warn("ncclCommInitRank : NBX_LL_MAX_BYTES differs across ranks");
+      return ncclInvalidUsage;
+    }
     if (j == c->rank) {
       table[j] = mp->flags;
+      llTable[j] = mp->ll;
       continue;
     }
     if (all[j].device != c->device) {
@@ -600,9 +642,15 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     HIPCHECK(hipIpcOpenMemHandle(&p, all[j].flagsHandle, hipIpcMemLazyEnablePeerAccess));
     mp->peerFlagMaps.push_back(p);
     table[j] = (uint64_t*)p;
+    void* q = nullptr;
+    HIPCHECK(hipIpcOpenMemHandle(&q, all[j].llHandle, hipIpcMemLazyEnablePeerAccess));
+    mp->peerLLMaps.push_back(q);
+    llTable[j] = (uint64_t*)q;
   }
   HIPCHECK(hipMalloc((void**)&mp->peerFlagsDev, c->nRanks * sizeof(uint64_t*)));
   HIPCHECK(hipMemcpy(mp->peerFlagsDev, table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
+  HIPCHECK(hipMalloc((void**)&mp->peerLLDev, c->nRanks * sizeof(uint64_t*)));
+  HIPCHECK(hipMemcpy(mp->peerLLDev, llTable.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
   // everyone has mapped everyone before the first collective
   int dummy = 0;
   std::vector<int> sink(c->nRanks);
@@ -619,7 +667,10 @@ void mpFree(ncclComm* c) {
   (void)hipDeviceSynchronize();
   for (auto& kv : mp->maps) (void)hipIpcCloseMemHandle(kv.second);
   for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
+  for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
   if (mp->peerFlagsDev) (void)hipFree(mp->peerFlagsDev);
+  if (mp->peerLLDev) (void)hipFree(mp->peerLLDev);
+  if (mp->ll) (void)hipFree(mp->ll);
   if (mp->flags) (void)hipFree(mp->flags);
   if (mp->hostWords) (void)hipHostFree(mp->hostWords);
   nbx::bootstrapClose(mp->bs);
@@ -632,6 +683,32 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
   const int eb = typeSize(dt);
+  // LL protocol: small AllReduce in one kernel, no host exchange (nbx_ll.h)
+  const uint64_t msgBytes = (uint64_t)count * (uint64_t)eb;
+  if (kind == kAllReduce && count > 0 && protoFromEnv() != 2 && msgBytes <= mp->llMaxBytes && n <= 64 &&
+      send != nullptr && recv != nullptr && ((uintptr_t)send % 8) == 0 && ((uintptr_t)recv % 8) == 0) {
+    const uint64_t seq = ++mp->seq;
+    nbx::LLArgs la{};
+    la.send = send;
+    la.recv = recv;
+    la.count = count;
+    la.nPacks = (msgBytes + 7) / 8;
+    la.peerLL = mp->peerLLDev;
+    la.myLL = mp->ll;
+    la.slotLines = mp->llSlotLines;
+    size_t off0, per;
+    blockRange(count, eb, n, 0, &off0, &per);
+    la.blockElts = per > 0 ? per : 1;
+    la.abortWord = mp->hostWordsDev;
+    la.errWord = mp->hostWordsDev + 1;
+    la.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
+    la.flag = (uint32_t)seq;
+    la.parity = (int32_t)(seq & 1);
+    la.rank = me;
+    la.nRanks = n;
+    la.postOp = 1;
+    return nbx::launchLLAllReduce(dt, op, la, stream);
+  }
   const uint64_t seq = ++mp->seq;
   MpCallInfo mine{};
   mine.seq = seq;

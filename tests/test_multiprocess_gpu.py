@@ -194,3 +194,97 @@ def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch):
     for r in range(n):
         assert res[r][0] == exp, f"rank {r}"
     print("8-rank shared-GPU allreduce ms/call:", [round(res[r][1], 3) for r in range(n)])
+
+
+LL_CASES = [  # (dtype, op, count): all <= 64 KiB -> LL protocol; the 40000-float case -> direct
+    (7, 0, 1), (7, 0, 3), (7, 0, 1000), (7, 0, 16384), (6, 0, 17), (9, 4, 4097), (2, 4, 999), (4, 2, 4096),
+    (10, 0, 33), (1, 3, 65536), (8, 1, 8191), (7, 0, 40000),
+]
+
+
+def _ll_input(dtype, count, r):
+    from oracle import oracle
+    return oracle.random_inputs(dtype, 8, count, seed=77 + dtype + count)[r]
+
+
+def _child_ll(uid_bytes, rank, n, q):
+    try:
+        import time
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        for it in range(3):   # repeated: exercises both LL parities and LL/direct interleaving
+            for dtype, op, count in LL_CASES:
+                x = _ll_input(dtype, count, rank)
+                tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+                ty = torch.zeros_like(tx)
+                comm.all_reduce(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
+                torch.cuda.synchronize()
+                out[(it, dtype, op, count)] = ty.cpu().numpy().copy()
+        # latency of a 4 KiB fp32 AllReduce (LL): 200 back-to-back calls
+        tx = torch.rand(1024, device="cuda")
+        ty = torch.empty_like(tx)
+        for _ in range(20):
+            comm.all_reduce(tx.data_ptr(), ty.data_ptr(), 1024, 7, 0, st)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(200):
+            comm.all_reduce(tx.data_ptr(), ty.data_ptr(), 1024, 7, 0, st)
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) * 1e6 / 200
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", (out, us)))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 3, 5])
+def test_multiprocess_ll_protocol(nbx, oracle, n, monkeypatch):
+    """LL protocol (one kernel, {data, flag} lines, no host exchange) for small
+    AllReduce messages, interleaved with a direct-path message; bitwise equal to
+    the direct schedule's fold order."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    uid = nbx.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_child_ll, args=(bytes(uid), r, n, q), daemon=True) for r in range(n)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", f"rank {rank}:\n{payload}"
+            res[rank] = payload
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+    for dtype, op, count in LL_CASES:
+        xs = [_ll_input(dtype, count, r) for r in range(n)]
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        st = oracle.NP_STORAGE[dtype]
+        eb = np.dtype(st).itemsize
+        full = np.empty(count, dtype=st)
+        for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+            if hi > lo:
+                order = [(c + 1 + k) % n for k in range(n)]
+                full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
+                                                  n_pre_op_srcs=n, post_op=devop == 4)[0]
+        for it in range(3):
+            for r in range(n):
+                got = res[r][0][(it, dtype, op, count)]
+                assert np.array_equal(got, full.view(np.uint8)), (it, dtype, op, count, r)
+    print(f"LL 4 KiB fp32 allreduce, {n} ranks sharing one GPU: us/call =",
+          [round(res[r][1], 1) for r in range(n)])
