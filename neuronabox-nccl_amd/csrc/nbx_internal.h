@@ -6,6 +6,8 @@
 
 namespace nbx {
 struct LLArgs;
-// Launch the LL-protocol AllReduce kernel of (datatype, op) (nbx_ll.h).
-ncclResult_t launchLLAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
+// Launch the LL collective kernel of (datatype, op) (nbx_ll.h); sets args.arriveTarget from *arrived and
+// advances it by the grid size.
+ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t* arrived,
+                          hipStream_t stream);
 }  // namespace nbx

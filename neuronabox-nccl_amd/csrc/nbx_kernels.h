@@ -182,7 +182,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
     ks.unroll[i] = un[i];
   }
   ks.elts = (const void*)&kReduceElts<Fn>;
-  ks.ll = (const void*)&kLLAllReduce<Fn>;
+  ks.ll = (const void*)&kLLColl<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.valid = 1;
   return ks;

@@ -1,32 +1,38 @@
-// nbx_ll.h — LL ("low latency") protocol AllReduce for small messages on the
-// multi-process communicator: one kernel, no host exchange per call.
+// nbx_ll.h — LL ("low latency") protocol for small messages on the
+// multi-process communicator: one kernel per collective, no host exchange.
 //
 // Wire format (the idea of NCCL's LL protocol, prims_ll.h:226-294 /
 // device.h ncclLLFifoLine): every 8-byte line is {u32 data, u32 flag} written
 // by ONE 64-bit system-scope store, so a reader that sees flag == seq also
 // sees that line's data (single-copy atomicity; no separate flag, no fence).
-// Each rank owns an IPC-registered LL buffer laid out
-//   [parity 2][source rank n][lines 2 * maxPacks]   (8-byte lines)
+// Each rank owns an IPC-registered, uncached LL buffer laid out
+//   [parity 2][source rank n][lines 2 * maxPacks]   data lines (8 bytes)
+//   [done n]                                        done words, one per writer
+//   [arrive 1]                                      local block-arrival counter
 // and the kernel of rank r
+//   0. waits until every peer it pushes to has finished reading the last LL
+//      call that used this parity (that peer's done word >= needDone) — the
+//      credit that makes a slot reusable even when a rank never waits for
+//      data (Reduce non-roots);
 //   1. pushes its message, 8 bytes per thread, as two lines into slot
-//      [seq & 1][r] of every peer's buffer (remote stores over xGMI);
-//   2. polls its own buffer's slots [seq & 1][j] for every peer j until the
-//      flags equal seq (bounded spin: timeout + abort word), reads its own
-//      contribution from `send`, and folds all n sources per element in the
-//      direct schedule's order (element in block c: ranks c+1, ..., c), so the
-//      result is bitwise the direct path's;
-//   3. stores the full result to `recv` — every rank computes the whole
-//      message, so there is no gather phase.
-// Parity buffers + stream order make reuse safe: a rank writes parity p again
-// only at seq+2, after it has seen every peer's seq+1 lines (LL) or passed the
-// seq+1 done-barrier (direct), i.e. after every peer finished reading seq.
+//      [seq & 1][r] of each target's buffer (remote stores over xGMI):
+//        AllReduce      — the whole message to every peer
+//        ReduceScatter  — send block j (recvcount elements) to peer j
+//        Reduce         — the whole message to the root only;
+//   2. polls its own slots [seq & 1][j] until the flags equal seq (bounded
+//      spin: timeout + abort word), takes its own contribution from `send`,
+//      and folds all n sources per element in the direct schedule's order so
+//      the result is bitwise the direct path's:
+//        AllReduce      — element in block c: ranks c+1, ..., c
+//        ReduceScatter  — ranks r+1, ..., r       (reduce_scatter.h:50-64)
+//        Reduce (root)  — ranks root+1, ..., root (reduce.h:44-67);
+//   3. stores the result; the last block to finish publishes this rank's
+//      done word (= seq) into every peer's buffer.
 #pragma once
 #include "nbx_functors.h"
 #include "nbx_ll_args.h"
 
 namespace nbx {
-
-
 
 template <class Fn>
 __device__ __forceinline__ uint64_t llLoadArg(const LLArgs& a) {
@@ -34,69 +40,117 @@ __device__ __forceinline__ uint64_t llLoadArg(const LLArgs& a) {
   return a.arg;
 }
 
-// 8 bytes of `p` starting at byte `off`, zero past `limit`
+// 8 bytes of `p` starting at byte `off`, zero past `limit` (any alignment)
 __device__ __forceinline__ uint64_t llLoadBytes(const unsigned char* p, uint64_t off, uint64_t limit) {
-  if (off + 8 <= limit) return *(const uint64_t*)(p + off);
+  if (off + 8 <= limit && (((uintptr_t)(p + off)) & 7u) == 0) return *(const uint64_t*)(p + off);
   uint64_t v = 0;
   for (int b = 0; b < 8; b++)
     if (off + b < limit) v |= (uint64_t)p[off + b] << (8 * b);
   return v;
 }
 
+__device__ __forceinline__ void llStoreBytes(unsigned char* p, uint64_t off, uint64_t limit, uint64_t v) {
+  if (off + 8 <= limit && (((uintptr_t)(p + off)) & 7u) == 0) {
+    *(uint64_t*)(p + off) = v;
+    return;
+  }
+  for (int b = 0; b < 8; b++)
+    if (off + b < limit) p[off + b] = (unsigned char)(v >> (8 * b));
+}
+
+// Bounded spin until *w >= target; false on timeout/abort.
+__device__ __forceinline__ bool llWait(const uint64_t* w, uint64_t target, const LLArgs& a, uint64_t t0) {
+  uint32_t spins = 0;
+  for (;;) {
+    const uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v >= target) return true;
+    if ((++spins & 1023u) == 0u) {
+      if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
+        *a.errWord = *a.abortWord != 0 ? 2 : 1;
+        return false;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool llIsTarget(const LLArgs& a, int j) {
+  if (j == a.rank) return false;
+  return a.mode != kLLReduce || j == a.root;
+}
+
 template <class Fn>
-__global__ __launch_bounds__(256) void kLLAllReduce(LLArgs a) {
+__global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPK = 8 / (int)sizeof(E);   // elements per 8-byte pack
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
-  const uint64_t bytes = a.count * sizeof(E);
+  const uint64_t bytes = a.count * sizeof(E);   // bytes per slot
   const uint64_t flagHi = (uint64_t)a.flag << 32;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = wall_clock64();
-  bool failed = false;
+  __shared__ int sFailed;
+  if (threadIdx.x == 0) sFailed = 0;
+  __syncthreads();
 
-  // 1. push: two {data, flag} lines per pack into every peer's slot [parity][me]
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nPacks; k += stride) {
-    const uint64_t v = llLoadBytes((const unsigned char*)a.send, k * 8, bytes);
-    const uint64_t l0 = (v & 0xffffffffull) | flagHi, l1 = (v >> 32) | flagHi;
-    for (int j = 0; j < n; j++) {
-      if (j == me) continue;
-      uint64_t* line = a.peerLL[j] + ((uint64_t)(a.parity * n + me) * a.slotLines + 2 * k);
-      __hip_atomic_store(line, l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(line + 1, l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 0. credits: each target has finished reading this parity's previous use
+  if (a.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, a.needDone, a, t0)) sFailed = 1;
+  }
+  __syncthreads();
+  bool failed = sFailed != 0;
+
+  // 1. push two {data, flag} lines per pack into each target's slot [parity][me]
+  if (!failed) {
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nPacks; k += stride) {
+      uint64_t whole = 0;
+      if (a.mode != kLLReduceScatter) whole = llLoadBytes((const unsigned char*)a.send, k * 8, bytes);
+      for (int j = 0; j < n; j++) {
+        if (!llIsTarget(a, j)) continue;
+        const uint64_t v = a.mode == kLLReduceScatter
+                               ? llLoadBytes((const unsigned char*)a.send + (uint64_t)j * bytes, k * 8, bytes)
+                               : whole;
+        const uint64_t l0 = (v & 0xffffffffull) | flagHi, l1 = (v >> 32) | flagHi;
+        uint64_t* line = a.peerLL[j] + ((uint64_t)(a.parity * n + me) * a.slotLines + 2 * k);
+        __hip_atomic_store(line, l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(line + 1, l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 
   // 2.+3. poll own slots, fold in the direct order, store the result
-  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nPacks; k += stride) {
+  const bool receives = a.mode != kLLReduce || me == a.root;
+  const unsigned char* own = (const unsigned char*)a.send + (a.mode == kLLReduceScatter ? (uint64_t)me * bytes : 0);
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; receives && k < a.nPacks; k += stride) {
     union Pk {
       uint64_t u;
       E e[EPK];
     };
-    const uint64_t firstElt = k * EPK;
-    const int c = (int)(firstElt / a.blockElts);       // packs never straddle 16-B-aligned blocks
-    const int first = (c + 1) % n;
+    int first;
+    if (a.mode == kLLAllReduce) {
+      const int c = (int)((k * EPK) / a.blockElts);   // packs never straddle 16-B-aligned blocks
+      first = (c + 1) % n;
+    } else {
+      first = ((a.mode == kLLReduce ? a.root : me) + 1) % n;
+    }
     Pk acc;
     acc.u = 0;
     for (int q = 0; q < n; q++) {
       const int j = (first + q) % n;
       Pk x;
       if (j == me) {
-        x.u = llLoadBytes((const unsigned char*)a.send, k * 8, bytes);
+        x.u = llLoadBytes(own, k * 8, bytes);
       } else {
         const uint64_t* line = a.myLL + ((uint64_t)(a.parity * n + j) * a.slotLines + 2 * k);
-        uint64_t l0, l1;
+        uint64_t l0 = 0, l1 = 0;
         uint32_t spins = 0;
-        for (;;) {
+        while (!failed) {
           l0 = __hip_atomic_load(line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           l1 = __hip_atomic_load(line + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((uint32_t)(l0 >> 32) == a.flag && (uint32_t)(l1 >> 32) == a.flag) break;
-          if (failed) break;
           if ((++spins & 1023u) == 0u) {
             if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
               *a.errWord = *a.abortWord != 0 ? 2 : 1;
               failed = true;
-              break;
             }
           }
         }
@@ -115,12 +169,19 @@ __global__ __launch_bounds__(256) void kLLAllReduce(LLArgs a) {
         for (int e = 0; e < EPK; e++) acc.e[e] = fn.post(acc.e[e]);
       }
     }
-    unsigned char* out = (unsigned char*)a.recv;
-    if (k * 8 + 8 <= bytes) {
-      *(uint64_t*)(out + k * 8) = acc.u;
-    } else {
-      for (int b = 0; b < 8; b++)
-        if (k * 8 + b < bytes) out[k * 8 + b] = (unsigned char)(acc.u >> (8 * b));
+    llStoreBytes((unsigned char*)a.recv, k * 8, bytes, acc.u);
+  }
+
+  // done word: after every block of this launch has consumed its lines
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t prev = __hip_atomic_fetch_add(a.arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1 == a.arriveTarget) {
+      for (int j = 0; j < n; j++) {
+        if (j == me) continue;
+        __hip_atomic_store(a.peerLL[j] + a.doneOff + me, a.seq, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }

@@ -1,19 +1,26 @@
-// nbx_ll_args.h — kernel arguments of the LL-protocol AllReduce (nbx_ll.h);
+// nbx_ll_args.h — kernel arguments of the LL-protocol collectives (nbx_ll.h);
 // device-free so host units can fill them.
 #pragma once
 #include <stdint.h>
 
 namespace nbx {
 
+enum LLMode : int32_t { kLLAllReduce = 0, kLLReduceScatter = 1, kLLReduce = 2 };
+
 struct LLArgs {
   const void* send;
   void* recv;
-  uint64_t count;          // elements
-  uint64_t nPacks;         // 8-byte packs covering count elements
+  uint64_t count;          // elements per slot: AllReduce/Reduce = count, ReduceScatter = recvcount
+  uint64_t nPacks;         // 8-byte packs covering `count` elements
   uint64_t* const* peerLL; // device table: rank -> LL buffer base
   uint64_t* myLL;
   uint64_t slotLines;      // lines per (parity, source) slot = 2 * max packs
-  uint64_t blockElts;      // direct-schedule block size (elements) -> fold order
+  uint64_t doneOff;        // line index of the done words (one per writer rank) in every LL buffer
+  uint64_t* arrive;        // local block-arrival counter (monotonic)
+  uint64_t arriveTarget;   // counter value after the last block of this launch arrives
+  uint64_t needDone;       // before pushing to peer j: wait until j's done word >= needDone
+  uint64_t seq;            // this call's sequence number (published as the done word)
+  uint64_t blockElts;      // AllReduce: direct-schedule block size (elements) -> fold order
   uint64_t arg;            // functor scalar (by value)
   const void* argPtr;      // device scalar or nullptr
   const volatile int* abortWord;
@@ -24,6 +31,8 @@ struct LLArgs {
   int32_t rank;
   int32_t nRanks;
   int32_t postOp;
+  int32_t mode;            // LLMode
+  int32_t root;            // kLLReduce
 };
 
 }  // namespace nbx

@@ -169,7 +169,8 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
 }  // namespace
 
 namespace nbx {
-ncclResult_t launchLLAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
+ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, uint64_t* arrived,
+                          hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
   if (!ks.valid || ks.ll == nullptr) return ncclInvalidArgument;
@@ -178,9 +179,12 @@ ncclResult_t launchLLAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, LLA
   size_t grid = (a.nPacks + 255) / 256;
   if (grid < 1) grid = 1;
   if (grid > 1024) grid = 1024;
+  a.arriveTarget = *arrived + grid;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);
-  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+  if (e != hipSuccess) return ncclUnhandledCudaError;
+  *arrived = a.arriveTarget;
+  return ncclSuccess;
 }
 }  // namespace nbx
 

@@ -500,12 +500,16 @@ struct MpState {
   uint64_t seq = 0;
   double timeoutSec = 300.0;
   std::map<std::pair<int, std::string>, void*> maps;   // (peer, ipc handle) -> mapped base
-  // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] of 8-byte lines, peers' mapped
+  // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] lines + [n] done words +
+  // arrival counter; peers' buffers mapped
   uint64_t* ll = nullptr;
   uint64_t** peerLLDev = nullptr;
   std::vector<void*> peerLLMaps;
   uint64_t llMaxBytes = 0;
   uint64_t llSlotLines = 0;
+  uint64_t llDoneOff = 0;
+  uint64_t llLastSeq[2] = {0, 0};   // last LL call per parity (credit target)
+  uint64_t llArrived = 0;           // arrival-counter value after the last LL launch
 };
 
 struct MpInitInfo {
@@ -518,7 +522,8 @@ struct MpInitInfo {
 
 // NCCL_PROTO (tuning.cc:254-259): "Simple" disables the LL protocol, "LL"
 // forces it for every message that fits the LL buffer; default: LL for
-// AllReduce messages up to NBX_LL_MAX_BYTES (64 KiB).
+// AllReduce / ReduceScatter / Reduce messages (per-rank block for
+// ReduceScatter) up to NBX_LL_MAX_BYTES (64 KiB).
 int protoFromEnv() {   // 0 auto, 1 LL, 2 Simple
   static const int p = [] {
     const char* v = std::getenv("NCCL_PROTO");
@@ -587,13 +592,27 @@ Algo algoFromEnv() {
   return a;
 }
 
+// Memory that other GPUs write and this GPU polls (barrier flags, LL lines).
+// Uncached (fine-grained, MTYPE UC) by default: a peer's system-scope store
+// over xGMI lands in HBM and no XCD L2 can hold a stale copy, which is what
+// RCCL uses for its flags too. NBX_SYNC_MEM=coarse selects plain hipMalloc
+// (A/B measurement only).
+hipError_t allocSyncMem(void** p, size_t bytes) {
+  static const bool coarse = [] {
+    const char* v = std::getenv("NBX_SYNC_MEM");
+    return v && strcasecmp(v, "coarse") == 0;
+  }();
+  if (coarse) return hipMalloc(p, bytes);
+  return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+}
+
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   MpState* mp = new MpState();
   c->mp = mp;
   const char* t = std::getenv("NBX_TIMEOUT_SEC");
   if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
   NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
-  HIPCHECK(hipMalloc((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
+  HIPCHECK(allocSyncMem((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
   HIPCHECK(hipMemset(mp->flags, 0, kNumSlots * sizeof(uint64_t)));
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mp->hostWords, 0, 64);
@@ -606,8 +625,9 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     if (mx < 1024) mx = 1024;
     mp->llMaxBytes = mx;
     mp->llSlotLines = 2 * (mx / 8);
-    const size_t llBytes = 2 * (size_t)c->nRanks * mp->llSlotLines * sizeof(uint64_t);
-    HIPCHECK(hipMalloc((void**)&mp->ll, llBytes));
+    mp->llDoneOff = 2 * (uint64_t)c->nRanks * mp->llSlotLines;
+    const size_t llBytes = (mp->llDoneOff + (uint64_t)c->nRanks + 1) * sizeof(uint64_t);
+    HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes));
     HIPCHECK(hipMemset(mp->ll, 0, llBytes));
   }
   MpInitInfo mine{};
@@ -683,19 +703,29 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
   const int eb = typeSize(dt);
-  // LL protocol: small AllReduce in one kernel, no host exchange (nbx_ll.h)
-  const uint64_t msgBytes = (uint64_t)count * (uint64_t)eb;
-  if (kind == kAllReduce && count > 0 && protoFromEnv() != 2 && msgBytes <= mp->llMaxBytes && n <= 64 &&
-      send != nullptr && recv != nullptr && ((uintptr_t)send % 8) == 0 && ((uintptr_t)recv % 8) == 0) {
+  // LL protocol: small collectives in one kernel, no host exchange (nbx_ll.h).
+  // The choice depends only on arguments every rank passes identically.
+  const uint64_t slotBytes = (uint64_t)count * (uint64_t)eb;   // RS: recvcount per block
+  if (count > 0 && protoFromEnv() != 2 && slotBytes <= mp->llMaxBytes && n <= 64) {
+    if (send == nullptr || (recv == nullptr && (kind != kReduce || me == root))) {
+      warn("rank %d passed a NULL buffer", me);
+      return ncclInvalidArgument;
+    }
     const uint64_t seq = ++mp->seq;
     nbx::LLArgs la{};
     la.send = send;
     la.recv = recv;
     la.count = count;
-    la.nPacks = (msgBytes + 7) / 8;
+    la.nPacks = (slotBytes + 7) / 8;
     la.peerLL = mp->peerLLDev;
     la.myLL = mp->ll;
     la.slotLines = mp->llSlotLines;
+    la.doneOff = mp->llDoneOff;
+    la.arrive = mp->ll + mp->llDoneOff + n;
+    la.parity = (int32_t)(seq & 1);
+    la.needDone = mp->llLastSeq[la.parity];
+    mp->llLastSeq[la.parity] = seq;
+    la.seq = seq;
     size_t off0, per;
     blockRange(count, eb, n, 0, &off0, &per);
     la.blockElts = per > 0 ? per : 1;
@@ -703,11 +733,12 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     la.errWord = mp->hostWordsDev + 1;
     la.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
     la.flag = (uint32_t)seq;
-    la.parity = (int32_t)(seq & 1);
     la.rank = me;
     la.nRanks = n;
     la.postOp = 1;
-    return nbx::launchLLAllReduce(dt, op, la, stream);
+    la.mode = kind == kAllReduce ? nbx::kLLAllReduce : kind == kReduceScatter ? nbx::kLLReduceScatter : nbx::kLLReduce;
+    la.root = root;
+    return nbx::launchLLColl(dt, op, la, &mp->llArrived, stream);
   }
   const uint64_t seq = ++mp->seq;
   MpCallInfo mine{};

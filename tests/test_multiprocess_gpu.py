@@ -196,15 +196,29 @@ def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch):
     print("8-rank shared-GPU allreduce ms/call:", [round(res[r][1], 3) for r in range(n)])
 
 
-LL_CASES = [  # (dtype, op, count): all <= 64 KiB -> LL protocol; the 40000-float case -> direct
-    (7, 0, 1), (7, 0, 3), (7, 0, 1000), (7, 0, 16384), (6, 0, 17), (9, 4, 4097), (2, 4, 999), (4, 2, 4096),
-    (10, 0, 33), (1, 3, 65536), (8, 1, 8191), (7, 0, 40000),
+# (kind, dtype, op, count, byte offset of send/recv): all <= 64 KiB per slot -> LL
+# protocol; the 40000-float AllReduce and the 20000-float ReduceScatter -> direct.
+# Reduce to a changing root back to back exercises the done-word credits (a
+# non-root never waits for data, so only the credits stop it from overwriting a
+# slot the root has not read yet).
+LL_CASES = [
+    ("ar", 7, 0, 1, 0), ("ar", 7, 0, 3, 0), ("ar", 7, 0, 1000, 0), ("ar", 7, 0, 16384, 0), ("ar", 6, 0, 17, 0),
+    ("ar", 9, 4, 4097, 0), ("ar", 2, 4, 999, 0), ("ar", 4, 2, 4096, 0), ("ar", 10, 0, 33, 0),
+    ("ar", 1, 3, 65536, 0), ("ar", 8, 1, 8191, 0), ("ar", 7, 0, 40000, 0), ("ar", 7, 0, 1001, 4),
+    ("ar", 0, 0, 77, 3), ("rs", 7, 0, 1000, 0), ("rs", 6, 4, 333, 2), ("rs", 0, 2, 5, 1), ("rs", 4, 4, 4096, 0),
+    ("rs", 7, 0, 20000, 0), ("red", 7, 0, 1000, 0), ("red", 9, 4, 777, 0), ("red", 2, 3, 64, 0),
+    ("red", 7, 0, 123, 4), ("red", 7, 1, 4096, 0), ("ar", 7, 0, 64, 0),
 ]
 
 
-def _ll_input(dtype, count, r):
+def _ll_input(kind, dtype, count, n, r):
     from oracle import oracle
-    return oracle.random_inputs(dtype, 8, count, seed=77 + dtype + count)[r]
+    total = count * n if kind == "rs" else count
+    return oracle.random_inputs(dtype, 8, total, seed=77 + dtype + count)[r]
+
+
+def _ll_root(i, n):
+    return (i * 3 + 1) % n
 
 
 def _child_ll(uid_bytes, rank, n, q):
@@ -220,13 +234,24 @@ def _child_ll(uid_bytes, rank, n, q):
         st = torch.cuda.current_stream().cuda_stream
         out = {}
         for it in range(3):   # repeated: exercises both LL parities and LL/direct interleaving
-            for dtype, op, count in LL_CASES:
-                x = _ll_input(dtype, count, rank)
-                tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
-                ty = torch.zeros_like(tx)
-                comm.all_reduce(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
-                torch.cuda.synchronize()
-                out[(it, dtype, op, count)] = ty.cpu().numpy().copy()
+            keep = []
+            for i, (kind, dtype, op, count, shift) in enumerate(LL_CASES):
+                x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
+                tx = torch.zeros(x.size + 16, dtype=torch.uint8, device="cuda")
+                tx[shift:shift + x.size] = torch.from_numpy(x.copy()).cuda()
+                out_bytes = x.size // n if kind == "rs" else x.size
+                ty = torch.zeros(out_bytes + 16, dtype=torch.uint8, device="cuda")
+                sp, rp = tx.data_ptr() + shift, ty.data_ptr() + shift
+                if kind == "ar":
+                    comm.all_reduce(sp, rp, count, dtype, op, st)
+                elif kind == "rs":
+                    comm.reduce_scatter(sp, rp, count, dtype, op, st)
+                else:
+                    comm.reduce(sp, rp, count, dtype, op, _ll_root(i, n), st)
+                keep.append((i, ty, shift, out_bytes))   # no sync between calls: ranks run ahead
+            torch.cuda.synchronize()
+            for i, ty, shift, nb in keep:
+                out[(it, i)] = ty[shift:shift + nb].cpu().numpy().copy()
         # latency of a 4 KiB fp32 AllReduce (LL): 200 back-to-back calls
         tx = torch.rand(1024, device="cuda")
         ty = torch.empty_like(tx)
@@ -249,8 +274,9 @@ def _child_ll(uid_bytes, rank, n, q):
 @pytest.mark.parametrize("n", [2, 3, 5])
 def test_multiprocess_ll_protocol(nbx, oracle, n, monkeypatch):
     """LL protocol (one kernel, {data, flag} lines, no host exchange) for small
-    AllReduce messages, interleaved with a direct-path message; bitwise equal to
-    the direct schedule's fold order."""
+    AllReduce / ReduceScatter / Reduce messages, misaligned buffers included,
+    issued back to back without host synchronisation and interleaved with
+    direct-path messages; bitwise equal to the direct schedule's fold order."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     uid = nbx.get_unique_id()
@@ -271,20 +297,32 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, monkeypatch):
         for p in procs:
             if p.is_alive():
                 p.terminate()
-    for dtype, op, count in LL_CASES:
-        xs = [_ll_input(dtype, count, r) for r in range(n)]
+    for i, (kind, dtype, op, count, shift) in enumerate(LL_CASES):
+        xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
         devop, arg = oracle.host_to_dev_redop(op, dtype, n)
         st = oracle.NP_STORAGE[dtype]
         eb = np.dtype(st).itemsize
-        full = np.empty(count, dtype=st)
-        for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
-            if hi > lo:
-                order = [(c + 1 + k) % n for k in range(n)]
-                full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
-                                                  n_pre_op_srcs=n, post_op=devop == 4)[0]
-        for it in range(3):
+        kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+        exp = {}
+        if kind == "ar":
+            full = np.empty(count, dtype=st)
+            for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+                if hi > lo:
+                    order = [(c + 1 + k) % n for k in range(n)]
+                    full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg, **kw)[0]
+            exp = {r: full for r in range(n)}
+        elif kind == "rs":
             for r in range(n):
-                got = res[r][0][(it, dtype, op, count)]
-                assert np.array_equal(got, full.view(np.uint8)), (it, dtype, op, count, r)
+                order = [(r + 1 + k) % n for k in range(n)]
+                exp[r] = oracle.reduce_multi([xs[j][r * count:(r + 1) * count] for j in order], dtype, devop, arg,
+                                             **kw)[0]
+        else:
+            root = _ll_root(i, n)
+            order = [(root + 1 + k) % n for k in range(n)]
+            exp[root] = oracle.reduce_multi([xs[j] for j in order], dtype, devop, arg, **kw)[0]
+        for it in range(3):
+            for r, e in exp.items():
+                got = res[r][0][(it, i)]
+                assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (it, kind, dtype, op, count, r)
     print(f"LL 4 KiB fp32 allreduce, {n} ranks sharing one GPU: us/call =",
           [round(res[r][1], 1) for r in range(n)])
