@@ -19,13 +19,23 @@ Extra JSON fields:
   cpu_baseline — the oracle's C restatement (oracle/reduce_oracle.c, a port of
                  the reference semantics) timed on this box's host cores on a
                  bounded sample of the same workload (rank 0, N=1 only).
+  collective   — N > 1 only, after the timed region: SURVEY §8(d) config D
+                 (ncclAllReduce direct + ring, ncclReduceScatter, 1 GiB fp32
+                 per rank, and a 4 KiB LL AllReduce) through libnbxccl's
+                 multi-process communicator across the N GPUs, checked exactly;
+                 run in a child process per rank (scripts/collective_leg.py) so
+                 a failure there is reported here instead of ending the bench.
+                 NBX_BENCH_COLLECTIVE=0 skips it.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import select
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -124,6 +134,108 @@ def cpu_baseline(seconds: float = 1.5):
                       f"{el:.2f} s wall x {threads} threads, oracle/reduce_oracle.c (gcc -O3)"}
 
 
+def _spawn_collective_leg(world: int, script: str | None = None):
+    """Start this rank's collective-leg child before the parent touches the GPU."""
+    if world <= 1 or os.environ.get("NBX_BENCH_COLLECTIVE", "1") == "0":
+        return None
+    script = script or os.path.join(ROOT, "scripts", "collective_leg.py")
+    log = tempfile.NamedTemporaryFile(prefix=f"nbx_coll_leg_r{os.environ.get('RANK', '0')}_", suffix=".log",
+                                      delete=False)
+    child = subprocess.Popen([sys.executable, script],
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=log, text=True, bufsize=1,
+                             cwd=ROOT)
+    child.nbx_log = log.name
+    return child
+
+
+def _read_line(child, prefix: str, timeout: float):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        r, _, _ = select.select([child.stdout], [], [], max(0.0, deadline - time.monotonic()))
+        if not r:
+            break
+        line = child.stdout.readline()
+        if not line:
+            return None   # child exited
+        if line.startswith(prefix + " "):
+            return line[len(prefix) + 1:].strip()
+    return None
+
+
+def _log_tail(child, n=5):
+    try:
+        with open(child.nbx_log) as f:
+            return " | ".join(f.read().strip().splitlines()[-n:])
+    except OSError:
+        return ""
+
+
+def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
+    """Drive the child through config D; every rank returns; rank 0 gets the summary."""
+    import torch.distributed as dist
+    ids = None
+    if rank == 0:
+        try:
+            child.stdin.write("ID\n")
+            child.stdin.flush()
+            ids = _read_line(child, "ID", 180)
+        except OSError:
+            ids = None
+    box = [ids]
+    dist.broadcast_object_list(box, src=0)
+    ids = box[0]
+    res = None
+    if ids is not None:
+        try:
+            child.stdin.write(f"RUN {ids}\n")
+            child.stdin.flush()
+            line = _read_line(child, "RESULT", result_timeout)
+            res = json.loads(line) if line else None
+        except (OSError, ValueError):
+            res = None
+    got = res is not None
+    try:
+        child.stdin.close()
+    except OSError:
+        pass
+    try:
+        child.wait(timeout=60 if got else 1)
+    except subprocess.TimeoutExpired:
+        child.kill()   # this rank's own child, by PID
+        child.wait()
+    if not got:
+        res = {"rank": rank, "ok": False, "errors": ["no result from the collective leg: " + _log_tail(child)]}
+    allres = [None] * world
+    dist.all_gather_object(allres, res)
+    if rank != 0:
+        return None
+    S = COUNT_D * 4
+    out = {"workload": "config D: 1 GiB fp32 per rank, ncclSum, one process per GPU, libnbxccl multi-process "
+                       "communicator (TCP bootstrap, hipIpc peer buffers, device flags)",
+           "n_ranks": world, "ok": all(r.get("ok") for r in allres),
+           "check": "exact (small-integer fp32 inputs), whole output, every rank"}
+    errs = [f"rank {r.get('rank')}: {e}" for r in allres for e in r.get("errors", [])]
+    if errs:
+        out["errors"] = errs[:8]
+
+    def agg(key, busfac, alg_bytes):
+        vals = [r.get(key) for r in allres]
+        if any(v is None for v in vals):
+            return None
+        ms = max(vals)
+        alg = alg_bytes / (ms * 1e-3) / 1e9
+        return {"ms": round(ms, 4), "algbw_GBs": round(alg, 2), "busbw_GBs": round(alg * busfac, 2)}
+    out["allreduce_direct"] = agg("allreduce_direct_ms", 2 * (world - 1) / world, S)
+    out["allreduce_ring"] = agg("allreduce_ring_ms", 2 * (world - 1) / world, S)
+    out["reduce_scatter"] = agg("reduce_scatter_ms", (world - 1) / world, S)
+    ll = [r.get("ll_allreduce_4KiB_us") for r in allres]
+    out["ll_allreduce_4KiB_us"] = None if any(v is None for v in ll) else round(max(ll), 2)
+    return out
+
+
+COUNT_D = 256 << 20   # config D: fp32 elements per rank (1 GiB)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,6 +246,7 @@ def main():
     ap.add_argument("--check", action="store_true", help="verify step output against the oracle (sampled)")
     args = ap.parse_args()
 
+    child = _spawn_collective_leg(int(os.environ.get("WORLD_SIZE", "1")))
     import torch
     world, rank, local = _dist_init()
     if args.gpus != world and world > 1:
@@ -211,9 +324,15 @@ def main():
                      "kernel": "kReducePacks<FnSumF<TyF32>, NSRC=8, U=4>", "kernel_avg_ms": round(kern_avg_ms, 5),
                      "alg_bytes_per_launch": ALG_BYTES},
         "cpu_baseline": None,
+        "collective": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if child is not None:
         del srcs, out
+        torch.cuda.empty_cache()
+        result["collective"] = collective_leg(child, world, rank)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if child is None:
+            del srcs, out
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -180,6 +180,14 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         raise ImportError(
             f"libnbxccl.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(make -C neuronabox-nccl_amd/csrc). There is no CPU fallback.")
+    # One HIP runtime per process: PyTorch-ROCm wheels ship their own
+    # libamdhip64 (soname libamdhip64.so.7, loaded by file name). Loading torch
+    # first makes libnbxccl's libamdhip64.so.7 dependency resolve to that copy;
+    # the other order maps two runtimes and the second sees no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
     for name, args in _SIGS.items():
         fn = getattr(lib, name)

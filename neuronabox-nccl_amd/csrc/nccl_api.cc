@@ -510,6 +510,8 @@ struct MpState {
   uint64_t llDoneOff = 0;
   uint64_t llLastSeq[2] = {0, 0};   // last LL call per parity (credit target)
   uint64_t llArrived = 0;           // arrival-counter value after the last LL launch
+  int proto = 0;                    // NCCL_PROTO at init: 0 auto, 1 LL, 2 Simple
+  bool ring = false;                // NCCL_ALGO=Ring at init
 };
 
 struct MpInitInfo {
@@ -524,14 +526,12 @@ struct MpInitInfo {
 // forces it for every message that fits the LL buffer; default: LL for
 // AllReduce / ReduceScatter / Reduce messages (per-rank block for
 // ReduceScatter) up to NBX_LL_MAX_BYTES (64 KiB).
+// Read when the communicator is created (as NCCL reads its tuning env at init).
 int protoFromEnv() {   // 0 auto, 1 LL, 2 Simple
-  static const int p = [] {
-    const char* v = std::getenv("NCCL_PROTO");
-    if (v && strcasecmp(v, "simple") == 0) return 2;
-    if (v && strcasecmp(v, "ll") == 0) return 1;
-    return 0;
-  }();
-  return p;
+  const char* v = std::getenv("NCCL_PROTO");
+  if (v && strcasecmp(v, "simple") == 0) return 2;
+  if (v && strcasecmp(v, "ll") == 0) return 1;
+  return 0;
 }
 
 struct MpCallInfo {
@@ -580,16 +580,13 @@ ncclResult_t mpBarrier(ncclComm* comm, int slot, uint64_t seq, hipStream_t strea
   return mpSignalWait(comm, slot, seq, seq, all, stream);
 }
 
-enum class Algo { Direct, Ring };
 
 // NCCL_ALGO (tuning.cc:254-259): "Ring" selects the ring schedule for
 // AllReduce; anything else (default) the one-shot direct exchange.
-Algo algoFromEnv() {
-  static const Algo a = [] {
-    const char* v = std::getenv("NCCL_ALGO");
-    return (v && strcasecmp(v, "ring") == 0) ? Algo::Ring : Algo::Direct;
-  }();
-  return a;
+// Read when the communicator is created.
+bool algoRingFromEnv() {
+  const char* v = std::getenv("NCCL_ALGO");
+  return v && strcasecmp(v, "ring") == 0;
 }
 
 // Memory that other GPUs write and this GPU polls (barrier flags, LL lines).
@@ -611,6 +608,8 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   c->mp = mp;
   const char* t = std::getenv("NBX_TIMEOUT_SEC");
   if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
+  mp->proto = protoFromEnv();
+  mp->ring = algoRingFromEnv();
   NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
   HIPCHECK(allocSyncMem((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
   HIPCHECK(hipMemset(mp->flags, 0, kNumSlots * sizeof(uint64_t)));
@@ -652,11 +651,15 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     if (all[j].device != c->device) {
       int can = 0;
       HIPCHECK(hipDeviceCanAccessPeer(&can, c->device, all[j].device));
-      if (can) {
-        hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
-        (void)hipGetLastError();
+      if (!can) {
+        // every data path here is a kernel load/store of peer memory; there is
+        // no host-staged transport, so fail cleanly instead of faulting later
+        warn("ncclCommInitRank : device %d cannot access peer device %d (no P2P)", c->device, all[j].device);
+        return ncclSystemError;
       }
+      hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+      (void)hipGetLastError();
     }
     void* p = nullptr;
     HIPCHECK(hipIpcOpenMemHandle(&p, all[j].flagsHandle, hipIpcMemLazyEnablePeerAccess));
@@ -706,7 +709,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   // LL protocol: small collectives in one kernel, no host exchange (nbx_ll.h).
   // The choice depends only on arguments every rank passes identically.
   const uint64_t slotBytes = (uint64_t)count * (uint64_t)eb;   // RS: recvcount per block
-  if (count > 0 && protoFromEnv() != 2 && slotBytes <= mp->llMaxBytes && n <= 64) {
+  if (count > 0 && mp->proto != 2 && slotBytes <= mp->llMaxBytes && n <= 64) {
     if (send == nullptr || (recv == nullptr && (kind != kReduce || me == root))) {
       warn("rank %d passed a NULL buffer", me);
       return ncclInvalidArgument;
@@ -790,7 +793,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   NCCLCHECK(mpBarrier(comm, kSlotEnter, seq, stream));
   const size_t total = kind == kReduceScatter ? count * (size_t)n : count;
   size_t off, len;
-  if (kind == kAllReduce && n > 2 && algoFromEnv() == Algo::Ring) {
+  if (kind == kAllReduce && n > 2 && mp->ring) {
     // 2'. ring reduce-scatter (all_reduce.h:60-79): chunk c starts at rank c+1 and
     // visits c+2, ..., c; at step s this rank folds chunk c = me-2-s as
     // Fn(pre(local), received) — NCCL's operand order (recvReduceSend: srcs[0] is

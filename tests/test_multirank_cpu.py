@@ -44,3 +44,72 @@ def test_max_over_ranks_gloo(world):
     for rank, m, value in res:
         assert m == float(world)   # max over ranks of 1 + r
         assert abs(value - world * 2.25 / (world / 10)) < 1e-9
+
+
+STUB_CHILD = r'''
+import json, os, sys
+rank = int(os.environ["RANK"])
+mode = os.environ.get("STUB_MODE", "ok")
+for line in sys.stdin:
+    p = line.split()
+    if p and p[0] == "ID":
+        print("ID aa bb", flush=True)
+    elif p and p[0] == "RUN":
+        assert p[1:3] == ["aa", "bb"]
+        if mode == "die" and rank == 1:
+            sys.exit(3)
+        if mode == "hang" and rank == 1:
+            import time; time.sleep(600)
+        print("RESULT " + json.dumps({"rank": rank, "ok": True, "errors": [],
+              "allreduce_direct_ms": 10.0 + rank, "allreduce_ring_ms": 20.0 + rank,
+              "reduce_scatter_ms": 5.0 + rank, "ll_allreduce_4KiB_us": 7.0 + rank}), flush=True)
+        break
+'''
+
+
+def _leg_worker(rank, world, port, script, mode, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      STUB_MODE=mode)
+    import bench
+    child = bench._spawn_collective_leg(world, script)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = bench.collective_leg(child, world, rank, result_timeout=10.0)
+    q.put((rank, out, child.returncode))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["ok", "die", "hang"])
+def test_collective_leg_protocol_gloo(tmp_path, mode):
+    """bench.py's config-D leg: the parent <-> child protocol, the id broadcast,
+    max-over-ranks aggregation (algbw / busbw), and that a child that dies or
+    hangs is reported (ok: false) without hanging or failing the bench."""
+    script = tmp_path / "stub_child.py"
+    script.write_text(STUB_CHILD)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_leg_worker, args=(r, world, port, str(script), mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (o, rc)) for r, o, rc in [q.get(timeout=180) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out = res[0][0]
+    assert res[1][0] is None
+    S = (256 << 20) * 4
+    if mode == "ok":
+        assert out["ok"] is True and "errors" not in out
+        assert out["allreduce_direct"]["ms"] == 11.0          # max over ranks
+        alg = S / 11e-3 / 1e9
+        assert abs(out["allreduce_direct"]["algbw_GBs"] - round(alg, 2)) < 1e-9
+        assert abs(out["allreduce_direct"]["busbw_GBs"] - round(alg * 2 * (world - 1) / world, 2)) < 1e-9
+        assert out["reduce_scatter"]["ms"] == 6.0
+        assert abs(out["reduce_scatter"]["busbw_GBs"] - round(S / 6e-3 / 1e9 * (world - 1) / world, 2)) < 1e-9
+        assert out["ll_allreduce_4KiB_us"] == 8.0
+    else:
+        assert out["ok"] is False
+        assert any(e.startswith("rank 1:") for e in out["errors"])
+        assert out["allreduce_direct"] is None
