@@ -25,7 +25,9 @@ Extra JSON fields:
                  multi-process communicator across the N GPUs, checked exactly;
                  run in a child process per rank (scripts/collective_leg.py) so
                  a failure there is reported here instead of ending the bench.
-                 NBX_BENCH_COLLECTIVE=0 skips it.
+                 Then `collective.rccl`: RCCL (torch.distributed "nccl") on the
+                 same shapes in the bench process, as the vendor reference.
+                 NBX_BENCH_COLLECTIVE=0 skips both, NBX_BENCH_RCCL=0 the RCCL part.
 """
 from __future__ import annotations
 
@@ -228,8 +230,54 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     out["allreduce_direct"] = agg("allreduce_direct_ms", 2 * (world - 1) / world, S)
     out["allreduce_ring"] = agg("allreduce_ring_ms", 2 * (world - 1) / world, S)
     out["reduce_scatter"] = agg("reduce_scatter_ms", (world - 1) / world, S)
-    ll = [r.get("ll_allreduce_4KiB_us") for r in allres]
-    out["ll_allreduce_4KiB_us"] = None if any(v is None for v in ll) else round(max(ll), 2)
+    for key in ("ll_allreduce_4KiB_us", "ll128_allreduce_1MiB_us"):
+        vals = [r.get(key) for r in allres]
+        out[key] = None if any(v is None for v in vals) else round(max(vals), 2)
+    return out
+
+
+def rccl_leg(world: int):
+    """RCCL (torch.distributed "nccl" on ROCm) on the same config-D shapes, in
+    this process after the collective leg: the vendor library's all-reduce /
+    reduce-scatter over the same xGMI links, as the reference point for
+    libnbxccl's numbers. Every rank returns the max-over-ranks times."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend() != "nccl":
+        return None
+    out = {"library": "RCCL via torch.distributed (backend nccl)", "ok": True}
+    try:
+        def timed(fn, iters):
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            return max_over_ranks((time.perf_counter() - t0) / iters, world)
+        rank = dist.get_rank()
+        x = torch.full((COUNT_D,), float(rank + 1), device="cuda")
+        S = COUNT_D * 4
+        t = timed(lambda: dist.all_reduce(x), 5)
+        out["allreduce"] = {"ms": round(t * 1e3, 4), "algbw_GBs": round(S / t / 1e9, 2),
+                            "busbw_GBs": round(S / t / 1e9 * 2 * (world - 1) / world, 2)}
+        y = torch.empty(COUNT_D // world, device="cuda")
+        x.fill_(float(rank + 1))
+        t = timed(lambda: dist.reduce_scatter_tensor(y, x), 5)
+        out["reduce_scatter"] = {"ms": round(t * 1e3, 4), "algbw_GBs": round(S / t / 1e9, 2),
+                                 "busbw_GBs": round(S / t / 1e9 * (world - 1) / world, 2)}
+        want = float(world * (world + 1) // 2)
+        if not bool((y == want).all().item()):
+            out["ok"] = False
+        for name, cnt in (("allreduce_1MiB_us", 256 << 10), ("allreduce_4KiB_us", 1024)):
+            z = torch.ones(cnt, device="cuda")
+            out[name] = round(timed(lambda: dist.all_reduce(z), 100) * 1e6, 2)
+        del x, y
+        torch.cuda.empty_cache()
+    except Exception as e:   # reported, never fatal to the bench line
+        out = {"ok": False, "errors": [f"{type(e).__name__}: {e}"]}
     return out
 
 
@@ -329,7 +377,12 @@ def main():
     if child is not None:
         del srcs, out
         torch.cuda.empty_cache()
-        result["collective"] = collective_leg(child, world, rank)
+        coll = collective_leg(child, world, rank)
+        if os.environ.get("NBX_BENCH_RCCL", "1") != "0":
+            rccl = rccl_leg(world)
+            if coll is not None:
+                coll["rccl"] = rccl
+        result["collective"] = coll
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if child is None:
             del srcs, out

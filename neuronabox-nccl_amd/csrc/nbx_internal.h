@@ -10,4 +10,7 @@ struct LLArgs;
 // advances it by the grid size.
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t* arrived,
                           hipStream_t stream);
+// The same for the LL128 kernel (args.nLines lines of 128 bytes).
+ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t* arrived,
+                             hipStream_t stream);
 }  // namespace nbx

@@ -29,7 +29,8 @@ struct KArgs {
 struct KernelSet {
   const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
-  const void* ll;                   // LL-protocol AllReduce (nbx_ll.h)
+  const void* ll;                   // LL-protocol collectives (nbx_ll.h)
+  const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;
   int valid;

@@ -6,6 +6,7 @@
 namespace nbx {
 
 enum LLMode : int32_t { kLLAllReduce = 0, kLLReduceScatter = 1, kLLReduce = 2 };
+constexpr int kL128MaxRanksHost = 8;   // LL128 kernel keeps one line per rank in registers
 
 struct LLArgs {
   const void* send;
@@ -26,6 +27,12 @@ struct LLArgs {
   const volatile int* abortWord;
   volatile int* errWord;
   uint64_t timeoutTicks;
+  // LL128 (kLL128Coll only): 128-byte lines, 120 payload bytes + 8-byte flag
+  uint64_t* const* peerL128;  // device table: rank -> LL128 buffer base
+  uint64_t* myL128;
+  uint64_t l128SlotLines;     // lines per (parity, source) slot
+  uint64_t nLines;            // lines covering this call's slot bytes
+  uint32_t l128Bytes;         // size of myL128 (buffer-descriptor range, < 4 GiB)
   uint32_t flag;
   int32_t parity;
   int32_t rank;

@@ -186,6 +186,33 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
   *arrived = a.arriveTarget;
   return ncclSuccess;
 }
+
+ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, uint64_t* arrived,
+                             hipStream_t stream) {
+  if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
+  const KernelSet& ks = table()[(int)dt][op.op];
+  if (!ks.valid || ks.ll128 == nullptr) return ncclInvalidArgument;
+  a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+  a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+  // 32 lines (8 lanes each) per 256-thread workgroup, at most one workgroup per
+  // CU by default (every block of the grid co-resident on its GPU, so a block
+  // waiting for its peers' lines never holds back a block they wait for).
+  // NBX_LL128_MAX_GRID lowers the cap, e.g. when several ranks share one GPU.
+  static const size_t maxGrid = [] {
+    const char* v = std::getenv("NBX_LL128_MAX_GRID");
+    long g = (v && *v) ? std::atol(v) : 256;
+    return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
+  }();
+  size_t grid = (a.nLines + 31) / 32;
+  if (grid < 1) grid = 1;
+  if (grid > maxGrid) grid = maxGrid;
+  a.arriveTarget = *arrived + grid;
+  void* args[] = {&a};
+  hipError_t e = hipLaunchKernel(ks.ll128, dim3((unsigned)grid), dim3(256), args, 0, stream);
+  if (e != hipSuccess) return ncclUnhandledCudaError;
+  *arrived = a.arriveTarget;
+  return ncclSuccess;
+}
 }  // namespace nbx
 
 extern "C" {

@@ -509,8 +509,16 @@ struct MpState {
   uint64_t llSlotLines = 0;
   uint64_t llDoneOff = 0;
   uint64_t llLastSeq[2] = {0, 0};   // last LL call per parity (credit target)
-  uint64_t llArrived = 0;           // arrival-counter value after the last LL launch
-  int proto = 0;                    // NCCL_PROTO at init: 0 auto, 1 LL, 2 Simple
+  uint64_t llArrived = 0;           // arrival-counter value after the last LL/LL128 launch
+  // LL128 protocol (nbx_ll.h kLL128Coll): own buffer [2][n][l128SlotLines] 128-B lines;
+  // shares the LL buffer's done words, arrival counter and parity credits
+  uint64_t* l128 = nullptr;
+  uint64_t** peerL128Dev = nullptr;
+  std::vector<void*> peerL128Maps;
+  uint64_t l128MaxBytes = 0;        // 0: LL128 unavailable (n > 8)
+  uint64_t l128SlotLines = 0;
+  uint64_t l128Bytes = 0;
+  int protoMask = 0;                // NCCL_PROTO at init: kProtoLL | kProtoLL128 | kProtoSimple
   bool ring = false;                // NCCL_ALGO=Ring at init
 };
 
@@ -519,19 +527,46 @@ struct MpInitInfo {
   int32_t device;
   hipIpcMemHandle_t flagsHandle;
   hipIpcMemHandle_t llHandle;
+  hipIpcMemHandle_t l128Handle;
   uint64_t llMaxBytes;
+  uint64_t l128MaxBytes;
+  int32_t protoMask;
 };
 
-// NCCL_PROTO (tuning.cc:254-259): "Simple" disables the LL protocol, "LL"
-// forces it for every message that fits the LL buffer; default: LL for
-// AllReduce / ReduceScatter / Reduce messages (per-rank block for
-// ReduceScatter) up to NBX_LL_MAX_BYTES (64 KiB).
+// NCCL_PROTO (tuning.cc:254-259, parseList): a comma-separated list of the
+// enabled protocols among LL, LL128, Simple, or "^list" for all but those.
+// Per message (per-rank block for ReduceScatter) the first enabled protocol
+// whose buffer holds it is used: LL up to NBX_LL_MAX_BYTES (64 KiB), LL128 up
+// to NBX_LL128_MAX_BYTES (1 MiB; n <= 8 ranks), else Simple (also the
+// fallback when Simple is disabled and nothing else fits).
 // Read when the communicator is created (as NCCL reads its tuning env at init).
-int protoFromEnv() {   // 0 auto, 1 LL, 2 Simple
+enum { kProtoLL = 1, kProtoLL128 = 2, kProtoSimple = 4, kProtoAll = 7 };
+int protoFromEnv() {
   const char* v = std::getenv("NCCL_PROTO");
-  if (v && strcasecmp(v, "simple") == 0) return 2;
-  if (v && strcasecmp(v, "ll") == 0) return 1;
-  return 0;
+  if (v == nullptr || *v == 0) return kProtoAll;
+  bool exclude = v[0] == '^';
+  std::string list(exclude ? v + 1 : v);
+  int mask = 0;
+  size_t pos = 0;
+  while (pos <= list.size()) {
+    size_t e = list.find(',', pos);
+    if (e == std::string::npos) e = list.size();
+    std::string tok = list.substr(pos, e - pos);
+    if (strcasecmp(tok.c_str(), "ll") == 0) mask |= kProtoLL;
+    else if (strcasecmp(tok.c_str(), "ll128") == 0) mask |= kProtoLL128;
+    else if (strcasecmp(tok.c_str(), "simple") == 0) mask |= kProtoSimple;
+    else if (!tok.empty()) warn("NCCL_PROTO: unknown protocol '%s' ignored", tok.c_str());
+    pos = e + 1;
+  }
+  return exclude ? (kProtoAll & ~mask) : mask;
+}
+
+enum MpProto { kMpLL, kMpLL128, kMpSimple };
+MpProto chooseProto(const MpState* mp, uint64_t slotBytes, int n) {
+  if (slotBytes == 0 || n > 64) return kMpSimple;
+  if ((mp->protoMask & kProtoLL) && slotBytes <= mp->llMaxBytes) return kMpLL;
+  if ((mp->protoMask & kProtoLL128) && mp->l128MaxBytes != 0 && slotBytes <= mp->l128MaxBytes) return kMpLL128;
+  return kMpSimple;
 }
 
 struct MpCallInfo {
@@ -608,7 +643,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   c->mp = mp;
   const char* t = std::getenv("NBX_TIMEOUT_SEC");
   if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
-  mp->proto = protoFromEnv();
+  mp->protoMask = protoFromEnv();
   mp->ring = algoRingFromEnv();
   NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
   HIPCHECK(allocSyncMem((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
@@ -629,23 +664,43 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes));
     HIPCHECK(hipMemset(mp->ll, 0, llBytes));
   }
+  // LL128 buffer: 2 parities x n sources x lines of 120 payload bytes (n <= 8)
+  if (c->nRanks <= nbx::kL128MaxRanksHost) {
+    const char* v = std::getenv("NBX_LL128_MAX_BYTES");
+    uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (1u << 20);
+    if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
+    if (mx != 0) {
+      mx = (mx + 15) & ~(uint64_t)15;
+      mp->l128MaxBytes = mx;
+      mp->l128SlotLines = (mx + 119) / 120;
+      mp->l128Bytes = 2 * (uint64_t)c->nRanks * mp->l128SlotLines * 128;
+      HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes));
+      HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
+    }
+  }
   MpInitInfo mine{};
   mine.pid = (int32_t)getpid();
   mine.device = c->device;
   mine.llMaxBytes = mp->llMaxBytes;
+  mine.l128MaxBytes = mp->l128MaxBytes;
+  mine.protoMask = mp->protoMask;
   HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
+  if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
   std::vector<MpInitInfo> all(c->nRanks);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
-  std::vector<uint64_t*> table(c->nRanks), llTable(c->nRanks);
+  std::vector<uint64_t*> table(c->nRanks), llTable(c->nRanks), l128Table(c->nRanks, nullptr);
   for (int j = 0; j < c->nRanks; j++) {
-    if (all[j].llMaxBytes != mp->llMaxBytes) {
-      warn("ncclCommInitRank : NBX_LL_MAX_BYTES differs across ranks");
+    // every rank must pick the same protocol for the same call
+    if (all[j].llMaxBytes != mp->llMaxBytes || all[j].l128MaxBytes != mp->l128MaxBytes ||
+        all[j].protoMask != mp->protoMask) {
+      warn("ncclCommInitRank : NCCL_PROTO / NBX_LL_MAX_BYTES / NBX_LL128_MAX_BYTES differ across ranks");
       return ncclInvalidUsage;
     }
     if (j == c->rank) {
       table[j] = mp->flags;
       llTable[j] = mp->ll;
+      l128Table[j] = mp->l128;
       continue;
     }
     if (all[j].device != c->device) {
@@ -669,11 +724,21 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     HIPCHECK(hipIpcOpenMemHandle(&q, all[j].llHandle, hipIpcMemLazyEnablePeerAccess));
     mp->peerLLMaps.push_back(q);
     llTable[j] = (uint64_t*)q;
+    if (mp->l128) {
+      void* w = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].l128Handle, hipIpcMemLazyEnablePeerAccess));
+      mp->peerL128Maps.push_back(w);
+      l128Table[j] = (uint64_t*)w;
+    }
   }
   HIPCHECK(hipMalloc((void**)&mp->peerFlagsDev, c->nRanks * sizeof(uint64_t*)));
   HIPCHECK(hipMemcpy(mp->peerFlagsDev, table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
   HIPCHECK(hipMalloc((void**)&mp->peerLLDev, c->nRanks * sizeof(uint64_t*)));
   HIPCHECK(hipMemcpy(mp->peerLLDev, llTable.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
+  if (mp->l128) {
+    HIPCHECK(hipMalloc((void**)&mp->peerL128Dev, c->nRanks * sizeof(uint64_t*)));
+    HIPCHECK(hipMemcpy(mp->peerL128Dev, l128Table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
+  }
   // everyone has mapped everyone before the first collective
   int dummy = 0;
   std::vector<int> sink(c->nRanks);
@@ -691,6 +756,9 @@ void mpFree(ncclComm* c) {
   for (auto& kv : mp->maps) (void)hipIpcCloseMemHandle(kv.second);
   for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
+  for (void* p : mp->peerL128Maps) (void)hipIpcCloseMemHandle(p);
+  if (mp->peerL128Dev) (void)hipFree(mp->peerL128Dev);
+  if (mp->l128) (void)hipFree(mp->l128);
   if (mp->peerFlagsDev) (void)hipFree(mp->peerFlagsDev);
   if (mp->peerLLDev) (void)hipFree(mp->peerLLDev);
   if (mp->ll) (void)hipFree(mp->ll);
@@ -706,10 +774,12 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
   const int eb = typeSize(dt);
-  // LL protocol: small collectives in one kernel, no host exchange (nbx_ll.h).
-  // The choice depends only on arguments every rank passes identically.
+  // LL / LL128 protocols: small and medium collectives in one kernel, no host
+  // exchange (nbx_ll.h). The choice depends only on arguments every rank
+  // passes identically (and on the init-time settings checked equal).
   const uint64_t slotBytes = (uint64_t)count * (uint64_t)eb;   // RS: recvcount per block
-  if (count > 0 && mp->proto != 2 && slotBytes <= mp->llMaxBytes && n <= 64) {
+  const MpProto proto = chooseProto(mp, slotBytes, n);
+  if (proto != kMpSimple) {
     if (send == nullptr || (recv == nullptr && (kind != kReduce || me == root))) {
       warn("rank %d passed a NULL buffer", me);
       return ncclInvalidArgument;
@@ -741,6 +811,14 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     la.postOp = 1;
     la.mode = kind == kAllReduce ? nbx::kLLAllReduce : kind == kReduceScatter ? nbx::kLLReduceScatter : nbx::kLLReduce;
     la.root = root;
+    if (proto == kMpLL128) {
+      la.peerL128 = mp->peerL128Dev;
+      la.myL128 = mp->l128;
+      la.l128SlotLines = mp->l128SlotLines;
+      la.nLines = (slotBytes + 119) / 120;
+      la.l128Bytes = (uint32_t)mp->l128Bytes;
+      return nbx::launchLL128Coll(dt, op, la, &mp->llArrived, stream);
+    }
     return nbx::launchLLColl(dt, op, la, &mp->llArrived, stream);
   }
   const uint64_t seq = ++mp->seq;

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """collective_leg.py — SURVEY §8(d) config D across real GPUs: ncclAllReduce /
 ncclReduceScatter of 1 GiB fp32 per rank through libnbxccl's multi-process
-communicator (one process per GPU, TCP bootstrap + hipIpc + device flags).
+communicator (one process per GPU, TCP bootstrap + hipIpc + device flags),
+plus the LL128 (1 MiB) and LL (4 KiB) protocols' latency, every output checked.
 
 Run as a CHILD of each bench.py rank (N > 1), so a failure here can never take
 the bench's own line down. It is spawned before the parent touches the GPU and
@@ -30,6 +31,8 @@ if ROOT not in sys.path:
 
 COUNT = 256 << 20          # fp32 elements per rank: 1 GiB (config D)
 LL_COUNT = 1024            # 4 KiB LL AllReduce latency probe
+LL128_COUNT = 256 << 10    # 1 MiB LL128 AllReduce (the protocol's largest default message)
+LL128_ITERS = 200
 WARMUP, ITERS = 2, 5
 
 
@@ -101,6 +104,26 @@ def run(ids, rank, world, dev):
     res["reduce_scatter_ms"] = _time_calls(lambda: comm.reduce_scatter(x.data_ptr(), yr.data_ptr(), rc, F32, SUM, st),
                                            ITERS)
 
+    # LL128 (1 MiB): exact on every one of LL128_ITERS calls with inputs that
+    # change per call (a torn 128-byte line or a stale slot would show up as a
+    # wrong value), then the per-call latency
+    x1 = x[:LL128_COUNT].clone()
+    e1 = exp[:LL128_COUNT]
+    y1 = torch.empty(LL128_COUNT, dtype=torch.float32, device="cuda")
+    bad = 0
+    for it in range(LL128_ITERS):
+        xi = x1 + float(it % 97)
+        comm.all_reduce(xi.data_ptr(), y1.data_ptr(), LL128_COUNT, F32, SUM, st)
+        if not torch.equal(y1, e1 + float(world * (it % 97))):
+            bad += 1
+    torch.cuda.synchronize()
+    if bad:
+        res["ok"] = False
+        res["errors"].append(f"ll128_allreduce: {bad} of {LL128_ITERS} calls wrong")
+    res["ll128_checked_calls"] = LL128_ITERS
+    res["ll128_allreduce_1MiB_us"] = 1e3 * _time_calls(
+        lambda: comm.all_reduce(x1.data_ptr(), y1.data_ptr(), LL128_COUNT, F32, SUM, st), 100)
+
     xs, ys = x[:LL_COUNT].clone(), torch.empty(LL_COUNT, dtype=torch.float32, device="cuda")
     comm.all_reduce(xs.data_ptr(), ys.data_ptr(), LL_COUNT, F32, SUM, st)
     torch.cuda.synchronize()
@@ -125,6 +148,8 @@ def main():
     dev = int(os.environ.get("NBX_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
     os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "120")
+    if "NBX_BENCH_DEVICE" in os.environ:   # rehearsal: every rank on one GPU, keep LL128 grids co-resident
+        os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
     for line in sys.stdin:
         parts = line.split()
         if not parts:

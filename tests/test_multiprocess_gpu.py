@@ -67,14 +67,19 @@ def _blocks(count, eb, n):
     return [(min(count, per * b), min(count, per * b + per)) for b in range(n)]
 
 
-@pytest.mark.parametrize("n,algo", [(2, "direct"), (3, "direct"), (3, "ring"), (4, "ring")])
-def test_multiprocess_collectives(nbx, oracle, n, algo, monkeypatch):
+@pytest.mark.parametrize("n,algo,proto", [(2, "direct", "LL,Simple"), (3, "direct", "LL,Simple"),
+                                          (3, "ring", "LL,Simple"), (4, "ring", "LL,Simple"), (3, "direct", "")])
+def test_multiprocess_collectives(nbx, oracle, n, algo, proto, monkeypatch):
     """NCCL_ALGO=Ring: NCCL's ring order (chunk c from rank c+1 to c, Fn(local,
     received)); for the commutative ops tested it is bit-identical to the
-    oracle's left fold in the order c+1, ..., c."""
+    oracle's left fold in the order c+1, ..., c. NCCL_PROTO=LL,Simple keeps the
+    40009-element messages on the Simple (direct / ring) path; the default
+    sends most of them through LL128."""
     # bounded waits everywhere: a failing rank must not strand its peers
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
+    monkeypatch.setenv("NCCL_PROTO", proto)
     monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
@@ -196,11 +201,12 @@ def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch):
     print("8-rank shared-GPU allreduce ms/call:", [round(res[r][1], 3) for r in range(n)])
 
 
-# (kind, dtype, op, count, byte offset of send/recv): all <= 64 KiB per slot -> LL
-# protocol; the 40000-float AllReduce and the 20000-float ReduceScatter -> direct.
-# Reduce to a changing root back to back exercises the done-word credits (a
-# non-root never waits for data, so only the credits stop it from overwriting a
-# slot the root has not read yet).
+# (kind, dtype, op, count, byte offset of send/recv). By default slots
+# <= 64 KiB take the LL protocol, <= 1 MiB LL128, larger ones the direct
+# (Simple) path; with NCCL_PROTO=LL128 every slot <= 1 MiB takes LL128. Reduce
+# to a changing root back to back exercises the done-word credits (a non-root
+# never waits for data, so only the credits stop it from overwriting a slot the
+# root has not read yet).
 LL_CASES = [
     ("ar", 7, 0, 1, 0), ("ar", 7, 0, 3, 0), ("ar", 7, 0, 1000, 0), ("ar", 7, 0, 16384, 0), ("ar", 6, 0, 17, 0),
     ("ar", 9, 4, 4097, 0), ("ar", 2, 4, 999, 0), ("ar", 4, 2, 4096, 0), ("ar", 10, 0, 33, 0),
@@ -208,6 +214,12 @@ LL_CASES = [
     ("ar", 0, 0, 77, 3), ("rs", 7, 0, 1000, 0), ("rs", 6, 4, 333, 2), ("rs", 0, 2, 5, 1), ("rs", 4, 4, 4096, 0),
     ("rs", 7, 0, 20000, 0), ("red", 7, 0, 1000, 0), ("red", 9, 4, 777, 0), ("red", 2, 3, 64, 0),
     ("red", 7, 0, 123, 4), ("red", 7, 1, 4096, 0), ("ar", 7, 0, 64, 0),
+    # LL128 range (64 KiB, 1 MiB] by default: odd lengths so 120-byte lines straddle 16-byte blocks
+    ("ar", 7, 0, 100003, 0), ("ar", 7, 4, 262144, 0), ("ar", 6, 4, 77777, 2), ("ar", 9, 0, 300001, 0),
+    ("ar", 4, 2, 50000, 8), ("ar", 11, 0, 600001, 1), ("rs", 7, 0, 30001, 4), ("rs", 2, 2, 131072, 0),
+    ("red", 7, 0, 99999, 0), ("red", 8, 4, 100000, 8),
+    # direct (Simple) path interleaved: > 1 MiB per slot
+    ("ar", 7, 0, 300000, 0), ("rs", 7, 4, 262145, 0),
 ]
 
 
@@ -221,8 +233,11 @@ def _ll_root(i, n):
     return (i * 3 + 1) % n
 
 
-def _child_ll(uid_bytes, rank, n, q):
+def _child_ll(uid_bytes, rank, n, q, proto):
     try:
+        import os
+        if proto:
+            os.environ["NCCL_PROTO"] = proto
         import time
 
         import torch
@@ -271,18 +286,23 @@ def _child_ll(uid_bytes, rank, n, q):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("n", [2, 3, 5])
-def test_multiprocess_ll_protocol(nbx, oracle, n, monkeypatch):
-    """LL protocol (one kernel, {data, flag} lines, no host exchange) for small
+@pytest.mark.parametrize("n,proto", [(2, ""), (3, ""), (5, ""), (2, "LL128"), (3, "LL128"), (8, "")])
+def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
+    """LL protocol (one kernel, {data, flag} 8-byte lines, no host exchange) for
+    small, LL128 (120 payload bytes + flag per 128-byte line) for medium
     AllReduce / ReduceScatter / Reduce messages, misaligned buffers included,
-    issued back to back without host synchronisation and interleaved with
-    direct-path messages; bitwise equal to the direct schedule's fold order."""
+    issued back to back without host synchronisation and interleaved with each
+    other and with direct-path messages; bitwise equal to the direct schedule's
+    fold order. NCCL_PROTO=LL128 routes every message <= 1 MiB through LL128."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    # all ranks share the test box's one GPU: keep every rank's LL128 grid
+    # co-resident (8 ranks x 16 workgroups), as one GPU per rank guarantees
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_child_ll, args=(bytes(uid), r, n, q), daemon=True) for r in range(n)]
+    procs = [ctx.Process(target=_child_ll, args=(bytes(uid), r, n, q, proto), daemon=True) for r in range(n)]
     for p in procs:
         p.start()
     res = {}
@@ -324,5 +344,5 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, monkeypatch):
             for r, e in exp.items():
                 got = res[r][0][(it, i)]
                 assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (it, kind, dtype, op, count, r)
-    print(f"LL 4 KiB fp32 allreduce, {n} ranks sharing one GPU: us/call =",
+    print(f"LL 4 KiB fp32 allreduce (NCCL_PROTO={proto or 'default'}), {n} ranks sharing one GPU: us/call =",
           [round(res[r][1], 1) for r in range(n)])
