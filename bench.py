@@ -230,6 +230,10 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     out["allreduce_direct"] = agg("allreduce_direct_ms", 2 * (world - 1) / world, S)
     out["allreduce_ring"] = agg("allreduce_ring_ms", 2 * (world - 1) / world, S)
     out["reduce_scatter"] = agg("reduce_scatter_ms", (world - 1) / world, S)
+    E = 128 << 20
+    out["config_e"] = {"int64_max": agg("config_e_int64_max_ms", 2 * (world - 1) / world, E),
+                       "fp8_e4m3_sum": agg("config_e_fp8_sum_ms", 2 * (world - 1) / world, E),
+                       "check": "bit-exact vs a GPU restatement of the direct schedule's fold order"}
     for key in ("ll_allreduce_4KiB_us", "ll128_allreduce_1MiB_us"):
         vals = [r.get(key) for r in allres]
         out[key] = None if any(v is None for v in vals) else round(max(vals), 2)

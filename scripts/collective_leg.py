@@ -2,7 +2,8 @@
 """collective_leg.py — SURVEY §8(d) config D across real GPUs: ncclAllReduce /
 ncclReduceScatter of 1 GiB fp32 per rank through libnbxccl's multi-process
 communicator (one process per GPU, TCP bootstrap + hipIpc + device flags),
-plus the LL128 (1 MiB) and LL (4 KiB) protocols' latency, every output checked.
+plus the LL128 (1 MiB) and LL (4 KiB) protocols' latency and config E (int64
+max + fp8 sum AllReduce, 128 MiB), every output checked.
 
 Run as a CHILD of each bench.py rank (N > 1), so a failure here can never take
 the bench's own line down. It is spawned before the parent touches the GPU and
@@ -33,6 +34,8 @@ COUNT = 256 << 20          # fp32 elements per rank: 1 GiB (config D)
 LL_COUNT = 1024            # 4 KiB LL AllReduce latency probe
 LL128_COUNT = 256 << 10    # 1 MiB LL128 AllReduce (the protocol's largest default message)
 LL128_ITERS = 200
+E_I64 = 16 << 20           # config E: int64 elements (128 MiB)
+E_F8 = 128 << 20           # config E: fp8 elements (128 MiB)
 WARMUP, ITERS = 2, 5
 
 
@@ -133,6 +136,10 @@ def run(ids, rank, world, dev):
     res["ll_allreduce_4KiB_us"] = 1e3 * _time_calls(
         lambda: comm.all_reduce(xs.data_ptr(), ys.data_ptr(), LL_COUNT, F32, SUM, st), 200)
 
+    del x, y, yr, exp, x1, e1, y1, xs, ys
+    torch.cuda.empty_cache()
+    config_e(comm, rank, world, st, res)
+
     torch.cuda.synchronize()
     if comm.async_error() != 0 or comm_ring.async_error() != 0:
         res["ok"] = False
@@ -140,6 +147,75 @@ def run(ids, rank, world, dev):
     comm_ring.destroy()
     comm.destroy()
     return res
+
+
+def _blocks(count, eb, n):
+    """The direct schedule's AllReduce blocks (nccl_api.cc blockRange): 16-byte aligned."""
+    epp = 16 // eb
+    per = -(-count // n)
+    per = -(-per // epp) * epp
+    return [(min(count, per * b), min(count, per * b + per)) for b in range(n)]
+
+
+def config_e(comm, rank, world, st, res):
+    """SURVEY §8(d) config E across the N GPUs: ncclAllReduce int64 ncclMax over
+    128 MiB (full-range random bits) and fp8 e4m3 ncclSum over 128 MiB (random
+    finite codes), checked bit-exact against a GPU restatement on the same
+    seeded inputs (every rank regenerates every rank's input): max is
+    order-free; the fp8 sum folds each block c in the direct schedule's order
+    c+1, ..., c with an fp32 add and an RNE narrowing per step (NaN = any NaN
+    code, the kernel's and torch's NaN encodings may differ)."""
+    import torch
+    I64, F8, MAX, SUM = 4, 10, 2, 0
+
+    def gen_i64(r):
+        g = torch.Generator(device="cuda").manual_seed(9001 + r)
+        return torch.randint(-2**63, 2**63 - 1, (E_I64,), dtype=torch.int64, device="cuda", generator=g)
+
+    def gen_f8(r):
+        g = torch.Generator(device="cuda").manual_seed(7001 + r)
+        c = torch.randint(0, 256, (E_F8,), dtype=torch.uint8, device="cuda", generator=g)
+        c[(c & 0x7f) == 0x7f] = 0   # finite codes only
+        return c
+
+    # int64 max
+    x = gen_i64(rank)
+    y = torch.empty_like(x)
+    comm.all_reduce(x.data_ptr(), y.data_ptr(), E_I64, I64, MAX, st)
+    torch.cuda.synchronize()
+    exp = gen_i64(0)
+    for r in range(1, world):
+        exp = torch.maximum(exp, gen_i64(r))
+    ok_i = torch.equal(y, exp)
+    res["config_e_int64_max_ms"] = _time_calls(lambda: comm.all_reduce(x.data_ptr(), y.data_ptr(), E_I64, I64, MAX,
+                                                                       st), ITERS)
+    del x, y, exp
+    # fp8 e4m3 sum
+    xs = [gen_f8(r) for r in range(world)]
+    y = torch.empty(E_F8, dtype=torch.uint8, device="cuda")
+    comm.all_reduce(xs[rank].data_ptr(), y.data_ptr(), E_F8, F8, SUM, st)
+    torch.cuda.synchronize()
+    f8 = torch.float8_e4m3fn
+    exp = torch.empty(E_F8, dtype=torch.uint8, device="cuda")
+    for c, (lo, hi) in enumerate(_blocks(E_F8, 1, world)):
+        if hi <= lo:
+            continue
+        acc = xs[(c + 1) % world][lo:hi].view(f8)
+        for q in range(1, world):
+            acc = (acc.float() + xs[(c + 1 + q) % world][lo:hi].view(f8).float()).to(f8)
+        exp[lo:hi] = acc.view(torch.uint8)
+    nan_e = (exp & 0x7f) == 0x7f
+    nan_g = (y & 0x7f) == 0x7f
+    ok_f = bool(((y == exp) | (nan_e & nan_g)).all().item())
+    res["config_e_fp8_nan_fraction"] = round(float(nan_e.float().mean().item()), 4)
+    res["config_e_fp8_sum_ms"] = _time_calls(lambda: comm.all_reduce(xs[rank].data_ptr(), y.data_ptr(), E_F8, F8, SUM,
+                                                                      st), ITERS)
+    del xs, y, exp
+    torch.cuda.empty_cache()
+    for name, ok in (("config_e_int64_max", ok_i), ("config_e_fp8_sum", ok_f)):
+        if not ok:
+            res["ok"] = False
+            res["errors"].append(f"{name}: output differs from the bit-exact restatement")
 
 
 def main():
