@@ -50,7 +50,7 @@ typedef struct {
 } nbxDevRedOpFull;
 
 #define NBX_MAX_SRCS 32   /* > 8 sources run as ordered multi-pass folds */
-#define NBX_MAX_DSTS 2
+#define NBX_MAX_DSTS 8    /* NCCL_MAX_DIRECT_ARITY + 1 (device.h:147): local output + 7 peers */
 
 /* Host-side op encoding: replaces hostToDevRedOp, enqueue.cc:1436-1512, for
  * the built-in ops (Sum/Prod/Max/Min/Avg). nRanks feeds ncclAvg. */

@@ -88,7 +88,7 @@ TYPE_SIZE = {
 
 NCCL_UNIQUE_ID_BYTES = 128
 NBX_MAX_SRCS = 32
-NBX_MAX_DSTS = 2
+NBX_MAX_DSTS = 8
 
 
 class ncclUniqueId(ctypes.Structure):

@@ -8,10 +8,11 @@ namespace nbx {
 
 constexpr int kBlock = 256;      // workgroup = 4 wave64
 constexpr int kMaxKSrcs = 8;     // sources per kernel pass
+constexpr int kMaxKDsts = 8;     // destinations: NCCL_MAX_DIRECT_ARITY + 1 (device.h:147, all_reduce.h:343-360)
 
 struct KArgs {
   const void* src[kMaxKSrcs];
-  void* dst[2];
+  void* dst[kMaxKDsts];
   uint64_t nElts;     // total elements
   uint64_t nPacks;    // 16-B packs in the aligned body (starts at headElts)
   uint64_t arg;       // ncclDevRedOpFull.scalarArg (by value)

@@ -61,14 +61,17 @@ __device__ __forceinline__ void reduceElt(const Fn& fn, const KArgs& a, int nSrc
     }
   }
   if constexpr (Fn::kHasPost) if (a.postOp) acc = fn.post(acc);
-  ((E*)a.dst[0])[i] = acc;
-  if (a.nDsts > 1) ((E*)a.dst[1])[i] = acc;
+#pragma unroll
+  for (int d = 0; d < kMaxKDsts; d++)
+    if (d < a.nDsts) ((E*)a.dst[d])[i] = acc;
 }
 
 // Fold one tile slice already in registers and store it (all U packs valid).
+// Destinations beyond the first are a uniform branch per store (the direct
+// schedules' push-gather writes every rank's output from one kernel).
 template <class Fn, int NSRC, int U>
 __device__ __forceinline__ void foldStore(const Fn& fn, const u32x4 (&v)[NSRC][U], uint32_t preMask, bool doPost,
-                                          u32x4* dst0, u32x4* dst1, bool two, uint64_t p) {
+                                          u32x4* const (&dst)[kMaxKDsts], int nDsts, uint64_t p) {
 #pragma unroll
   for (int u = 0; u < U; u++) {
     u32x4 acc = v[0][u];
@@ -80,8 +83,10 @@ __device__ __forceinline__ void foldStore(const Fn& fn, const u32x4 (&v)[NSRC][U
       acc = fn.redPack(acc, t);
     }
     if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
-    stPack(dst0 + p + u * kBlock, acc);
-    if (two) stPack(dst1 + p + u * kBlock, acc);
+    stPack(dst[0] + p + u * kBlock, acc);
+#pragma unroll
+    for (int d = 1; d < kMaxKDsts; d++)
+      if (d < nDsts) stPack(dst[d] + p + u * kBlock, acc);
   }
 }
 
@@ -106,9 +111,10 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
   const u32x4* src[NSRC];
 #pragma unroll
   for (int s = 0; s < NSRC; s++) src[s] = (const u32x4*)((const char*)a.src[s] + headBytes);
-  u32x4* dst0 = (u32x4*)((char*)a.dst[0] + headBytes);
-  u32x4* dst1 = (u32x4*)((char*)a.dst[1] + headBytes);
-  const bool two = a.nDsts > 1;
+  u32x4* dst[kMaxKDsts];
+#pragma unroll
+  for (int d = 0; d < kMaxKDsts; d++) dst[d] = (u32x4*)((char*)a.dst[d] + headBytes);
+  const int nDsts = a.nDsts;
   const bool doPost = Fn::kHasPost && a.postOp;
   const uint32_t preMask = a.preMask;
   const uint64_t n = a.nPacks;
@@ -119,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
       // full tile: issue every load first, then fold
       u32x4 v[NSRC][U];
       loadTile<NSRC, U>(v, src, p);
-      foldStore<Fn, NSRC, U>(fn, v, preMask, doPost, dst0, dst1, two, p);
+      foldStore<Fn, NSRC, U>(fn, v, preMask, doPost, dst, nDsts, p);
     } else {
       // last, partial tile
 #pragma unroll
@@ -129,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
           u32x4 v1[NSRC][1];
 #pragma unroll
           for (int s = 0; s < NSRC; s++) v1[s][0] = ldPack(src[s] + q);
-          foldStore<Fn, NSRC, 1>(fn, v1, preMask, doPost, dst0, dst1, two, q);
+          foldStore<Fn, NSRC, 1>(fn, v1, preMask, doPost, dst, nDsts, q);
         }
       }
     }

@@ -188,33 +188,40 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// LL128 protocol for medium messages (NCCL's LL128 wire format,
-// prims_ll128.h:185-291, device.h NCCL_LL128_LINEELEMS / _DATAELEMS): a line is
-// 128 bytes = 16 u64 words, words 0..14 carry 120 payload bytes and word 15 the
-// flag (= seq). Eight consecutive lanes own one line, 16 bytes each, and move it
-// with ONE wave instruction (global_store_dwordx4 sc0 sc1 on the writer,
-// buffer_load_dwordx4 sc0 sc1 on the reader), so a reader whose lane 7 sees
-// the flag trusts the other 112 bytes of that load — the same 128-byte
-// single-transaction assumption NCCL makes on NVLink. Buffers, parities, done
-// words and credits are the LL protocol's (above); only the slot format and
-// the 94 % payload efficiency (vs LL's 50 %) differ. Restricted to n <= 8
-// ranks (one node): a lane keeps the lines of all n sources in registers and
-// folds each 8-byte word in its own direct-schedule order.
-constexpr int kL128LineBytes = 128;
-constexpr int kL128DataBytes = 120;
+// LL128 protocol for medium messages (NCCL's LL128 idea, prims_ll128.h:185-291:
+// lines of several 16-byte lane chunks, one flag word per line, the whole line
+// moved by ONE wave store instruction and polled by ONE wave load
+// instruction, so a reader whose flag lane sees the flag trusts the rest of
+// the line). NCCL uses 128-byte lines (120 payload bytes + 8-byte flag) and
+// relies on NVLink delivering a 128-byte store whole. gfx950 does not: a
+// 128-byte line torn at its 64-byte halves was observed (flag half new,
+// first half stale; scripts/ll128_stress.py, profiles/r1/ll128_stress_128B.jsonl),
+// so lines here are 64 bytes — 56 payload bytes in words 0..6 and the flag
+// (= seq) in word 7, four consecutive lanes per line, 16 bytes each:
+// global_store_dwordx4 sc0 sc1 (system scope) on the writer,
+// buffer_load_dwordx4 sc0 sc1 (volatile) on the reader, flag checked by lane 3
+// and broadcast with a width-4 __shfl. Payload efficiency 87.5 % (LL: 50 %).
+// Buffers, parities, done words and credits are the LL protocol's (above).
+// Restricted to n <= 8 ranks (one node): a lane keeps the line of every source
+// in registers and folds each 8-byte word in its own direct-schedule order.
+constexpr int kL128Lanes = 4;                 // lanes per line
+constexpr int kL128LineBytes = 64;
+constexpr int kL128DataBytes = 56;
 constexpr int kL128MaxRanks = kL128MaxRanksHost;
 constexpr int kL128LoadAux = 1 | 16 | (int)(1u << 31);   // sc0 sc1 (system scope), volatile
+static_assert(kL128LineBytes == kL128LineBytesHost && kL128DataBytes == kL128DataBytesHost &&
+                  kL128Lanes == kL128LanesHost, "host/device layout");
 
 __device__ __forceinline__ void l128StoreLine16(uint64_t* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-// lanes' 16 bytes of payload line i (lane 7: 8 payload bytes + the flag word)
+// lane t's 16 bytes of payload line i (the last lane: 8 payload bytes + the flag word)
 __device__ __forceinline__ u32x4 l128Payload(const unsigned char* src, uint64_t bytes, uint64_t i, int t,
                                              uint64_t flagWord) {
   const uint64_t off = i * kL128DataBytes + (uint64_t)t * 16;
   const uint64_t w0 = llLoadBytes(src, off, bytes);
-  const uint64_t w1 = t == 7 ? flagWord : llLoadBytes(src, off + 8, bytes);
+  const uint64_t w1 = t == kL128Lanes - 1 ? flagWord : llLoadBytes(src, off + 8, bytes);
   return (u32x4){(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
 }
 
@@ -236,10 +243,10 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   constexpr int EPK = 8 / (int)sizeof(E);
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
-  const int t = (int)(threadIdx.x & 7u);   // lane within the line's group of 8
+  const int t = (int)(threadIdx.x % kL128Lanes);   // lane within the line's group
   const uint64_t bytes = a.count * sizeof(E);
-  const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) >> 3;
-  const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+  const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) / kL128Lanes;
+  const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kL128Lanes;
   const uint64_t t0 = wall_clock64();
   __shared__ int sFailed;
   if (threadIdx.x == 0) sFailed = 0;
@@ -262,7 +269,8 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
         const u32x4 v = a.mode == kLLReduceScatter
                             ? l128Payload((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, a.seq)
                             : whole;
-        uint64_t* line = a.peerL128[j] + ((uint64_t)(a.parity * n + me) * a.l128SlotLines + i) * 16 + 2 * t;
+        uint64_t* line = a.peerL128[j] + ((uint64_t)(a.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) +
+                         2 * t;
         l128StoreLine16(line, v);
       }
     }
@@ -298,7 +306,8 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
       for (int q = 0; q < kL128MaxRanks; q++) {
         if ((need >> q) & 1u) {
           const uint64_t fw = ((uint64_t)v[q].w << 32) | v[q].z;
-          if (__shfl((int)(fw == a.seq), 7, 8)) need &= ~(1u << q);   // the group's lane 7 holds the flag
+          // the group's last lane holds the flag
+          if (__shfl((int)(fw == a.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
         }
       }
       if (need != 0 && (++spins & 1023u) == 0u) {
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
     const uint64_t off = i * kL128DataBytes + (uint64_t)t * 16;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
-      if (k == 1 && t == 7) break;   // word 15 is the flag
+      if (k == 1 && t == kL128Lanes - 1) break;   // the line's last word is the flag
       int first;
       if (a.mode == kLLAllReduce) {
         const int c = (int)(((off + 8 * k) / sizeof(E)) / a.blockElts);   // 8-byte words never straddle blocks

@@ -7,6 +7,9 @@ namespace nbx {
 
 enum LLMode : int32_t { kLLAllReduce = 0, kLLReduceScatter = 1, kLLReduce = 2 };
 constexpr int kL128MaxRanksHost = 8;   // LL128 kernel keeps one line per rank in registers
+constexpr int kL128LineBytesHost = 64;  // LL128 line: 56 payload bytes + 8-byte flag (nbx_ll.h)
+constexpr int kL128DataBytesHost = 56;
+constexpr int kL128LanesHost = 4;       // lanes (16 bytes each) per LL128 line
 
 struct LLArgs {
   const void* send;
@@ -27,7 +30,7 @@ struct LLArgs {
   const volatile int* abortWord;
   volatile int* errWord;
   uint64_t timeoutTicks;
-  // LL128 (kLL128Coll only): 128-byte lines, 120 payload bytes + 8-byte flag
+  // LL128 (kLL128Coll only): 64-byte lines, 56 payload bytes + 8-byte flag
   uint64_t* const* peerL128;  // device table: rank -> LL128 buffer base
   uint64_t* myL128;
   uint64_t l128SlotLines;     // lines per (parity, source) slot

@@ -111,8 +111,7 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
   KArgs a;
   std::memset(&a, 0, sizeof(a));
   for (int s = 0; s < nSrcs; s++) a.src[s] = srcs[s];
-  for (int d = 0; d < nDsts; d++) a.dst[d] = dsts[d];
-  a.dst[1] = nDsts > 1 ? dsts[1] : dsts[0];
+  for (int d = 0; d < kMaxKDsts; d++) a.dst[d] = dsts[d < nDsts ? d : 0];
   a.nElts = count;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
@@ -194,7 +193,7 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   if (!ks.valid || ks.ll128 == nullptr) return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
-  // 32 lines (8 lanes each) per 256-thread workgroup, at most one workgroup per
+  // 64 lines (4 lanes each) per 256-thread workgroup, at most one workgroup per
   // CU by default (every block of the grid co-resident on its GPU, so a block
   // waiting for its peers' lines never holds back a block they wait for).
   // NBX_LL128_MAX_GRID lowers the cap, e.g. when several ranks share one GPU.
@@ -203,7 +202,8 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
     long g = (v && *v) ? std::atol(v) : 256;
     return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
   }();
-  size_t grid = (a.nLines + 31) / 32;
+  const size_t linesPerBlock = 256 / kL128LanesHost;
+  size_t grid = (a.nLines + linesPerBlock - 1) / linesPerBlock;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
   a.arriveTarget = *arrived + grid;

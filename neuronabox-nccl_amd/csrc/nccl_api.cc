@@ -367,6 +367,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   // 2. reduce: rank r folds block r of every send buffer in ring order r+1..r
   const size_t total = p0.kind == kReduceScatter ? p0.count * (size_t)n : p0.count;
   const int postOp = 1;   // the fold is complete in one pass: apply SumPostDiv here
+  const bool push = n <= NBX_MAX_DSTS;
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
     size_t off, len;
@@ -386,14 +387,18 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
       int j = (first + k) % n;
       srcs[k] = (const char*)parts[j].send + off * (size_t)eb;
     }
-    void* dst;
-    if (p0.kind == kReduceScatter) dst = parts[r].recv;
-    else if (p0.kind == kReduce) dst = (char*)parts[p0.root].recv + off * (size_t)eb;
-    else dst = (char*)parts[r].recv + off * (size_t)eb;
-    void* dsts[1] = {dst};
+    // AllReduce with n <= NBX_MAX_DSTS: push-gather — the fold stores block r
+    // into every rank's output at once (all peer links busy in one kernel,
+    // the CollNet-direct scatter shape, all_reduce.h:343-360)
+    std::vector<void*> dsts;
+    if (p0.kind == kReduceScatter) dsts.push_back(parts[r].recv);
+    else if (p0.kind == kReduce) dsts.push_back((char*)parts[p0.root].recv + off * (size_t)eb);
+    else if (!push) dsts.push_back((char*)parts[r].recv + off * (size_t)eb);
+    else
+      for (int k = 0; k < n; k++) dsts.push_back((char*)parts[(r + k) % n].recv + off * (size_t)eb);
     nbxDevRedOpFull op = parts[r].op;
-    NBX_TRACE("clique reduce rank %d off=%zu len=%zu dst=%p src0=%p", r, off, len, dst, srcs[0]);
-    NCCLCHECK(nbxReduceMulti(dsts, 1, srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n, postOp,
+    NBX_TRACE("clique reduce rank %d off=%zu len=%zu dst=%p src0=%p", r, off, len, dsts[0], srcs[0]);
+    NCCLCHECK(nbxReduceMulti(dsts.data(), (int)dsts.size(), srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n, postOp,
                              (ncclStream_t)parts[r].stream));
   }
   for (int r = 0; r < n; r++) {
@@ -401,8 +406,8 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
     HIPCHECK(hipEventRecord(c->evReduced[r], parts[r].stream));
   }
   NBX_TRACE("clique reduce launched");
-  // 3. gather (AllReduce only): rank r pulls block j from rank j's recv buffer
-  if (p0.kind == kAllReduce) {
+  // 3. gather (AllReduce with n > NBX_MAX_DSTS only): rank r pulls block j from rank j's recv buffer
+  if (p0.kind == kAllReduce && !push) {
     for (int r = 0; r < n; r++) {
       DevGuard g(c->devs[r]);
       for (int j = 0; j < n; j++)
@@ -510,7 +515,7 @@ struct MpState {
   uint64_t llDoneOff = 0;
   uint64_t llLastSeq[2] = {0, 0};   // last LL call per parity (credit target)
   uint64_t llArrived = 0;           // arrival-counter value after the last LL/LL128 launch
-  // LL128 protocol (nbx_ll.h kLL128Coll): own buffer [2][n][l128SlotLines] 128-B lines;
+  // LL128 protocol (nbx_ll.h kLL128Coll): own buffer [2][n][l128SlotLines] 64-B lines;
   // shares the LL buffer's done words, arrival counter and parity credits
   uint64_t* l128 = nullptr;
   uint64_t** peerL128Dev = nullptr;
@@ -664,7 +669,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes));
     HIPCHECK(hipMemset(mp->ll, 0, llBytes));
   }
-  // LL128 buffer: 2 parities x n sources x lines of 120 payload bytes (n <= 8)
+  // LL128 buffer: 2 parities x n sources x 64-byte lines of 56 payload bytes (n <= 8)
   if (c->nRanks <= nbx::kL128MaxRanksHost) {
     const char* v = std::getenv("NBX_LL128_MAX_BYTES");
     uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (1u << 20);
@@ -672,8 +677,8 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     if (mx != 0) {
       mx = (mx + 15) & ~(uint64_t)15;
       mp->l128MaxBytes = mx;
-      mp->l128SlotLines = (mx + 119) / 120;
-      mp->l128Bytes = 2 * (uint64_t)c->nRanks * mp->l128SlotLines * 128;
+      mp->l128SlotLines = (mx + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+      mp->l128Bytes = 2 * (uint64_t)c->nRanks * mp->l128SlotLines * nbx::kL128LineBytesHost;
       HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes));
       HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
     }
@@ -815,7 +820,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
       la.peerL128 = mp->peerL128Dev;
       la.myL128 = mp->l128;
       la.l128SlotLines = mp->l128SlotLines;
-      la.nLines = (slotBytes + 119) / 120;
+      la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
       la.l128Bytes = (uint32_t)mp->l128Bytes;
       return nbx::launchLL128Coll(dt, op, la, &mp->llArrived, stream);
     }
@@ -867,9 +872,21 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
       warn("rank %d passed a NULL buffer", j);
       return ncclInvalidArgument;
     }
-  // 1. every rank's stream has reached the collective (its inputs are written)
+  // 1. every rank's stream has reached the collective (its inputs are written,
+  //    its output may be written by peers)
   NCCLCHECK(mpBarrier(comm, kSlotEnter, seq, stream));
   const size_t total = kind == kReduceScatter ? count * (size_t)n : count;
+  // AllReduce with n <= NBX_MAX_DSTS: push-gather — the kernel completing a
+  // block stores it into every rank's output at once (all xGMI links busy in
+  // one kernel, the CollNet-direct scatter shape all_reduce.h:343-360), so
+  // there is no separate gather phase and no barrier before it
+  const bool push = kind == kAllReduce && n <= NBX_MAX_DSTS;
+  std::vector<void*> pushDsts;
+  auto allOutputs = [&](size_t o) {
+    pushDsts.clear();
+    for (int k = 0; k < n; k++) pushDsts.push_back(recvP[(me + k) % n] + o * (size_t)eb);
+    return pushDsts.data();
+  };
   size_t off, len;
   if (kind == kAllReduce && n > 2 && mp->ring) {
     // 2'. ring reduce-scatter (all_reduce.h:60-79): chunk c starts at rank c+1 and
@@ -890,8 +907,9 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
                                st == 0 ? (const void*)(sendP[left] + off * (size_t)eb)
                                        : (const void*)(recvP[left] + off * (size_t)eb)};
         void* dsts[1] = {recvP[me] + off * (size_t)eb};
-        NCCLCHECK(nbxReduceMulti(dsts, 1, srcs, 2, len, dt, op, st == 0 ? 2 : 1, st == n - 2 ? 1 : 0,
-                                 (ncclStream_t)stream));
+        const bool last = st == n - 2;
+        NCCLCHECK(nbxReduceMulti(last && push ? allOutputs(off) : dsts, last && push ? n : 1, srcs, 2, len, dt, op,
+                                 st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream));
       }
       if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, base + st + 1, base + st + 1, 1ull << left, stream));
     }
@@ -913,11 +931,12 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
                 : kind == kReduce      ? (void*)(recvP[root] + off * (size_t)eb)
                                        : (void*)(recvP[me] + off * (size_t)eb);
     void* dsts[1] = {dst};
-    NCCLCHECK(nbxReduceMulti(dsts, 1, srcs.data(), n, len, dt, op, n, 1, (ncclStream_t)stream));
+    NCCLCHECK(nbxReduceMulti(push ? allOutputs(off) : dsts, push ? n : 1, srcs.data(), n, len, dt, op, n, 1,
+                             (ncclStream_t)stream));
   }
   }
-  // 3. AllReduce: gather the peers' reduced blocks
-  if (kind == kAllReduce) {
+  // 3. AllReduce with n > NBX_MAX_DSTS: gather the peers' reduced blocks
+  if (kind == kAllReduce && !push) {
     NCCLCHECK(mpBarrier(comm, kSlotReduced, seq, stream));
     nbxDevRedOpFull copyOp{nbxDevSum, 0, 0};
     for (int k = 1; k < n; k++) {

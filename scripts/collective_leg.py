@@ -108,7 +108,7 @@ def run(ids, rank, world, dev):
                                            ITERS)
 
     # LL128 (1 MiB): exact on every one of LL128_ITERS calls with inputs that
-    # change per call (a torn 128-byte line or a stale slot would show up as a
+    # change per call (a torn line or a stale slot would show up as a
     # wrong value), then the per-call latency
     x1 = x[:LL128_COUNT].clone()
     e1 = exp[:LL128_COUNT]

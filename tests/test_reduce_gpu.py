@@ -175,6 +175,19 @@ def test_two_destinations(nbx, oracle, torch_gpu, dtype):
     run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, ndst=2)
 
 
+@pytest.mark.parametrize("dtype,ndst,nsrc", [(7, 8, 8), (7, 3, 2), (6, 5, 8), (2, 8, 3), (4, 7, 4), (10, 4, 8)])
+def test_many_destinations(nbx, oracle, torch_gpu, dtype, ndst, nsrc):
+    """Up to NBX_MAX_DSTS = 8 destinations (the direct schedules' push-gather:
+    local output + 7 peers), mixed shared misalignment included."""
+    srcs = oracle.random_inputs(dtype, nsrc, 50021, seed=ndst * 10 + nsrc)
+    run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, ndst=ndst)
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    off = (3 * eb) % 16
+    run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, ndst=ndst, src_off=[off] * nsrc, dst_off=[off] * ndst)
+    run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, ndst=ndst, src_off=[off] * nsrc,
+             dst_off=[(off + eb * d) % 16 for d in range(ndst)])   # mixed alignments: element kernel
+
+
 @pytest.mark.parametrize("nsrc", [9, 15, 16, 20, 32])
 def test_many_sources_multipass(nbx, oracle, torch_gpu, nsrc):
     srcs = oracle.random_inputs(7, nsrc, 30011, seed=nsrc)
@@ -214,7 +227,7 @@ def test_invalid_arguments(nbx, torch_gpu):
     E = nbx.ncclResult.ncclInvalidArgument
     assert nbx.reduce_multi_raw([p], [], 16, 7, op) == E                       # no sources
     assert nbx.reduce_multi_raw([p], [p] * 33, 16, 7, op) == E                 # > NBX_MAX_SRCS
-    assert nbx.reduce_multi_raw([p, p, p], [p], 16, 7, op) == E                # > 2 destinations
+    assert nbx.reduce_multi_raw([p] * 9, [p], 16, 7, op) == E                  # > NBX_MAX_DSTS (8)
     assert nbx.reduce_multi_raw([p], [p], 16, 12, op) == E                     # bad datatype
     op.op = 4
     op.scalarArg = 2
