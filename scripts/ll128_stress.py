@@ -4,8 +4,8 @@ test of the suite): N processes (all on GPU 0, or one per GPU with
 --per-gpu) run ITERS back-to-back LL128 collectives with inputs that change
 every call (small integers, so any fold order gives the exact result) and
 check every output. Mismatching elements are binned by the 8-byte word of the
-payload line they travel in (bins assume the 120-byte payload of the
-original 128-byte line; pass --line-payload 56 for the 64-byte line): a torn
+payload line they travel in (--line-payload: 56 for the current 64-byte line,
+the default; the original 128-byte-line run binned by 120): a torn
 line — the flag visible before part of the payload — shows up as mismatches
 concentrated in one part of the line (with 128-byte lines: words 0..7, the
 first 64-byte half, profiles/r1/ll128_stress_128B.jsonl).
