@@ -151,10 +151,17 @@ def _spawn_collective_leg(world: int, script: str | None = None):
 
 
 def _read_line(child, prefix: str, timeout: float):
+    """Next line of the child's stdout starting with `prefix`; a heartbeat goes
+    to stderr every 30 s while waiting (a long leg never looks hung)."""
     deadline = time.monotonic() + timeout
+    t0 = time.monotonic()
     while time.monotonic() < deadline:
-        r, _, _ = select.select([child.stdout], [], [], max(0.0, deadline - time.monotonic()))
+        r, _, _ = select.select([child.stdout], [], [], max(0.0, min(30.0, deadline - time.monotonic())))
         if not r:
+            if time.monotonic() < deadline:
+                print(f"[bench rank {os.environ.get('RANK', '0')}] collective leg running "
+                      f"({time.monotonic() - t0:.0f} s)", file=sys.stderr, flush=True)
+                continue
             break
         line = child.stdout.readline()
         if not line:
@@ -237,6 +244,11 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     for key in ("ll_allreduce_4KiB_us", "ll128_allreduce_1MiB_us"):
         vals = [r.get(key) for r in allres]
         out[key] = None if any(v is None for v in vals) else round(max(vals), 2)
+    sw = {"bytes": allres[0].get("sweep_bytes"), "what": "fp32 sum AllReduce us/call, max over ranks, per protocol"}
+    for name in ("LL", "LL128", "Simple"):
+        rows = [r.get("sweep_" + name + "_us") for r in allres]
+        sw[name] = None if any(v is None for v in rows) else [max(col) for col in zip(*rows)]
+    out["protocol_sweep"] = sw
     return out
 
 
@@ -278,6 +290,12 @@ def rccl_leg(world: int):
         for name, cnt in (("allreduce_1MiB_us", 256 << 10), ("allreduce_4KiB_us", 1024)):
             z = torch.ones(cnt, device="cuda")
             out[name] = round(timed(lambda: dist.all_reduce(z), 100) * 1e6, 2)
+        sweep = []
+        for b in SWEEP_BYTES:
+            z = torch.ones(b // 4, device="cuda")
+            sweep.append(round(timed(lambda: dist.all_reduce(z), 50 if b <= (1 << 20) else 20) * 1e6, 2))
+        out["sweep_bytes"] = SWEEP_BYTES
+        out["sweep_allreduce_us"] = sweep
         del x, y
         torch.cuda.empty_cache()
     except Exception as e:   # reported, never fatal to the bench line
@@ -286,6 +304,7 @@ def rccl_leg(world: int):
 
 
 COUNT_D = 256 << 20   # config D: fp32 elements per rank (1 GiB)
+SWEEP_BYTES = [4 << 10, 32 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]   # = collective_leg.SWEEP_BYTES
 
 
 def main():

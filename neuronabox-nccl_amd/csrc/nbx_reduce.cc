@@ -175,9 +175,17 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
   if (!ks.valid || ks.ll == nullptr) return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+  // one 8-byte pack per thread; NBX_LL_MAX_GRID caps the workgroups (default
+  // 1024), e.g. when several ranks share one GPU and every rank's grid must
+  // stay co-resident for the ranks' spinning blocks to make progress
+  static const size_t maxGrid = [] {
+    const char* v = std::getenv("NBX_LL_MAX_GRID");
+    long g = (v && *v) ? std::atol(v) : 1024;
+    return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
+  }();
   size_t grid = (a.nPacks + 255) / 256;
   if (grid < 1) grid = 1;
-  if (grid > 1024) grid = 1024;
+  if (grid > maxGrid) grid = maxGrid;
   a.arriveTarget = *arrived + grid;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);

@@ -10,8 +10,9 @@ the bench's own line down. It is spawned before the parent touches the GPU and
 talks over stdin/stdout:
 
   parent -> child   "ID\\n"               (rank 0 only)
-  child  -> parent  "ID <hex> <hex>\\n"   two ncclUniqueIds (direct comm, ring comm)
-  parent -> child   "RUN <hex> <hex>\\n"  (every rank, after the parent's broadcast)
+  child  -> parent  "ID <hex> x5\\n"      ncclUniqueIds: direct, ring, and the LL / LL128 /
+                                         Simple comms of the protocol sweep
+  parent -> child   "RUN <hex> x5\\n"     (every rank, after the parent's broadcast)
   child  -> parent  "RESULT <json>\\n"
 
 Inputs are small integers in fp32 (x_r[i] = (7 i + 13 r) mod 1024), so every
@@ -44,6 +45,11 @@ def _emit(line: str) -> None:
     sys.stdout.flush()
 
 
+def _progress(msg: str) -> None:   # to this rank's leg log (stderr); its tail is reported on failure
+    sys.stderr.write(f"[leg {time.strftime('%H:%M:%S')}] {msg}\n")
+    sys.stderr.flush()
+
+
 def _pkg():
     from __graft_entry__ import _load_package
     nbx = _load_package()
@@ -51,14 +57,75 @@ def _pkg():
     return nbx
 
 
-def _time_calls(fn, iters):
+_ALIGN = []   # set by run(): a tiny collective that lines the ranks up before a timed loop
+
+
+def _time_calls(fn, iters, warmup=2):
+    """ms per call of `fn` after `warmup` untimed calls, started with the ranks
+    lined up (a small AllReduce + device sync), so no rank's timed loop absorbs
+    a peer's late arrival."""
     import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    for f in _ALIGN:
+        f()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(iters):
         fn()
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) * 1e3 / iters
+
+
+SWEEP_BYTES = [4 << 10, 32 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]
+SWEEP_PROTOS = (("LL", {"NCCL_PROTO": "LL", "NBX_LL_MAX_BYTES": str(16 << 20)}),
+                ("LL128", {"NCCL_PROTO": "LL128", "NBX_LL128_MAX_BYTES": str(16 << 20)}),
+                ("Simple", {"NCCL_PROTO": "Simple"}))
+
+
+def protocol_sweep(ids, rank, world, st, shared_gpu, res):
+    """AllReduce fp32 sum latency per protocol and message size (one
+    communicator per protocol, forced by NCCL_PROTO at init, the LL / LL128
+    buffers enlarged to 16 MiB), each size checked exactly once."""
+    import torch
+    from __graft_entry__ import _load_package
+    nbx = _load_package()
+    sizes = [b for b in SWEEP_BYTES if not shared_gpu or b <= (1 << 20)]
+    res["sweep_bytes"] = sizes
+    for (name, env), uid in zip(SWEEP_PROTOS, ids):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            c = nbx.Communicator.init_rank(world, nbx.ncclUniqueId.from_buffer_copy(bytes.fromhex(uid)), rank)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        times = []
+        for b in sizes:
+            n = b // 4
+            idx = torch.arange(n, dtype=torch.int32, device="cuda")
+            x = ((idx * 5 + 3 * rank) % 512).to(torch.float32)
+            want = sum(((idx * 5 + 3 * r) % 512).to(torch.float32) for r in range(world))
+            y = torch.empty_like(x)
+            c.all_reduce(x.data_ptr(), y.data_ptr(), n, 7, 0, st)
+            torch.cuda.synchronize()
+            if not torch.equal(y, want):
+                res["ok"] = False
+                res["errors"].append(f"sweep {name} {b} B: output differs")
+            iters = 50 if b <= (1 << 20) else 20
+            for _ in range(5):
+                c.all_reduce(x.data_ptr(), y.data_ptr(), n, 7, 0, st)
+            times.append(round(1e3 * _time_calls(lambda: c.all_reduce(x.data_ptr(), y.data_ptr(), n, 7, 0, st),
+                                                 iters), 2))
+        res["sweep_" + name + "_us"] = times
+        if c.async_error() != 0:
+            res["ok"] = False
+            res["errors"].append(f"sweep {name}: async error")
+        c.destroy()
 
 
 def run(ids, rank, world, dev):
@@ -73,6 +140,9 @@ def run(ids, rank, world, dev):
     st = torch.cuda.current_stream().cuda_stream
     F32, SUM = 7, 0
     res = {"rank": rank, "ok": True, "errors": []}
+    al_x = torch.ones(16, device="cuda")
+    al_y = torch.empty_like(al_x)
+    _ALIGN[:] = [lambda: comm.all_reduce(al_x.data_ptr(), al_y.data_ptr(), 16, F32, SUM, st)]
 
     idx = torch.arange(COUNT, dtype=torch.int32, device="cuda")
     x = ((idx * 7 + 13 * rank) % 1024).to(torch.float32)
@@ -88,6 +158,7 @@ def run(ids, rank, world, dev):
             bad = int((got != want).sum().item())
             res["errors"].append(f"{name}: {bad} elements differ")
 
+    _progress("communicators ready")
     for name, c in (("allreduce_direct", comm), ("allreduce_ring", comm_ring)):
         y.zero_()
         c.all_reduce(x.data_ptr(), y.data_ptr(), COUNT, F32, SUM, st)
@@ -107,6 +178,7 @@ def run(ids, rank, world, dev):
     res["reduce_scatter_ms"] = _time_calls(lambda: comm.reduce_scatter(x.data_ptr(), yr.data_ptr(), rc, F32, SUM, st),
                                            ITERS)
 
+    _progress("config D done")
     # LL128 (1 MiB): exact on every one of LL128_ITERS calls with inputs that
     # change per call (a torn line or a stale slot would show up as a
     # wrong value), then the per-call latency
@@ -138,7 +210,11 @@ def run(ids, rank, world, dev):
 
     del x, y, yr, exp, x1, e1, y1, xs, ys
     torch.cuda.empty_cache()
+    _progress("LL / LL128 done")
     config_e(comm, rank, world, st, res)
+    _progress("config E done")
+    protocol_sweep(ids[2:5], rank, world, st, "NBX_BENCH_DEVICE" in os.environ, res)
+    _progress("protocol sweep done")
 
     torch.cuda.synchronize()
     if comm.async_error() != 0 or comm_ring.async_error() != 0:
@@ -224,18 +300,19 @@ def main():
     dev = int(os.environ.get("NBX_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
     os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "120")
-    if "NBX_BENCH_DEVICE" in os.environ:   # rehearsal: every rank on one GPU, keep LL128 grids co-resident
+    if "NBX_BENCH_DEVICE" in os.environ:   # rehearsal: every rank on one GPU, keep LL/LL128 grids co-resident
         os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
+        os.environ.setdefault("NBX_LL_MAX_GRID", "64")
     for line in sys.stdin:
         parts = line.split()
         if not parts:
             continue
         if parts[0] == "ID":
             nbx = _pkg()   # imports torch first (one HIP runtime); no GPU use: the root is a host thread
-            _emit("ID " + " ".join(bytes(nbx.get_unique_id()).hex() for _ in range(2)))
+            _emit("ID " + " ".join(bytes(nbx.get_unique_id()).hex() for _ in range(5)))
         elif parts[0] == "RUN":
             try:
-                res = run(parts[1:3], rank, world, dev)
+                res = run(parts[1:6], rank, world, dev)
             except Exception as e:   # reported to the parent, never raised past it
                 res = {"rank": rank, "ok": False, "errors": [f"{type(e).__name__}: {e}"]}
             _emit("RESULT " + json.dumps(res))

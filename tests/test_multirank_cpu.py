@@ -62,7 +62,9 @@ for line in sys.stdin:
             import time; time.sleep(600)
         print("RESULT " + json.dumps({"rank": rank, "ok": True, "errors": [],
               "allreduce_direct_ms": 10.0 + rank, "allreduce_ring_ms": 20.0 + rank,
-              "reduce_scatter_ms": 5.0 + rank, "ll_allreduce_4KiB_us": 7.0 + rank}), flush=True)
+              "reduce_scatter_ms": 5.0 + rank, "ll_allreduce_4KiB_us": 7.0 + rank,
+              "sweep_bytes": [4096, 65536], "sweep_LL_us": [3.0 + rank, 9.0 - rank],
+              "sweep_LL128_us": [4.0, 5.0], "sweep_Simple_us": [50.0, 60.0 + rank]}), flush=True)
         break
 '''
 
@@ -109,6 +111,9 @@ def test_collective_leg_protocol_gloo(tmp_path, mode):
         assert out["reduce_scatter"]["ms"] == 6.0
         assert abs(out["reduce_scatter"]["busbw_GBs"] - round(S / 6e-3 / 1e9 * (world - 1) / world, 2)) < 1e-9
         assert out["ll_allreduce_4KiB_us"] == 8.0
+        sw = out["protocol_sweep"]   # column-wise max over ranks
+        assert sw["bytes"] == [4096, 65536]
+        assert sw["LL"] == [4.0, 9.0] and sw["LL128"] == [4.0, 5.0] and sw["Simple"] == [50.0, 61.0]
     else:
         assert out["ok"] is False
         assert any(e.startswith("rank 1:") for e in out["errors"])
