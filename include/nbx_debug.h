@@ -4,6 +4,8 @@
 #ifndef NBX_DEBUG_H_
 #define NBX_DEBUG_H_
 
+#include <stdint.h>
+
 #include "nccl.h"
 
 #ifdef __cplusplus
@@ -15,6 +17,14 @@ extern "C" {
  * varying length, verifying every contribution. Exercises the host bootstrap
  * that multi-process ncclCommInitRank uses (the role of src/bootstrap.cc). */
 ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds);
+
+/* NCCL_PROTO parsing (tuning.cc:254-259 list syntax: "LL,LL128", "^Simple",
+ * case-insensitive; NULL or "" = all): bit 0 LL, bit 1 LL128, bit 2 Simple. */
+int nbxDebugProtoMask(const char* ncclProto);
+
+/* The multi-process communicator's per-message protocol choice: 0 LL, 1 LL128,
+ * 2 Simple, for a message (per-rank block for ReduceScatter) of slotBytes. */
+int nbxDebugChooseProto(int protoMask, uint64_t slotBytes, int nRanks, uint64_t llMaxBytes, uint64_t ll128MaxBytes);
 
 #ifdef __cplusplus
 }

@@ -504,7 +504,12 @@ struct MpState {
   int* hostWordsDev = nullptr;
   uint64_t seq = 0;
   double timeoutSec = 300.0;
-  std::map<std::pair<int, std::string>, void*> maps;   // (peer, ipc handle) -> mapped base
+  struct Mapping {
+    void* base;
+    uint64_t lastUse;   // seq of the last collective that used it
+  };
+  std::map<std::pair<int, std::string>, Mapping> maps;   // (peer, ipc handle) -> mapped base
+  size_t mapsMax = 512;   // NBX_IPC_CACHE_MAX: beyond this, unused mappings are closed
   // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] lines + [n] done words +
   // arrival counter; peers' buffers mapped
   uint64_t* ll = nullptr;
@@ -546,8 +551,7 @@ struct MpInitInfo {
 // fallback when Simple is disabled and nothing else fits).
 // Read when the communicator is created (as NCCL reads its tuning env at init).
 enum { kProtoLL = 1, kProtoLL128 = 2, kProtoSimple = 4, kProtoAll = 7 };
-int protoFromEnv() {
-  const char* v = std::getenv("NCCL_PROTO");
+int protoFromString(const char* v) {
   if (v == nullptr || *v == 0) return kProtoAll;
   bool exclude = v[0] == '^';
   std::string list(exclude ? v + 1 : v);
@@ -565,13 +569,17 @@ int protoFromEnv() {
   }
   return exclude ? (kProtoAll & ~mask) : mask;
 }
+int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
 
-enum MpProto { kMpLL, kMpLL128, kMpSimple };
-MpProto chooseProto(const MpState* mp, uint64_t slotBytes, int n) {
+enum MpProto { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2 };
+MpProto chooseProtoFor(int mask, uint64_t slotBytes, int n, uint64_t llMax, uint64_t l128Max) {
   if (slotBytes == 0 || n > 64) return kMpSimple;
-  if ((mp->protoMask & kProtoLL) && slotBytes <= mp->llMaxBytes) return kMpLL;
-  if ((mp->protoMask & kProtoLL128) && mp->l128MaxBytes != 0 && slotBytes <= mp->l128MaxBytes) return kMpLL128;
+  if ((mask & kProtoLL) && slotBytes <= llMax) return kMpLL;
+  if ((mask & kProtoLL128) && l128Max != 0 && n <= nbx::kL128MaxRanksHost && slotBytes <= l128Max) return kMpLL128;
   return kMpSimple;
+}
+MpProto chooseProto(const MpState* mp, uint64_t slotBytes, int n) {
+  return chooseProtoFor(mp->protoMask, slotBytes, n, mp->llMaxBytes, mp->l128MaxBytes);
 }
 
 struct MpCallInfo {
@@ -596,12 +604,13 @@ ncclResult_t mapPeer(MpState* mp, int peer, const hipIpcMemHandle_t& h, void** b
   auto key = std::make_pair(peer, std::string((const char*)&h, sizeof(h)));
   auto it = mp->maps.find(key);
   if (it != mp->maps.end()) {
-    *base = it->second;
+    it->second.lastUse = mp->seq;
+    *base = it->second.base;
     return ncclSuccess;
   }
   void* p = nullptr;
   HIPCHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  mp->maps[key] = p;
+  mp->maps[key] = MpState::Mapping{p, mp->seq};
   *base = p;
   return ncclSuccess;
 }
@@ -648,6 +657,8 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   c->mp = mp;
   const char* t = std::getenv("NBX_TIMEOUT_SEC");
   if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
+  const char* cm = std::getenv("NBX_IPC_CACHE_MAX");
+  if (cm && std::atol(cm) > 0) mp->mapsMax = (size_t)std::atol(cm);
   mp->protoMask = protoFromEnv();
   mp->ring = algoRingFromEnv();
   NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
@@ -758,7 +769,7 @@ void mpFree(ncclComm* c) {
   if (!mp) return;
   DevGuard g(c->device);
   (void)hipDeviceSynchronize();
-  for (auto& kv : mp->maps) (void)hipIpcCloseMemHandle(kv.second);
+  for (auto& kv : mp->maps) (void)hipIpcCloseMemHandle(kv.second.base);
   for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerL128Maps) (void)hipIpcCloseMemHandle(p);
@@ -849,6 +860,21 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     }
   }
   if (count == 0) return ncclSuccess;
+  // Bound the mapping cache: a peer's freed-and-reallocated buffers come back
+  // with new handles, and every open mapping pins the peer's old allocation.
+  // Past the bound, wait for this device's work (no kernel in flight uses a
+  // mapping), then close every mapping not used by the previous call.
+  if (mp->maps.size() > mp->mapsMax) {
+    HIPCHECK(hipDeviceSynchronize());
+    for (auto it = mp->maps.begin(); it != mp->maps.end();) {
+      if (it->second.lastUse + 1 < seq) {
+        (void)hipIpcCloseMemHandle(it->second.base);
+        it = mp->maps.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
   std::vector<const char*> sendP(n, nullptr);
   std::vector<char*> recvP(n, nullptr);
   for (int j = 0; j < n; j++) {
@@ -1296,6 +1322,13 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
   }
   if (--t_groupDepth > 0) return ncclSuccess;
   return flushPending();
+}
+
+NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
+
+NBX_EXPORT int nbxDebugChooseProto(int protoMask, uint64_t slotBytes, int nRanks, uint64_t llMaxBytes,
+                                   uint64_t ll128MaxBytes) {
+  return (int)chooseProtoFor(protoMask, slotBytes, nRanks, llMaxBytes, ll128MaxBytes);
 }
 
 NBX_EXPORT ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds) {

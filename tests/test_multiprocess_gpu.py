@@ -67,20 +67,23 @@ def _blocks(count, eb, n):
     return [(min(count, per * b), min(count, per * b + per)) for b in range(n)]
 
 
-@pytest.mark.parametrize("n,algo,proto", [(2, "direct", "LL,Simple"), (3, "direct", "LL,Simple"),
-                                          (3, "ring", "LL,Simple"), (4, "ring", "LL,Simple"), (3, "direct", "")])
-def test_multiprocess_collectives(nbx, oracle, n, algo, proto, monkeypatch):
+@pytest.mark.parametrize("n,algo,proto,cache", [(2, "direct", "LL,Simple", ""), (3, "direct", "LL,Simple", ""),
+                                                (3, "ring", "LL,Simple", ""), (4, "ring", "LL,Simple", ""),
+                                                (3, "direct", "", ""), (3, "direct", "LL,Simple", "2")])
+def test_multiprocess_collectives(nbx, oracle, n, algo, proto, cache, monkeypatch):
     """NCCL_ALGO=Ring: NCCL's ring order (chunk c from rank c+1 to c, Fn(local,
     received)); for the commutative ops tested it is bit-identical to the
     oracle's left fold in the order c+1, ..., c. NCCL_PROTO=LL,Simple keeps the
     40009-element messages on the Simple (direct / ring) path; the default
-    sends most of them through LL128."""
+    sends most of them through LL128. NBX_IPC_CACHE_MAX=2 makes nearly every
+    Simple call close and re-open peer mappings (fresh buffers per case)."""
     # bounded waits everywhere: a failing rank must not strand its peers
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
     monkeypatch.setenv("NCCL_PROTO", proto)
     monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
+    monkeypatch.setenv("NBX_IPC_CACHE_MAX", cache)
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -1,0 +1,49 @@
+"""Protocol selection of the multi-process communicator, on the CPU through
+the library's debug hooks (include/nbx_debug.h): NCCL_PROTO parsing in NCCL's
+list syntax (tuning.cc:254-259: "LL,LL128", "^Simple", case-insensitive) and
+the per-message choice LL (<= LL max) -> LL128 (<= LL128 max, <= 8 ranks) ->
+Simple."""
+import ctypes
+
+import pytest
+
+LL, LL128, SIMPLE, ALL = 1, 2, 4, 7
+P_LL, P_LL128, P_SIMPLE = 0, 1, 2
+
+
+@pytest.fixture(scope="module")
+def lib(nbx):
+    lib = nbx.load_library()
+    lib.nbxDebugProtoMask.argtypes = [ctypes.c_char_p]
+    lib.nbxDebugProtoMask.restype = ctypes.c_int
+    lib.nbxDebugChooseProto.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+    lib.nbxDebugChooseProto.restype = ctypes.c_int
+    return lib
+
+
+@pytest.mark.parametrize("s,mask", [
+    (None, ALL), ("", ALL), ("LL", LL), ("ll128", LL128), ("Simple", SIMPLE), ("LL,Simple", LL | SIMPLE),
+    ("LL128,LL", LL | LL128), ("^LL128", LL | SIMPLE), ("^ll,simple", LL128), ("^", ALL), ("LL,,Simple", LL | SIMPLE),
+    ("bogus", 0), ("LL,bogus", LL),
+])
+def test_nccl_proto_parsing(lib, s, mask):
+    assert lib.nbxDebugProtoMask(None if s is None else s.encode()) == mask
+
+
+K, M = 1 << 10, 1 << 20
+
+
+@pytest.mark.parametrize("mask,nbytes,n,want", [
+    (ALL, 4, 2, P_LL), (ALL, 64 * K, 8, P_LL), (ALL, 64 * K + 1, 8, P_LL128), (ALL, M, 8, P_LL128),
+    (ALL, M + 1, 8, P_SIMPLE), (ALL, 256 * K, 9, P_SIMPLE),          # LL128 only up to 8 ranks
+    (ALL, 4 * K, 9, P_LL), (ALL, 0, 4, P_SIMPLE), (ALL, 4 * K, 65, P_SIMPLE),
+    (LL | SIMPLE, 256 * K, 4, P_SIMPLE), (LL128 | SIMPLE, 4, 4, P_LL128), (SIMPLE, 4, 4, P_SIMPLE),
+    (LL, 256 * K, 4, P_SIMPLE),                                        # nothing enabled fits: Simple
+    (LL128, 2 * M, 4, P_SIMPLE),
+])
+def test_protocol_choice(lib, mask, nbytes, n, want):
+    assert lib.nbxDebugChooseProto(mask, nbytes, n, 64 * K, M) == want
+
+
+def test_ll128_disabled_by_zero_max(lib):
+    assert lib.nbxDebugChooseProto(ALL, 256 * K, 4, 64 * K, 0) == P_SIMPLE
