@@ -14,9 +14,13 @@
 // with a direct one-shot exchange over xGMI peer access: rank r's kernel reads
 // block r of every rank's send buffer (nSrcs = nRanks, the CollNet-direct
 // shape all_reduce.h:318-327), folding in ring order r+1, r+2, ..., r — the
-// order in which NCCL's ring reduce-scatter accumulates block r — then the
-// reduced blocks are gathered peer-to-peer. Cross-device ordering is by HIP
-// events (stream-ordered, asynchronous, graph-capturable), not spin flags.
+// order in which NCCL's ring reduce-scatter accumulates block r — and, for
+// AllReduce, storing the finished block into every rank's output from the
+// same kernel (push-gather, all_reduce.h:343-360). Cross-device ordering is by
+// HIP events (stream-ordered, asynchronous, graph-capturable), not spin flags.
+// One process per GPU (ncclCommInitRank, nranks > 1) runs the same schedules
+// over hipIpc-mapped peer buffers with device flag barriers, plus the LL /
+// LL128 protocols for small / medium messages (nbx_ll.h).
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
