@@ -322,3 +322,33 @@ def test_host_staged_reduce(nbx, oracle, torch_gpu, monkeypatch, dtype, devop, c
     exp = oracle.reduce_multi(srcs, dtype, devop, arg, npre, devop == 4, threads=8)[0]
     for o in outs:
         assert_same(o, exp, dtype)
+
+
+def test_beyond_32bit_counts(nbx, torch_gpu):
+    """Maximum sizes: element counts and byte offsets past 2^32 (u8 sum of
+    4 GiB + 37 elements; f32 sum of 2^30 + 5 elements = 4 GiB + 20 B per
+    buffer), plus a 1-element head from a shared misalignment, checked in full
+    against torch on the GPU (u8 + wraps like the SWAR functor; one f32 add is
+    correctly rounded either way)."""
+    torch = torch_gpu
+    st = torch.cuda.current_stream().cuda_stream
+    n = (1 << 32) + 37
+    g = torch.Generator(device="cuda").manual_seed(99)
+    a = torch.randint(0, 256, (n + 1,), dtype=torch.uint8, device="cuda", generator=g)
+    b = torch.randint(0, 256, (n + 1,), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.empty(n + 1, dtype=torch.uint8, device="cuda")
+    op = nbx.host_to_dev_redop(nbx.ncclRedOp.ncclSum, nbx.ncclDataType.ncclUint8, 1)
+    # one byte in: every pointer shares misalignment 1 (head element + aligned body + tail)
+    nbx.reduce_multi([out.data_ptr() + 1], [a.data_ptr() + 1, b.data_ptr() + 1], n, 1, op, 0, False, st)
+    torch.cuda.synchronize()
+    assert torch.equal(out[1:], a[1:] + b[1:])
+    del a, b, out
+    torch.cuda.empty_cache()
+    m = (1 << 30) + 5
+    x = torch.rand(m, device="cuda", generator=g)
+    y = torch.rand(m, device="cuda", generator=g)
+    o = torch.empty_like(x)
+    op = nbx.host_to_dev_redop(nbx.ncclRedOp.ncclSum, nbx.ncclDataType.ncclFloat32, 1)
+    nbx.reduce_multi([o.data_ptr()], [x.data_ptr(), y.data_ptr()], m, 7, op, 0, False, st)
+    torch.cuda.synchronize()
+    assert torch.equal(o, x + y)
