@@ -6,11 +6,9 @@
 
 namespace nbx {
 struct LLArgs;
-// Launch the LL collective kernel of (datatype, op) (nbx_ll.h); sets args.arriveTarget from *arrived and
-// advances it by the grid size.
-ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t* arrived,
-                          hipStream_t stream);
-// The same for the LL128 kernel (args.nLines lines of 128 bytes).
-ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t* arrived,
-                             hipStream_t stream);
+// Launch the LL collective kernel of (datatype, op) (nbx_ll.h); sequencing is
+// device-resident (args.state).
+ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
+// The same for the LL128 kernel (args.nLines 64-byte lines).
+ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
 }  // namespace nbx

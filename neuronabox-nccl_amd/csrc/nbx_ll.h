@@ -8,8 +8,11 @@
 // Each rank owns an IPC-registered, uncached LL buffer laid out
 //   [parity 2][source rank n][lines 2 * maxPacks]   data lines (8 bytes)
 //   [done n]                                        done words, one per writer
-//   [arrive 1]                                      local block-arrival counter
-// and the kernel of rank r
+// plus a private LLState (seq, per-parity last seq, block-arrival counter) in
+// plain device memory; the sequence lives on the device so a graph-captured
+// call replays with fresh numbers. The kernel of rank r
+//   -. reads seq = state.seq + 1 (parity seq & 1, credit target
+//      state.lastSeq[parity]);
 //   0. waits until every peer it pushes to has finished reading the last LL
 //      call that used this parity (that peer's done word >= needDone) — the
 //      credit that makes a slot reusable even when a rank never waits for
@@ -27,7 +30,7 @@
 //        ReduceScatter  — ranks r+1, ..., r       (reduce_scatter.h:50-64)
 //        Reduce (root)  — ranks root+1, ..., root (reduce.h:44-67);
 //   3. stores the result; the last block to finish publishes this rank's
-//      done word (= seq) into every peer's buffer.
+//      done word (= seq) into every peer's buffer and advances the state.
 #pragma once
 #include "nbx_functors.h"
 #include "nbx_ll_args.h"
@@ -78,6 +81,38 @@ __device__ __forceinline__ bool llIsTarget(const LLArgs& a, int j) {
   return a.mode != kLLReduce || j == a.root;
 }
 
+// This launch's sequence number, parity and credit target (see LLState).
+struct LLCall {
+  uint64_t seq;
+  uint64_t needDone;
+  int parity;
+  uint32_t flag;
+};
+
+__device__ __forceinline__ LLCall llBegin(const LLArgs& a) {
+  LLCall c;
+  c.seq = __hip_atomic_load(&a.state->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  c.parity = (int)(c.seq & 1u);
+  c.needDone = __hip_atomic_load(&a.state->lastSeq[c.parity], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  c.flag = (uint32_t)c.seq;
+  return c;
+}
+
+// Thread 0 of every block, after the block's reads of its own slots: the last
+// block to arrive publishes this rank's done word (= seq) in every peer's
+// buffer and advances the state for the next launch.
+__device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c) {
+  const uint64_t prev = __hip_atomic_fetch_add(&a.state->arrive, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev + 1 != (uint64_t)gridDim.x) return;
+  for (int j = 0; j < a.nRanks; j++) {
+    if (j == a.rank) continue;
+    __hip_atomic_store(a.peerLL[j] + a.doneOff + a.rank, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __hip_atomic_store(&a.state->lastSeq[c.parity], c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&a.state->arrive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&a.state->seq, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <class Fn>
 __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   using E = typename Fn::Elt;
@@ -85,7 +120,8 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
   const uint64_t bytes = a.count * sizeof(E);   // bytes per slot
-  const uint64_t flagHi = (uint64_t)a.flag << 32;
+  const LLCall call = llBegin(a);
+  const uint64_t flagHi = (uint64_t)call.flag << 32;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int sFailed;
@@ -93,8 +129,8 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   __syncthreads();
 
   // 0. credits: each target has finished reading this parity's previous use
-  if (a.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
-    if (!llWait(a.myLL + a.doneOff + threadIdx.x, a.needDone, a, t0)) sFailed = 1;
+  if (call.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0)) sFailed = 1;
   }
   __syncthreads();
   bool failed = sFailed != 0;
@@ -110,7 +146,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
                                ? llLoadBytes((const unsigned char*)a.send + (uint64_t)j * bytes, k * 8, bytes)
                                : whole;
         const uint64_t l0 = (v & 0xffffffffull) | flagHi, l1 = (v >> 32) | flagHi;
-        uint64_t* line = a.peerLL[j] + ((uint64_t)(a.parity * n + me) * a.slotLines + 2 * k);
+        uint64_t* line = a.peerLL[j] + ((uint64_t)(call.parity * n + me) * a.slotLines + 2 * k);
         __hip_atomic_store(line, l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(line + 1, l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -140,13 +176,13 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
       if (j == me) {
         x.u = llLoadBytes(own, k * 8, bytes);
       } else {
-        const uint64_t* line = a.myLL + ((uint64_t)(a.parity * n + j) * a.slotLines + 2 * k);
+        const uint64_t* line = a.myLL + ((uint64_t)(call.parity * n + j) * a.slotLines + 2 * k);
         uint64_t l0 = 0, l1 = 0;
         uint32_t spins = 0;
         while (!failed) {
           l0 = __hip_atomic_load(line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           l1 = __hip_atomic_load(line + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          if ((uint32_t)(l0 >> 32) == a.flag && (uint32_t)(l1 >> 32) == a.flag) break;
+          if ((uint32_t)(l0 >> 32) == call.flag && (uint32_t)(l1 >> 32) == call.flag) break;
           if ((++spins & 1023u) == 0u) {
             if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
               *a.errWord = *a.abortWord != 0 ? 2 : 1;
@@ -174,16 +210,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
 
   // done word: after every block of this launch has consumed its lines
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t prev = __hip_atomic_fetch_add(a.arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev + 1 == a.arriveTarget) {
-      for (int j = 0; j < n; j++) {
-        if (j == me) continue;
-        __hip_atomic_store(a.peerLL[j] + a.doneOff + me, a.seq, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  if (threadIdx.x == 0) llEnd(a, call);
 }
 
 
@@ -248,13 +275,14 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) / kL128Lanes;
   const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kL128Lanes;
   const uint64_t t0 = wall_clock64();
+  const LLCall call = llBegin(a);
   __shared__ int sFailed;
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
 
   // 0. credits (as kLLColl)
-  if (a.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
-    if (!llWait(a.myLL + a.doneOff + threadIdx.x, a.needDone, a, t0)) sFailed = 1;
+  if (call.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0)) sFailed = 1;
   }
   __syncthreads();
   bool failed = sFailed != 0;
@@ -263,13 +291,13 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   if (!failed) {
     for (uint64_t i = g0; i < a.nLines; i += groups) {
       u32x4 whole = {0, 0, 0, 0};
-      if (a.mode != kLLReduceScatter) whole = l128Payload((const unsigned char*)a.send, bytes, i, t, a.seq);
+      if (a.mode != kLLReduceScatter) whole = l128Payload((const unsigned char*)a.send, bytes, i, t, call.seq);
       for (int j = 0; j < n; j++) {
         if (!llIsTarget(a, j)) continue;
         const u32x4 v = a.mode == kLLReduceScatter
-                            ? l128Payload((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, a.seq)
+                            ? l128Payload((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, call.seq)
                             : whole;
-        uint64_t* line = a.peerL128[j] + ((uint64_t)(a.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) +
+        uint64_t* line = a.peerL128[j] + ((uint64_t)(call.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) +
                          2 * t;
         l128StoreLine16(line, v);
       }
@@ -297,7 +325,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
 #pragma unroll
       for (int q = 0; q < kL128MaxRanks; q++) {
         if ((need >> q) & 1u) {
-          const uint32_t off = (uint32_t)((((uint64_t)(a.parity * n + q)) * a.l128SlotLines + i) *
+          const uint32_t off = (uint32_t)((((uint64_t)(call.parity * n + q)) * a.l128SlotLines + i) *
                                           kL128LineBytes) + (uint32_t)t * 16u;
           v[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kL128LoadAux));
         }
@@ -307,7 +335,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
         if ((need >> q) & 1u) {
           const uint64_t fw = ((uint64_t)v[q].w << 32) | v[q].z;
           // the group's last lane holds the flag
-          if (__shfl((int)(fw == a.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
+          if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
         }
       }
       if (need != 0 && (++spins & 1023u) == 0u) {
@@ -357,15 +385,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
 
   // done word (as kLLColl)
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint64_t prev = __hip_atomic_fetch_add(a.arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev + 1 == a.arriveTarget) {
-      for (int j = 0; j < n; j++) {
-        if (j == me) continue;
-        __hip_atomic_store(a.peerLL[j] + a.doneOff + me, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-  }
+  if (threadIdx.x == 0) llEnd(a, call);
 }
 
 }  // namespace nbx

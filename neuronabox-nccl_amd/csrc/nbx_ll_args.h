@@ -11,6 +11,18 @@ constexpr int kL128LineBytesHost = 64;  // LL128 line: 56 payload bytes + 8-byte
 constexpr int kL128DataBytesHost = 56;
 constexpr int kL128LanesHost = 4;       // lanes (16 bytes each) per LL128 line
 
+// Device-resident sequencing of the LL-family calls of one communicator
+// (plain device memory of this rank, zero at init). Kept on the device, not
+// passed by the host, so a captured graph replays with fresh sequence numbers:
+// every block of a launch reads seq at its start; the launch's last block
+// (the one whose arrival completes `arrive`) publishes the done words, then
+// advances seq / lastSeq and resets `arrive` for the next launch.
+struct LLState {
+  uint64_t seq;         // last completed LL-family call (the pending one is seq + 1)
+  uint64_t lastSeq[2];  // last call that used each parity's slots (credit target)
+  uint64_t arrive;      // blocks of the running launch that have finished
+};
+
 struct LLArgs {
   const void* send;
   void* recv;
@@ -20,10 +32,7 @@ struct LLArgs {
   uint64_t* myLL;
   uint64_t slotLines;      // lines per (parity, source) slot = 2 * max packs
   uint64_t doneOff;        // line index of the done words (one per writer rank) in every LL buffer
-  uint64_t* arrive;        // local block-arrival counter (monotonic)
-  uint64_t arriveTarget;   // counter value after the last block of this launch arrives
-  uint64_t needDone;       // before pushing to peer j: wait until j's done word >= needDone
-  uint64_t seq;            // this call's sequence number (published as the done word)
+  LLState* state;          // this rank's sequencing state (device memory)
   uint64_t blockElts;      // AllReduce: direct-schedule block size (elements) -> fold order
   uint64_t arg;            // functor scalar (by value)
   const void* argPtr;      // device scalar or nullptr
@@ -36,8 +45,6 @@ struct LLArgs {
   uint64_t l128SlotLines;     // lines per (parity, source) slot
   uint64_t nLines;            // lines covering this call's slot bytes
   uint32_t l128Bytes;         // size of myL128 (buffer-descriptor range, < 4 GiB)
-  uint32_t flag;
-  int32_t parity;
   int32_t rank;
   int32_t nRanks;
   int32_t postOp;

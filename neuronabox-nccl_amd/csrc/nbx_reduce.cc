@@ -168,8 +168,7 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
 }  // namespace
 
 namespace nbx {
-ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, uint64_t* arrived,
-                          hipStream_t stream) {
+ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
   if (!ks.valid || ks.ll == nullptr) return ncclInvalidArgument;
@@ -186,16 +185,13 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
   size_t grid = (a.nPacks + 255) / 256;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
-  a.arriveTarget = *arrived + grid;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
-  *arrived = a.arriveTarget;
   return ncclSuccess;
 }
 
-ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, uint64_t* arrived,
-                             hipStream_t stream) {
+ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
   if (!ks.valid || ks.ll128 == nullptr) return ncclInvalidArgument;
@@ -214,11 +210,9 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   size_t grid = (a.nLines + linesPerBlock - 1) / linesPerBlock;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
-  a.arriveTarget = *arrived + grid;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll128, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
-  *arrived = a.arriveTarget;
   return ncclSuccess;
 }
 }  // namespace nbx

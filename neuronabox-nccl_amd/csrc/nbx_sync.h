@@ -4,9 +4,10 @@
 #include <stdint.h>
 
 namespace nbx {
-// Post `postValue` to this rank's flag `slot`; wait until every rank in
-// `waitMask` (bit j = rank j) has flag `slot` >= `waitValue`.
-hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t postValue,
-                             uint64_t waitValue, uint64_t waitMask, const int* abortWordDev, int* errWordDev,
-                             double timeoutSec, hipStream_t stream);
+// Advance this rank's epoch of `slot` (epochsDev: device counters, one per
+// slot) to v, post v to flag `slot`; wait until every rank in `waitMask`
+// (bit j = rank j) has flag `slot` >= v.
+hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t waitMask,
+                             uint64_t* epochsDev, const int* abortWordDev, int* errWordDev, double timeoutSec,
+                             hipStream_t stream);
 }  // namespace nbx

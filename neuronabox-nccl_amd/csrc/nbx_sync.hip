@@ -15,18 +15,26 @@
 
 namespace nbx {
 
-// Posts `postValue` to this rank's flag `slot`, then waits until every rank j
-// with bit j of `waitMask` has flag `slot` >= `waitValue`.
+// Advances this rank's epoch of flag `slot` (plain device memory, one counter
+// per slot) to v, posts v to the flag, then waits until every rank j with bit j
+// of `waitMask` has flag `slot` >= v. Every rank issues the same sequence of
+// barriers on a slot, so the epochs agree without the host passing values —
+// which is what lets a graph-captured collective replay.
 __global__ __launch_bounds__(64) void kPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlags, int n, int slot,
-                                                   uint64_t postValue, uint64_t waitValue, uint64_t waitMask,
+                                                   uint64_t waitMask, uint64_t* epochs,
                                                    const volatile int* abortWord, volatile int* errWord,
                                                    uint64_t timeoutTicks) {
   const int lane = (int)threadIdx.x;
-  const uint64_t seq = waitValue;
+  __shared__ uint64_t sV;
   if (lane == 0) {
+    const uint64_t v = epochs[slot] + 1;
+    epochs[slot] = v;
+    sV = v;
     __atomic_thread_fence(__ATOMIC_RELEASE);   // order prior work of this kernel (none) and the flag
-    __hip_atomic_store(myFlags + slot, postValue, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(myFlags + slot, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  __syncthreads();
+  const uint64_t seq = sV;
   if (lane < n && ((waitMask >> lane) & 1ull)) {
     const uint64_t* f = peerFlags[lane] + slot;
     const uint64_t t0 = wall_clock64();
@@ -49,13 +57,13 @@ __global__ __launch_bounds__(64) void kPeerBarrier(uint64_t* myFlags, uint64_t* 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: drop stale cached peer data
 }
 
-hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t postValue,
-                             uint64_t waitValue, uint64_t waitMask, const int* abortWordDev, int* errWordDev,
-                             double timeoutSec, hipStream_t stream) {
+hipError_t launchPeerBarrier(uint64_t* myFlags, uint64_t* const* peerFlagsDev, int n, int slot, uint64_t waitMask,
+                             uint64_t* epochsDev, const int* abortWordDev, int* errWordDev, double timeoutSec,
+                             hipStream_t stream) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
   const uint64_t ticks = (uint64_t)(timeoutSec * 1.0e8);   // wall_clock64 runs at 100 MHz
-  hipLaunchKernelGGL(kPeerBarrier, dim3(1), dim3(64), 0, stream, myFlags, peerFlagsDev, n, slot, postValue,
-                     waitValue, waitMask, (const volatile int*)abortWordDev, (volatile int*)errWordDev, ticks);
+  hipLaunchKernelGGL(kPeerBarrier, dim3(1), dim3(64), 0, stream, myFlags, peerFlagsDev, n, slot, waitMask, epochsDev,
+                     (const volatile int*)abortWordDev, (volatile int*)errWordDev, ticks);
   return hipGetLastError();
 }
 

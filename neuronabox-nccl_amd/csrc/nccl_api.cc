@@ -510,8 +510,9 @@ struct MpState {
   double timeoutSec = 300.0;
   struct Mapping {
     void* base;
-    uint64_t lastUse;   // seq of the last collective that used it
+    uint64_t lastUse;   // seq of the last collective that used it; kPinned: used by a captured graph
   };
+  static constexpr uint64_t kPinned = ~0ull;
   std::map<std::pair<int, std::string>, Mapping> maps;   // (peer, ipc handle) -> mapped base
   size_t mapsMax = 512;   // NBX_IPC_CACHE_MAX: beyond this, unused mappings are closed
   // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] lines + [n] done words +
@@ -522,8 +523,8 @@ struct MpState {
   uint64_t llMaxBytes = 0;
   uint64_t llSlotLines = 0;
   uint64_t llDoneOff = 0;
-  uint64_t llLastSeq[2] = {0, 0};   // last LL call per parity (credit target)
-  uint64_t llArrived = 0;           // arrival-counter value after the last LL/LL128 launch
+  nbx::LLState* llState = nullptr;  // device-resident LL-family sequencing (nbx_ll_args.h)
+  uint64_t* epochs = nullptr;       // device-resident barrier epochs, one per flag slot
   // LL128 protocol (nbx_ll.h kLL128Coll): own buffer [2][n][l128SlotLines] 64-B lines;
   // shares the LL buffer's done words, arrival counter and parity credits
   uint64_t* l128 = nullptr;
@@ -604,33 +605,37 @@ ncclResult_t ipcHandleOf(const void* p, hipIpcMemHandle_t* h, uint64_t* off) {
   return ncclSuccess;
 }
 
-ncclResult_t mapPeer(MpState* mp, int peer, const hipIpcMemHandle_t& h, void** base) {
+// `pin`: the call is being captured into a graph, whose replays keep using the
+// mapping — it is never evicted.
+ncclResult_t mapPeer(MpState* mp, int peer, const hipIpcMemHandle_t& h, void** base, bool pin) {
   auto key = std::make_pair(peer, std::string((const char*)&h, sizeof(h)));
+  const uint64_t use = pin ? MpState::kPinned : mp->seq;
   auto it = mp->maps.find(key);
   if (it != mp->maps.end()) {
-    it->second.lastUse = mp->seq;
+    if (it->second.lastUse != MpState::kPinned) it->second.lastUse = use;
     *base = it->second.base;
     return ncclSuccess;
   }
   void* p = nullptr;
   HIPCHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  mp->maps[key] = MpState::Mapping{p, mp->seq};
+  mp->maps[key] = MpState::Mapping{p, use};
   *base = p;
   return ncclSuccess;
 }
 
-// Post `post` on `slot`, wait for the ranks in `mask` to reach `wait` on it.
-ncclResult_t mpSignalWait(ncclComm* comm, int slot, uint64_t post, uint64_t wait, uint64_t mask, hipStream_t stream) {
+// Advance this rank's epoch of `slot`, post it, wait for the ranks in `mask`
+// to reach it (epochs live on the device: graph replays stay in step).
+ncclResult_t mpSignalWait(ncclComm* comm, int slot, uint64_t mask, hipStream_t stream) {
   MpState* mp = comm->mp;
-  HIPCHECK(nbx::launchPeerBarrier(mp->flags, mp->peerFlagsDev, comm->nRanks, slot, post, wait, mask,
+  HIPCHECK(nbx::launchPeerBarrier(mp->flags, mp->peerFlagsDev, comm->nRanks, slot, mask, mp->epochs,
                                   mp->hostWordsDev, mp->hostWordsDev + 1, mp->timeoutSec, stream));
   return ncclSuccess;
 }
 
-ncclResult_t mpBarrier(ncclComm* comm, int slot, uint64_t seq, hipStream_t stream) {
+ncclResult_t mpBarrier(ncclComm* comm, int slot, hipStream_t stream) {
   const int n = comm->nRanks;
   const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
-  return mpSignalWait(comm, slot, seq, seq, all, stream);
+  return mpSignalWait(comm, slot, all, stream);
 }
 
 
@@ -668,6 +673,10 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
   HIPCHECK(allocSyncMem((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
   HIPCHECK(hipMemset(mp->flags, 0, kNumSlots * sizeof(uint64_t)));
+  HIPCHECK(hipMalloc((void**)&mp->epochs, kNumSlots * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->epochs, 0, kNumSlots * sizeof(uint64_t)));
+  HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
+  HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mp->hostWords, 0, 64);
   HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
@@ -782,6 +791,8 @@ void mpFree(ncclComm* c) {
   if (mp->peerFlagsDev) (void)hipFree(mp->peerFlagsDev);
   if (mp->peerLLDev) (void)hipFree(mp->peerLLDev);
   if (mp->ll) (void)hipFree(mp->ll);
+  if (mp->epochs) (void)hipFree(mp->epochs);
+  if (mp->llState) (void)hipFree(mp->llState);
   if (mp->flags) (void)hipFree(mp->flags);
   if (mp->hostWords) (void)hipHostFree(mp->hostWords);
   nbx::bootstrapClose(mp->bs);
@@ -804,7 +815,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
       warn("rank %d passed a NULL buffer", me);
       return ncclInvalidArgument;
     }
-    const uint64_t seq = ++mp->seq;
+    ++mp->seq;
     nbx::LLArgs la{};
     la.send = send;
     la.recv = recv;
@@ -814,18 +825,13 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     la.myLL = mp->ll;
     la.slotLines = mp->llSlotLines;
     la.doneOff = mp->llDoneOff;
-    la.arrive = mp->ll + mp->llDoneOff + n;
-    la.parity = (int32_t)(seq & 1);
-    la.needDone = mp->llLastSeq[la.parity];
-    mp->llLastSeq[la.parity] = seq;
-    la.seq = seq;
+    la.state = mp->llState;
     size_t off0, per;
     blockRange(count, eb, n, 0, &off0, &per);
     la.blockElts = per > 0 ? per : 1;
     la.abortWord = mp->hostWordsDev;
     la.errWord = mp->hostWordsDev + 1;
     la.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
-    la.flag = (uint32_t)seq;
     la.rank = me;
     la.nRanks = n;
     la.postOp = 1;
@@ -837,9 +843,9 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
       la.l128SlotLines = mp->l128SlotLines;
       la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
       la.l128Bytes = (uint32_t)mp->l128Bytes;
-      return nbx::launchLL128Coll(dt, op, la, &mp->llArrived, stream);
+      return nbx::launchLL128Coll(dt, op, la, stream);
     }
-    return nbx::launchLLColl(dt, op, la, &mp->llArrived, stream);
+    return nbx::launchLLColl(dt, op, la, stream);
   }
   const uint64_t seq = ++mp->seq;
   MpCallInfo mine{};
@@ -868,10 +874,13 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   // with new handles, and every open mapping pins the peer's old allocation.
   // Past the bound, wait for this device's work (no kernel in flight uses a
   // mapping), then close every mapping not used by the previous call.
-  if (mp->maps.size() > mp->mapsMax) {
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(stream, &capture));
+  const bool capturing = capture != hipStreamCaptureStatusNone;
+  if (mp->maps.size() > mp->mapsMax && !capturing) {
     HIPCHECK(hipDeviceSynchronize());
     for (auto it = mp->maps.begin(); it != mp->maps.end();) {
-      if (it->second.lastUse + 1 < seq) {
+      if (it->second.lastUse != MpState::kPinned && it->second.lastUse + 1 < seq) {
         (void)hipIpcCloseMemHandle(it->second.base);
         it = mp->maps.erase(it);
       } else {
@@ -889,11 +898,11 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     }
     void* b = nullptr;
     if (all[j].hasSend) {
-      NCCLCHECK(mapPeer(mp, j, all[j].sendH, &b));
+      NCCLCHECK(mapPeer(mp, j, all[j].sendH, &b, capturing));
       sendP[j] = (const char*)b + all[j].sendOff;
     }
     if (all[j].hasRecv) {
-      NCCLCHECK(mapPeer(mp, j, all[j].recvH, &b));
+      NCCLCHECK(mapPeer(mp, j, all[j].recvH, &b, capturing));
       recvP[j] = (char*)b + all[j].recvOff;
     }
   }
@@ -904,7 +913,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     }
   // 1. every rank's stream has reached the collective (its inputs are written,
   //    its output may be written by peers)
-  NCCLCHECK(mpBarrier(comm, kSlotEnter, seq, stream));
+  NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
   const size_t total = kind == kReduceScatter ? count * (size_t)n : count;
   // AllReduce with n <= NBX_MAX_DSTS: push-gather — the kernel completing a
   // block stores it into every rank's output at once (all xGMI links busy in
@@ -927,7 +936,6 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     // neighbour's raw input (its `send`, PreOp applies to both sources); the last
     // step (c == me) applies postOp. Every rank works on a different chunk at
     // each step, so all ring links carry 1/n of the data concurrently.
-    const uint64_t base = seq * 64;
     const int left = (me + n - 1) % n;
     for (int st = 0; st < n - 1; st++) {
       const int c = ((me - 2 - st) % n + n) % n;
@@ -941,7 +949,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
         NCCLCHECK(nbxReduceMulti(last && push ? allOutputs(off) : dsts, last && push ? n : 1, srcs, 2, len, dt, op,
                                  st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream));
       }
-      if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, base + st + 1, base + st + 1, 1ull << left, stream));
+      if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, 1ull << left, stream));
     }
   } else {
   // 2. direct reduce of this rank's block
@@ -967,7 +975,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   }
   // 3. AllReduce with n > NBX_MAX_DSTS: gather the peers' reduced blocks
   if (kind == kAllReduce && !push) {
-    NCCLCHECK(mpBarrier(comm, kSlotReduced, seq, stream));
+    NCCLCHECK(mpBarrier(comm, kSlotReduced, stream));
     nbxDevRedOpFull copyOp{nbxDevSum, 0, 0};
     for (int k = 1; k < n; k++) {
       const int j = (me + k) % n;
@@ -980,7 +988,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     }
   }
   // 4. nobody reuses its buffers while a peer may still read them
-  NCCLCHECK(mpBarrier(comm, kSlotDone, seq, stream));
+  NCCLCHECK(mpBarrier(comm, kSlotDone, stream));
   return ncclSuccess;
 }
 

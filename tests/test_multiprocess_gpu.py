@@ -349,3 +349,110 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
                 assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (it, kind, dtype, op, count, r)
     print(f"LL 4 KiB fp32 allreduce (NCCL_PROTO={proto or 'default'}), {n} ranks sharing one GPU: us/call =",
           [round(res[r][1], 1) for r in range(n)])
+
+
+GRAPH_CASES = [(1000, "LL"), (100003, "LL128"), (600000, "Simple")]   # fp32 counts -> protocol by default
+
+
+def _child_graph(uid_bytes, uid_ring_bytes, rank, n, q):
+    """Capture one graph holding AllReduce calls of every protocol (direct
+    comm) plus a ring-schedule AllReduce (ring comm), replay it with inputs
+    changed between replays, check every output each time."""
+    try:
+        import os
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        os.environ["NCCL_ALGO"] = "Ring"
+        os.environ["NCCL_PROTO"] = "Simple"
+        ring = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_ring_bytes), rank)
+        s = torch.cuda.Stream()
+        bufs = []
+        for cnt, _ in GRAPH_CASES + [(300001, "ring")]:
+            x = torch.empty(cnt, device="cuda")
+            y = torch.empty(cnt, device="cuda")
+            bufs.append((cnt, x, y))
+
+        def issue(st):
+            for i, (cnt, x, y) in enumerate(bufs):
+                c = ring if i == len(bufs) - 1 else comm
+                c.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, st)
+
+        def fill(it):
+            for cnt, x, y in bufs:
+                idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+                x.copy_(torch.remainder(idx * 3 + 11 * rank + 17 * it, 257))
+                y.fill_(-1)
+
+        with torch.cuda.stream(s):
+            fill(0)
+            issue(s.cuda_stream)   # eager warm-up: maps every peer buffer before capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+            issue(s.cuda_stream)
+        torch.cuda.synchronize()
+        bad = []
+        for it in range(1, 6):
+            with torch.cuda.stream(s):
+                fill(it)
+                g.replay()
+            s.synchronize()
+            for k, (cnt, x, y) in enumerate(bufs):
+                idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+                want = sum(torch.remainder(idx * 3 + 11 * r + 17 * it, 257) for r in range(n))
+                if not torch.equal(y, want):
+                    bad.append((it, k, int((y != want).sum())))
+        # eager calls after the replays still line up with the peers
+        with torch.cuda.stream(s):
+            fill(9)
+            issue(s.cuda_stream)
+        s.synchronize()
+        for k, (cnt, x, y) in enumerate(bufs):
+            idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+            want = sum(torch.remainder(idx * 3 + 11 * r + 17 * 9, 257) for r in range(n))
+            if not torch.equal(y, want):
+                bad.append(("eager", k, int((y != want).sum())))
+        assert comm.async_error() == 0 and ring.async_error() == 0
+        del g
+        ring.destroy()
+        comm.destroy()
+        q.put((rank, "ok", bad))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multiprocess_graph_capture(nbx, n, monkeypatch):
+    """ncclAllReduce captured into a HIP graph on the multi-process communicator
+    (LL, LL128, Simple direct and ring schedules in one graph) replays
+    correctly: sequence numbers, credits and barrier epochs are device-resident,
+    so every replay advances them like an eager call."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
+    monkeypatch.delenv("NCCL_PROTO", raising=False)
+    monkeypatch.delenv("NCCL_ALGO", raising=False)
+    uid, uid_ring = nbx.get_unique_id(), nbx.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_child_graph, args=(bytes(uid), bytes(uid_ring), r, n, q), daemon=True)
+             for r in range(n)]
+    for p in procs:
+        p.start()
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", f"rank {rank}:\n{payload}"
+            assert payload == [], f"rank {rank}: wrong outputs {payload}"
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
