@@ -245,7 +245,7 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
         vals = [r.get(key) for r in allres]
         out[key] = None if any(v is None for v in vals) else round(max(vals), 2)
     sw = {"bytes": allres[0].get("sweep_bytes"), "what": "fp32 sum AllReduce us/call, max over ranks, per protocol"}
-    for name in ("LL", "LL128", "Simple"):
+    for name in ("LL", "LL128", "LL128_oneshot", "Simple"):
         rows = [r.get("sweep_" + name + "_us") for r in allres]
         sw[name] = None if any(v is None for v in rows) else [max(col) for col in zip(*rows)]
     out["protocol_sweep"] = sw

@@ -22,9 +22,12 @@ ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, 
  * case-insensitive; NULL or "" = all): bit 0 LL, bit 1 LL128, bit 2 Simple. */
 int nbxDebugProtoMask(const char* ncclProto);
 
-/* The multi-process communicator's per-message protocol choice: 0 LL, 1 LL128,
- * 2 Simple, for a message (per-rank block for ReduceScatter) of slotBytes. */
-int nbxDebugChooseProto(int protoMask, uint64_t slotBytes, int nRanks, uint64_t llMaxBytes, uint64_t ll128MaxBytes);
+/* The multi-process communicator's per-message protocol choice: 0 LL, 1 LL128
+ * (one-shot), 2 Simple, 3 LL128 two-shot AllReduce, for a message of slotBytes
+ * (per-rank block for ReduceScatter) whose direct-schedule AllReduce block is
+ * blockBytes. */
+int nbxDebugChooseProto(int protoMask, int allReduce, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
+                        uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax);
 
 #ifdef __cplusplus
 }

@@ -11,4 +11,7 @@ struct LLArgs;
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
 // The same for the LL128 kernel (args.nLines 64-byte lines).
 ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
+// LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
+ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
+                                   hipStream_t stream);
 }  // namespace nbx

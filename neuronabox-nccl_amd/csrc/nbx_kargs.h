@@ -32,6 +32,7 @@ struct KernelSet {
   const void* elts;
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
+  const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;
   int valid;

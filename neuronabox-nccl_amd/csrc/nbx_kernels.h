@@ -190,6 +190,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.elts = (const void*)&kReduceElts<Fn>;
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
+  ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.valid = 1;
   return ks;

@@ -388,4 +388,173 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   if (threadIdx.x == 0) llEnd(a, call);
 }
 
+
+// ---------------------------------------------------------------------------
+// LL128 two-shot AllReduce (medium messages, n <= 8 ranks): the one-shot
+// kernel above sends the whole message to every peer ((n-1) x M per rank); this
+// one moves 2 (n-1)/n x M, as a ring would, in one kernel and two hops:
+//   A. push block j of `send` (the direct schedule's 16-byte-aligned blocks)
+//      into peer j's reduce-scatter sub-slot [parity][RS][me];
+//   B. for this rank's block: poll the n-1 RS sub-slots, fold with the own
+//      contribution in the direct order me+1, ..., me (bitwise the direct
+//      path's result), store it to `recv` and push the folded lines into every
+//      peer's all-gather sub-slot [parity][AG][me];
+//   C. for every other block j: poll AG sub-slot [parity][AG][j], copy the
+//      payload into `recv`.
+// The LL128 buffer's per-parity region (n slots of l128SlotLines lines) is
+// split into 2n sub-slots of subSlotLines lines ([RS][source], [AG][source]).
+// Credits, sequencing and done words are the LL family's (llBegin / llEnd).
+__device__ __forceinline__ void l128BlockRange(const LLArgs& a, int j, int eb, uint64_t* offBytes,
+                                               uint64_t* lenBytes) {
+  uint64_t lo = a.blockElts * (uint64_t)j, hi = lo + a.blockElts;
+  if (lo > a.count) lo = a.count;
+  if (hi > a.count) hi = a.count;
+  *offBytes = lo * (uint64_t)eb;
+  *lenBytes = (hi - lo) * (uint64_t)eb;
+}
+
+template <class Fn>
+__global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
+  using E = typename Fn::Elt;
+  constexpr int EPK = 8 / (int)sizeof(E);
+  constexpr int eb = (int)sizeof(E);
+  const Fn fn(llLoadArg<Fn>(a));
+  const int n = a.nRanks, me = a.rank;
+  const int t = (int)(threadIdx.x % kL128Lanes);
+  const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) / kL128Lanes;
+  const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kL128Lanes;
+  const uint64_t t0 = wall_clock64();
+  const LLCall call = llBegin(a);
+  const uint64_t S = a.nLines;   // sub-slot lines (nLines carries subSlotLines here)
+  auto subSlot = [&](int region, int src) { return (uint64_t)((call.parity * 2 + region) * n + src) * S; };
+  __shared__ int sFailed;
+  if (threadIdx.x == 0) sFailed = 0;
+  __syncthreads();
+  if (call.needDone != 0 && (int)threadIdx.x < n && (int)threadIdx.x != me) {
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0)) sFailed = 1;
+  }
+  __syncthreads();
+  bool failed = sFailed != 0;
+  const unsigned char* send = (const unsigned char*)a.send;
+  unsigned char* recv = (unsigned char*)a.recv;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.myL128, (short)0, (int)a.l128Bytes,
+                                                                      0x00020000);
+  // A. reduce-scatter pushes
+  for (int j = 0; j < n && !failed; j++) {
+    if (j == me) continue;
+    uint64_t off, len;
+    l128BlockRange(a, j, eb, &off, &len);
+    const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
+    for (uint64_t i = g0; i < lines; i += groups) {
+      const u32x4 v = l128Payload(send + off, len, i, t, call.seq);
+      l128StoreLine16(a.peerL128[j] + (subSlot(0, me) + i) * (kL128LineBytes / 8) + 2 * t, v);
+    }
+  }
+  // B. own block: fold, store, all-gather pushes
+  {
+    uint64_t off, len;
+    l128BlockRange(a, me, eb, &off, &len);
+    const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
+    const int first = (me + 1) % n;
+    for (uint64_t i = g0; i < lines; i += groups) {
+      u32x4 v[kL128MaxRanks];
+      uint32_t need = 0;
+#pragma unroll
+      for (int q = 0; q < kL128MaxRanks; q++) {
+        v[q] = (u32x4){0, 0, 0, 0};
+        if (q < n) {
+          if (q == me) v[q] = l128Payload(send + off, len, i, t, 0);
+          else need |= 1u << q;
+        }
+      }
+      uint32_t spins = 0;
+      while (need != 0 && !failed) {
+#pragma unroll
+        for (int q = 0; q < kL128MaxRanks; q++)
+          if ((need >> q) & 1u)
+            v[q] = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           rs, (uint32_t)((subSlot(0, q) + i) * kL128LineBytes) + (uint32_t)t * 16u, 0, kL128LoadAux));
+#pragma unroll
+        for (int q = 0; q < kL128MaxRanks; q++) {
+          if ((need >> q) & 1u) {
+            const uint64_t fw = ((uint64_t)v[q].w << 32) | v[q].z;
+            if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
+          }
+        }
+        if (need != 0 && (++spins & 1023u) == 0u) {
+          if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
+            *a.errWord = *a.abortWord != 0 ? 2 : 1;
+            failed = true;
+          }
+        }
+      }
+      union Pk {
+        uint64_t u;
+        E e[EPK];
+      };
+      uint64_t w[2] = {0, call.seq};
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k == 1 && t == kL128Lanes - 1) break;   // the flag word
+        Pk acc;
+        acc.u = 0;
+        for (int q = 0; q < n; q++) {
+          const int j = first + q < n ? first + q : first + q - n;
+          Pk x;
+          x.u = l128Pick(v, j, k);
+#pragma unroll
+          for (int e = 0; e < EPK; e++) {
+            E y = x.e[e];
+            if constexpr (Fn::kHasPre) y = fn.pre(y);
+            acc.e[e] = q == 0 ? y : fn.red(acc.e[e], y);
+          }
+        }
+        if constexpr (Fn::kHasPost) {
+          if (a.postOp) {
+#pragma unroll
+            for (int e = 0; e < EPK; e++) acc.e[e] = fn.post(acc.e[e]);
+          }
+        }
+        w[k] = acc.u;
+        llStoreBytes(recv + off, i * kL128DataBytes + (uint64_t)t * 16 + 8 * k, len, acc.u);
+      }
+      const u32x4 line = {(uint32_t)w[0], (uint32_t)(w[0] >> 32), (uint32_t)w[1], (uint32_t)(w[1] >> 32)};
+      for (int j = 0; j < n; j++) {
+        if (j == me || failed) continue;
+        l128StoreLine16(a.peerL128[j] + (subSlot(1, me) + i) * (kL128LineBytes / 8) + 2 * t, line);
+      }
+    }
+  }
+  // C. the other blocks arrive folded: copy them into recv
+  for (int j = 0; j < n; j++) {
+    if (j == me) continue;
+    uint64_t off, len;
+    l128BlockRange(a, j, eb, &off, &len);
+    const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
+    for (uint64_t i = g0; i < lines; i += groups) {
+      u32x4 v = {0, 0, 0, 0};
+      uint32_t spins = 0;
+      while (!failed) {
+        v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          rs, (uint32_t)((subSlot(1, j) + i) * kL128LineBytes) + (uint32_t)t * 16u, 0,
+                                          kL128LoadAux));
+        const uint64_t fw = ((uint64_t)v.w << 32) | v.z;
+        if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) break;
+        if ((++spins & 1023u) == 0u) {
+          if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
+            *a.errWord = *a.abortWord != 0 ? 2 : 1;
+            failed = true;
+          }
+        }
+      }
+      const uint64_t o = i * kL128DataBytes + (uint64_t)t * 16;
+      llStoreBytes(recv + off, o, len, ((uint64_t)v.y << 32) | v.x);
+      if (t != kL128Lanes - 1) llStoreBytes(recv + off, o + 8, len, ((uint64_t)v.w << 32) | v.z);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) llEnd(a, call);
+}
+
 }  // namespace nbx

@@ -215,6 +215,28 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   if (e != hipSuccess) return ncclUnhandledCudaError;
   return ncclSuccess;
 }
+
+ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, uint64_t blockLines,
+                                   hipStream_t stream) {
+  if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
+  const KernelSet& ks = table()[(int)dt][op.op];
+  if (!ks.valid || ks.ll128x2 == nullptr) return ncclInvalidArgument;
+  a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+  a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+  static const size_t maxGrid = [] {   // as launchLL128Coll
+    const char* v = std::getenv("NBX_LL128_MAX_GRID");
+    long g = (v && *v) ? std::atol(v) : 256;
+    return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
+  }();
+  const size_t linesPerBlock = 256 / kL128LanesHost;
+  size_t grid = (blockLines + linesPerBlock - 1) / linesPerBlock;
+  if (grid < 1) grid = 1;
+  if (grid > maxGrid) grid = maxGrid;
+  void* args[] = {&a};
+  hipError_t e = hipLaunchKernel(ks.ll128x2, dim3((unsigned)grid), dim3(256), args, 0, stream);
+  if (e != hipSuccess) return ncclUnhandledCudaError;
+  return ncclSuccess;
+}
 }  // namespace nbx
 
 extern "C" {

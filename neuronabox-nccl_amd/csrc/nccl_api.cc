@@ -531,6 +531,7 @@ struct MpState {
   uint64_t** peerL128Dev = nullptr;
   std::vector<void*> peerL128Maps;
   uint64_t l128MaxBytes = 0;        // 0: LL128 unavailable (n > 8)
+  uint64_t l128OneShotMax = 0;      // AllReduce, n > 2: one-shot up to this, two-shot above
   uint64_t l128SlotLines = 0;
   uint64_t l128Bytes = 0;
   int protoMask = 0;                // NCCL_PROTO at init: kProtoLL | kProtoLL128 | kProtoSimple
@@ -545,6 +546,7 @@ struct MpInitInfo {
   hipIpcMemHandle_t l128Handle;
   uint64_t llMaxBytes;
   uint64_t l128MaxBytes;
+  uint64_t l128OneShotMax;
   int32_t protoMask;
 };
 
@@ -576,15 +578,30 @@ int protoFromString(const char* v) {
 }
 int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
 
-enum MpProto { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2 };
-MpProto chooseProtoFor(int mask, uint64_t slotBytes, int n, uint64_t llMax, uint64_t l128Max) {
+// Per message: LL up to the LL max; LL128 one-shot (every rank pushes the
+// whole message to every target) up to the LL128 max — for AllReduce with more
+// than 2 ranks only up to the one-shot max; above that LL128 two-shot
+// AllReduce (reduce-scatter + all-gather hops, 2 (n-1)/n x M per rank) while
+// a rank's block fits half an LL128 slot; else Simple.
+enum MpProto { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2, kMpLL128x2 = 3 };
+// Lines per (parity, source) slot: holds maxBytes one-shot, and each half (a
+// two-shot sub-slot) holds maxBytes / 2.
+uint64_t l128SlotLinesFor(uint64_t maxBytes) {
+  const uint64_t half = (maxBytes + 1) / 2;
+  return 2 * ((half + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost);
+}
+MpProto chooseProtoFor(int mask, bool allReduce, uint64_t slotBytes, uint64_t blockBytes, int n, uint64_t llMax,
+                       uint64_t l128Max, uint64_t oneShotMax) {
   if (slotBytes == 0 || n > 64) return kMpSimple;
   if ((mask & kProtoLL) && slotBytes <= llMax) return kMpLL;
-  if ((mask & kProtoLL128) && l128Max != 0 && n <= nbx::kL128MaxRanksHost && slotBytes <= l128Max) return kMpLL128;
+  if ((mask & kProtoLL128) && l128Max != 0 && n <= nbx::kL128MaxRanksHost) {
+    if (!allReduce || n <= 2 || slotBytes <= oneShotMax) {
+      if (slotBytes <= l128Max) return kMpLL128;
+    } else if (blockBytes <= (l128SlotLinesFor(l128Max) / 2) * nbx::kL128DataBytesHost) {
+      return kMpLL128x2;
+    }
+  }
   return kMpSimple;
-}
-MpProto chooseProto(const MpState* mp, uint64_t slotBytes, int n) {
-  return chooseProtoFor(mp->protoMask, slotBytes, n, mp->llMaxBytes, mp->l128MaxBytes);
 }
 
 struct MpCallInfo {
@@ -696,12 +713,14 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   // LL128 buffer: 2 parities x n sources x 64-byte lines of 56 payload bytes (n <= 8)
   if (c->nRanks <= nbx::kL128MaxRanksHost) {
     const char* v = std::getenv("NBX_LL128_MAX_BYTES");
-    uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (1u << 20);
+    uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (4u << 20);
+    const char* o = std::getenv("NBX_LL128_ONESHOT_MAX");
+    mp->l128OneShotMax = (o && *o) ? std::strtoull(o, nullptr, 10) : (256u << 10);
     if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
     if (mx != 0) {
       mx = (mx + 15) & ~(uint64_t)15;
       mp->l128MaxBytes = mx;
-      mp->l128SlotLines = (mx + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+      mp->l128SlotLines = l128SlotLinesFor(mx);
       mp->l128Bytes = 2 * (uint64_t)c->nRanks * mp->l128SlotLines * nbx::kL128LineBytesHost;
       HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes));
       HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
@@ -712,6 +731,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.device = c->device;
   mine.llMaxBytes = mp->llMaxBytes;
   mine.l128MaxBytes = mp->l128MaxBytes;
+  mine.l128OneShotMax = mp->l128OneShotMax;
   mine.protoMask = mp->protoMask;
   HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
@@ -722,8 +742,9 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   for (int j = 0; j < c->nRanks; j++) {
     // every rank must pick the same protocol for the same call
     if (all[j].llMaxBytes != mp->llMaxBytes || all[j].l128MaxBytes != mp->l128MaxBytes ||
-        all[j].protoMask != mp->protoMask) {
-      warn("ncclCommInitRank : NCCL_PROTO / NBX_LL_MAX_BYTES / NBX_LL128_MAX_BYTES differ across ranks");
+        all[j].l128OneShotMax != mp->l128OneShotMax || all[j].protoMask != mp->protoMask) {
+      warn("ncclCommInitRank : NCCL_PROTO / NBX_LL_MAX_BYTES / NBX_LL128_MAX_BYTES / NBX_LL128_ONESHOT_MAX differ "
+           "across ranks");
       return ncclInvalidUsage;
     }
     if (j == c->rank) {
@@ -809,7 +830,10 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   // exchange (nbx_ll.h). The choice depends only on arguments every rank
   // passes identically (and on the init-time settings checked equal).
   const uint64_t slotBytes = (uint64_t)count * (uint64_t)eb;   // RS: recvcount per block
-  const MpProto proto = chooseProto(mp, slotBytes, n);
+  size_t off0, per;
+  blockRange(count, eb, n, 0, &off0, &per);   // the direct schedule's AllReduce block
+  const MpProto proto = chooseProtoFor(mp->protoMask, kind == kAllReduce, slotBytes, (uint64_t)per * (uint64_t)eb, n,
+                                       mp->llMaxBytes, mp->l128MaxBytes, mp->l128OneShotMax);
   if (proto != kMpSimple) {
     if (send == nullptr || (recv == nullptr && (kind != kReduce || me == root))) {
       warn("rank %d passed a NULL buffer", me);
@@ -826,8 +850,6 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     la.slotLines = mp->llSlotLines;
     la.doneOff = mp->llDoneOff;
     la.state = mp->llState;
-    size_t off0, per;
-    blockRange(count, eb, n, 0, &off0, &per);
     la.blockElts = per > 0 ? per : 1;
     la.abortWord = mp->hostWordsDev;
     la.errWord = mp->hostWordsDev + 1;
@@ -837,12 +859,18 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
     la.postOp = 1;
     la.mode = kind == kAllReduce ? nbx::kLLAllReduce : kind == kReduceScatter ? nbx::kLLReduceScatter : nbx::kLLReduce;
     la.root = root;
-    if (proto == kMpLL128) {
+    if (proto == kMpLL128 || proto == kMpLL128x2) {
       la.peerL128 = mp->peerL128Dev;
       la.myL128 = mp->l128;
       la.l128SlotLines = mp->l128SlotLines;
-      la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
       la.l128Bytes = (uint32_t)mp->l128Bytes;
+      if (proto == kMpLL128x2) {
+        la.nLines = mp->l128SlotLines / 2;   // sub-slot lines: [parity][RS|AG][source]
+        const uint64_t blockLines = ((uint64_t)per * (uint64_t)eb + nbx::kL128DataBytesHost - 1) /
+                                    nbx::kL128DataBytesHost;
+        return nbx::launchLL128AllReduce2(dt, op, la, blockLines, stream);
+      }
+      la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
       return nbx::launchLL128Coll(dt, op, la, stream);
     }
     return nbx::launchLLColl(dt, op, la, stream);
@@ -1338,9 +1366,10 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
 
 NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
 
-NBX_EXPORT int nbxDebugChooseProto(int protoMask, uint64_t slotBytes, int nRanks, uint64_t llMaxBytes,
-                                   uint64_t ll128MaxBytes) {
-  return (int)chooseProtoFor(protoMask, slotBytes, nRanks, llMaxBytes, ll128MaxBytes);
+NBX_EXPORT int nbxDebugChooseProto(int protoMask, int allReduce, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
+                                   uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax) {
+  return (int)chooseProtoFor(protoMask, allReduce != 0, slotBytes, blockBytes, nRanks, llMaxBytes, ll128MaxBytes,
+                             ll128OneShotMax);
 }
 
 NBX_EXPORT ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds) {

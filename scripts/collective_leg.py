@@ -10,9 +10,9 @@ the bench's own line down. It is spawned before the parent touches the GPU and
 talks over stdin/stdout:
 
   parent -> child   "ID\\n"               (rank 0 only)
-  child  -> parent  "ID <hex> x5\\n"      ncclUniqueIds: direct, ring, and the LL / LL128 /
-                                         Simple comms of the protocol sweep
-  parent -> child   "RUN <hex> x5\\n"     (every rank, after the parent's broadcast)
+  child  -> parent  "ID <hex> x6\\n"      ncclUniqueIds: direct, ring, and the LL / LL128 /
+                                         LL128-one-shot / Simple comms of the protocol sweep
+  parent -> child   "RUN <hex> x6\\n"     (every rank, after the parent's broadcast)
   child  -> parent  "RESULT <json>\\n"
 
 Inputs are small integers in fp32 (x_r[i] = (7 i + 13 r) mod 1024), so every
@@ -81,13 +81,17 @@ def _time_calls(fn, iters, warmup=2):
 SWEEP_BYTES = [4 << 10, 32 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]
 SWEEP_PROTOS = (("LL", {"NCCL_PROTO": "LL", "NBX_LL_MAX_BYTES": str(16 << 20)}),
                 ("LL128", {"NCCL_PROTO": "LL128", "NBX_LL128_MAX_BYTES": str(16 << 20)}),
+                ("LL128_oneshot", {"NCCL_PROTO": "LL128", "NBX_LL128_MAX_BYTES": str(16 << 20),
+                                   "NBX_LL128_ONESHOT_MAX": str(16 << 20)}),
                 ("Simple", {"NCCL_PROTO": "Simple"}))
 
 
 def protocol_sweep(ids, rank, world, st, shared_gpu, res):
     """AllReduce fp32 sum latency per protocol and message size (one
     communicator per protocol, forced by NCCL_PROTO at init, the LL / LL128
-    buffers enlarged to 16 MiB), each size checked exactly once."""
+    buffers enlarged to 16 MiB; "LL128" switches to the two-shot kernel above
+    256 KiB with > 2 ranks, "LL128_oneshot" never does), each size checked
+    exactly once."""
     import torch
     from __graft_entry__ import _load_package
     nbx = _load_package()
@@ -213,7 +217,7 @@ def run(ids, rank, world, dev):
     _progress("LL / LL128 done")
     config_e(comm, rank, world, st, res)
     _progress("config E done")
-    protocol_sweep(ids[2:5], rank, world, st, "NBX_BENCH_DEVICE" in os.environ, res)
+    protocol_sweep(ids[2:6], rank, world, st, "NBX_BENCH_DEVICE" in os.environ, res)
     _progress("protocol sweep done")
 
     torch.cuda.synchronize()
@@ -309,10 +313,10 @@ def main():
             continue
         if parts[0] == "ID":
             nbx = _pkg()   # imports torch first (one HIP runtime); no GPU use: the root is a host thread
-            _emit("ID " + " ".join(bytes(nbx.get_unique_id()).hex() for _ in range(5)))
+            _emit("ID " + " ".join(bytes(nbx.get_unique_id()).hex() for _ in range(6)))
         elif parts[0] == "RUN":
             try:
-                res = run(parts[1:6], rank, world, dev)
+                res = run(parts[1:7], rank, world, dev)
             except Exception as e:   # reported to the parent, never raised past it
                 res = {"rank": rank, "ok": False, "errors": [f"{type(e).__name__}: {e}"]}
             _emit("RESULT " + json.dumps(res))

@@ -205,11 +205,12 @@ def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch):
 
 
 # (kind, dtype, op, count, byte offset of send/recv). By default slots
-# <= 64 KiB take the LL protocol, <= 1 MiB LL128, larger ones the direct
-# (Simple) path; with NCCL_PROTO=LL128 every slot <= 1 MiB takes LL128. Reduce
-# to a changing root back to back exercises the done-word credits (a non-root
-# never waits for data, so only the credits stop it from overwriting a slot the
-# root has not read yet).
+# <= 64 KiB take the LL protocol; LL128 one-shot up to 4 MiB (AllReduce with
+# > 2 ranks: up to 256 KiB), LL128 two-shot AllReduce above that while a rank's
+# block fits 2 MiB; the rest the direct (Simple) path. With NCCL_PROTO=LL128
+# every message takes LL128. Reduce to a changing root back to back exercises
+# the done-word credits (a non-root never waits for data, so only the credits
+# stop it from overwriting a slot the root has not read yet).
 LL_CASES = [
     ("ar", 7, 0, 1, 0), ("ar", 7, 0, 3, 0), ("ar", 7, 0, 1000, 0), ("ar", 7, 0, 16384, 0), ("ar", 6, 0, 17, 0),
     ("ar", 9, 4, 4097, 0), ("ar", 2, 4, 999, 0), ("ar", 4, 2, 4096, 0), ("ar", 10, 0, 33, 0),
@@ -217,12 +218,14 @@ LL_CASES = [
     ("ar", 0, 0, 77, 3), ("rs", 7, 0, 1000, 0), ("rs", 6, 4, 333, 2), ("rs", 0, 2, 5, 1), ("rs", 4, 4, 4096, 0),
     ("rs", 7, 0, 20000, 0), ("red", 7, 0, 1000, 0), ("red", 9, 4, 777, 0), ("red", 2, 3, 64, 0),
     ("red", 7, 0, 123, 4), ("red", 7, 1, 4096, 0), ("ar", 7, 0, 64, 0),
-    # LL128 range (64 KiB, 1 MiB] by default: odd lengths so 120-byte lines straddle 16-byte blocks
-    ("ar", 7, 0, 100003, 0), ("ar", 7, 4, 262144, 0), ("ar", 6, 4, 77777, 2), ("ar", 9, 0, 300001, 0),
-    ("ar", 4, 2, 50000, 8), ("ar", 11, 0, 600001, 1), ("rs", 7, 0, 30001, 4), ("rs", 2, 2, 131072, 0),
-    ("red", 7, 0, 99999, 0), ("red", 8, 4, 100000, 8),
-    # direct (Simple) path interleaved: > 1 MiB per slot
-    ("ar", 7, 0, 300000, 0), ("rs", 7, 4, 262145, 0),
+    # LL128 one-shot range: odd lengths so 56-byte lines straddle 16-byte blocks
+    ("ar", 7, 0, 50003, 0), ("ar", 6, 4, 77777, 2), ("ar", 4, 2, 30000, 8), ("rs", 7, 0, 30001, 4),
+    ("rs", 2, 2, 131072, 0), ("red", 7, 0, 99999, 0), ("red", 8, 4, 100000, 8),
+    # LL128 two-shot AllReduce (> 256 KiB with > 2 ranks; one-shot with 2 ranks)
+    ("ar", 7, 4, 262144, 0), ("ar", 9, 0, 300001, 0), ("ar", 11, 0, 600001, 1), ("ar", 7, 0, 300000, 4),
+    ("ar", 2, 2, 1000003, 0), ("ar", 8, 0, 200001, 0),
+    # direct (Simple) path interleaved: > 4 MiB per slot
+    ("ar", 7, 0, 1100000, 0), ("rs", 7, 4, 1048577, 0),
 ]
 
 
@@ -296,7 +299,7 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
     AllReduce / ReduceScatter / Reduce messages, misaligned buffers included,
     issued back to back without host synchronisation and interleaved with each
     other and with direct-path messages; bitwise equal to the direct schedule's
-    fold order. NCCL_PROTO=LL128 routes every message <= 1 MiB through LL128."""
+    fold order. NCCL_PROTO=LL128 routes every message that fits through LL128."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     # all ranks share the test box's one GPU: keep every rank's LL128 grid
@@ -351,7 +354,9 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
           [round(res[r][1], 1) for r in range(n)])
 
 
-GRAPH_CASES = [(1000, "LL"), (100003, "LL128"), (600000, "Simple")]   # fp32 counts -> protocol by default
+# fp32 counts -> protocol by default (2-3 ranks): LL, LL128 one-shot, LL128
+# two-shot (3 ranks; one-shot at 2), Simple
+GRAPH_CASES = [(1000, "LL"), (50003, "LL128"), (300001, "LL128 two-shot"), (1500000, "Simple")]
 
 
 def _child_graph(uid_bytes, uid_ring_bytes, rank, n, q):

@@ -64,7 +64,8 @@ for line in sys.stdin:
               "allreduce_direct_ms": 10.0 + rank, "allreduce_ring_ms": 20.0 + rank,
               "reduce_scatter_ms": 5.0 + rank, "ll_allreduce_4KiB_us": 7.0 + rank,
               "sweep_bytes": [4096, 65536], "sweep_LL_us": [3.0 + rank, 9.0 - rank],
-              "sweep_LL128_us": [4.0, 5.0], "sweep_Simple_us": [50.0, 60.0 + rank]}), flush=True)
+              "sweep_LL128_us": [4.0, 5.0], "sweep_LL128_oneshot_us": [4.5, 5.5],
+              "sweep_Simple_us": [50.0, 60.0 + rank]}), flush=True)
         break
 '''
 
@@ -114,6 +115,7 @@ def test_collective_leg_protocol_gloo(tmp_path, mode):
         sw = out["protocol_sweep"]   # column-wise max over ranks
         assert sw["bytes"] == [4096, 65536]
         assert sw["LL"] == [4.0, 9.0] and sw["LL128"] == [4.0, 5.0] and sw["Simple"] == [50.0, 61.0]
+        assert sw["LL128_oneshot"] == [4.5, 5.5]
     else:
         assert out["ok"] is False
         assert any(e.startswith("rank 1:") for e in out["errors"])

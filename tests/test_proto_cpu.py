@@ -1,8 +1,9 @@
 """Protocol selection of the multi-process communicator, on the CPU through
 the library's debug hooks (include/nbx_debug.h): NCCL_PROTO parsing in NCCL's
 list syntax (tuning.cc:254-259: "LL,LL128", "^Simple", case-insensitive) and
-the per-message choice LL (<= LL max) -> LL128 (<= LL128 max, <= 8 ranks) ->
-Simple."""
+the per-message choice LL (<= LL max) -> LL128 one-shot (<= LL128 max, <= 8
+ranks; AllReduce with > 2 ranks only up to the one-shot max) -> LL128 two-shot
+AllReduce (a rank's block fits half an LL128 slot) -> Simple."""
 import ctypes
 
 import pytest
@@ -16,7 +17,8 @@ def lib(nbx):
     lib = nbx.load_library()
     lib.nbxDebugProtoMask.argtypes = [ctypes.c_char_p]
     lib.nbxDebugProtoMask.restype = ctypes.c_int
-    lib.nbxDebugChooseProto.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
+    lib.nbxDebugChooseProto.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
     lib.nbxDebugChooseProto.restype = ctypes.c_int
     return lib
 
@@ -31,19 +33,29 @@ def test_nccl_proto_parsing(lib, s, mask):
 
 
 K, M = 1 << 10, 1 << 20
+P_LL128X2 = 3
 
 
-@pytest.mark.parametrize("mask,nbytes,n,want", [
-    (ALL, 4, 2, P_LL), (ALL, 64 * K, 8, P_LL), (ALL, 64 * K + 1, 8, P_LL128), (ALL, M, 8, P_LL128),
-    (ALL, M + 1, 8, P_SIMPLE), (ALL, 256 * K, 9, P_SIMPLE),          # LL128 only up to 8 ranks
-    (ALL, 4 * K, 9, P_LL), (ALL, 0, 4, P_SIMPLE), (ALL, 4 * K, 65, P_SIMPLE),
-    (LL | SIMPLE, 256 * K, 4, P_SIMPLE), (LL128 | SIMPLE, 4, 4, P_LL128), (SIMPLE, 4, 4, P_SIMPLE),
-    (LL, 256 * K, 4, P_SIMPLE),                                        # nothing enabled fits: Simple
-    (LL128, 2 * M, 4, P_SIMPLE),
+def _block(nbytes, n, eb=4):
+    epp = 16 // eb
+    per = -(-(nbytes // eb) // n)
+    return (-(-per // epp) * epp) * eb
+
+
+@pytest.mark.parametrize("mask,ar,nbytes,n,want", [
+    (ALL, 1, 4, 2, P_LL), (ALL, 1, 64 * K, 8, P_LL), (ALL, 1, 64 * K + 4, 8, P_LL128), (ALL, 1, 256 * K, 8, P_LL128),
+    (ALL, 1, 256 * K + 4, 8, P_LL128X2), (ALL, 1, 16 * M, 8, P_LL128X2), (ALL, 1, 16 * M + 1024, 8, P_SIMPLE),
+    (ALL, 1, 4 * M, 2, P_LL128), (ALL, 1, 4 * M + 4, 2, P_SIMPLE),      # 2 ranks: one-shot only
+    (ALL, 1, 6 * M, 3, P_LL128X2), (ALL, 1, 8 * M, 3, P_SIMPLE),
+    (ALL, 0, 4 * M, 8, P_LL128), (ALL, 0, 4 * M + 4, 8, P_SIMPLE),      # RS / Reduce: one-shot up to the max
+    (ALL, 1, 256 * K, 9, P_SIMPLE), (ALL, 1, 4 * K, 9, P_LL),           # LL128 only up to 8 ranks
+    (ALL, 1, 0, 4, P_SIMPLE), (ALL, 1, 4 * K, 65, P_SIMPLE),
+    (LL | SIMPLE, 1, 256 * K, 4, P_SIMPLE), (LL128 | SIMPLE, 1, 4, 4, P_LL128), (SIMPLE, 1, 4, 4, P_SIMPLE),
+    (LL, 1, 256 * K, 4, P_SIMPLE),                                       # nothing enabled fits: Simple
 ])
-def test_protocol_choice(lib, mask, nbytes, n, want):
-    assert lib.nbxDebugChooseProto(mask, nbytes, n, 64 * K, M) == want
+def test_protocol_choice(lib, mask, ar, nbytes, n, want):
+    assert lib.nbxDebugChooseProto(mask, ar, nbytes, _block(nbytes, n), n, 64 * K, 4 * M, 256 * K) == want
 
 
 def test_ll128_disabled_by_zero_max(lib):
-    assert lib.nbxDebugChooseProto(ALL, 256 * K, 4, 64 * K, 0) == P_SIMPLE
+    assert lib.nbxDebugChooseProto(ALL, 1, 256 * K, 64 * K, 4, 64 * K, 0, 256 * K) == P_SIMPLE
