@@ -35,6 +35,8 @@ COUNT = 256 << 20          # fp32 elements per rank: 1 GiB (config D)
 LL_COUNT = 1024            # 4 KiB LL AllReduce latency probe
 LL128_COUNT = 256 << 10    # 1 MiB LL128 AllReduce (the protocol's largest default message)
 LL128_ITERS = 200
+SIMPLE_STRESS_COUNT = 8 << 20   # 32 MiB fp32: above every LL/LL128 threshold
+SIMPLE_STRESS_ITERS = 30
 E_I64 = 16 << 20           # config E: int64 elements (128 MiB)
 E_F8 = 128 << 20           # config E: fp8 elements (128 MiB)
 WARMUP, ITERS = 2, 5
@@ -182,6 +184,23 @@ def run(ids, rank, world, dev):
     res["reduce_scatter_ms"] = _time_calls(lambda: comm.reduce_scatter(x.data_ptr(), yr.data_ptr(), rc, F32, SUM, st),
                                            ITERS)
 
+    # Simple path with inputs that change every call (direct and ring schedules,
+    # 32 MiB): catches any stale peer data a cache could serve across calls
+    xs_ = x[:SIMPLE_STRESS_COUNT]
+    es_ = exp[:SIMPLE_STRESS_COUNT]
+    ys_ = torch.empty(SIMPLE_STRESS_COUNT, dtype=torch.float32, device="cuda")
+    for name, c in (("direct", comm), ("ring", comm_ring)):
+        bad = 0
+        for it in range(SIMPLE_STRESS_ITERS):
+            xi = xs_ + float(it % 89)
+            c.all_reduce(xi.data_ptr(), ys_.data_ptr(), SIMPLE_STRESS_COUNT, F32, SUM, st)
+            if not torch.equal(ys_, es_ + float(world * (it % 89))):
+                bad += 1
+        if bad:
+            res["ok"] = False
+            res["errors"].append(f"simple_{name}_stress: {bad} of {SIMPLE_STRESS_ITERS} calls wrong")
+    res["simple_stress_checked_calls"] = 2 * SIMPLE_STRESS_ITERS
+    del xs_, es_, ys_
     _progress("config D done")
     # LL128 (1 MiB): exact on every one of LL128_ITERS calls with inputs that
     # change per call (a torn line or a stale slot would show up as a
