@@ -23,10 +23,10 @@ ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, 
 int nbxDebugProtoMask(const char* ncclProto);
 
 /* The multi-process communicator's per-message protocol choice: 0 LL, 1 LL128
- * (one-shot), 2 Simple, 3 LL128 two-shot AllReduce, for a message of slotBytes
- * (per-rank block for ReduceScatter) whose direct-schedule AllReduce block is
- * blockBytes. */
-int nbxDebugChooseProto(int protoMask, int allReduce, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
+ * (one-shot), 2 Simple, 3 LL128 two-shot, for a message of slotBytes (per-rank
+ * block for ReduceScatter) whose direct-schedule block is blockBytes;
+ * twoShotKind = 1 for AllReduce / Reduce, 0 for ReduceScatter. */
+int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
                         uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax);
 
 #ifdef __cplusplus

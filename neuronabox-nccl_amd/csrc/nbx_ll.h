@@ -390,17 +390,21 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// LL128 two-shot AllReduce (medium messages, n <= 8 ranks): the one-shot
-// kernel above sends the whole message to every peer ((n-1) x M per rank); this
-// one moves 2 (n-1)/n x M, as a ring would, in one kernel and two hops:
+// LL128 two-shot AllReduce / Reduce (medium messages, n <= 8 ranks): the
+// one-shot kernel above sends the whole message to every target ((n-1) x M per
+// rank for AllReduce, (n-1) x M into the root for Reduce); this one moves
+// 2 (n-1)/n x M per rank (AllReduce; Reduce: (n-1)/n x M into the root), in one
+// kernel and two hops:
 //   A. push block j of `send` (the direct schedule's 16-byte-aligned blocks)
 //      into peer j's reduce-scatter sub-slot [parity][RS][me];
 //   B. for this rank's block: poll the n-1 RS sub-slots, fold with the own
-//      contribution in the direct order me+1, ..., me (bitwise the direct
-//      path's result), store it to `recv` and push the folded lines into every
-//      peer's all-gather sub-slot [parity][AG][me];
-//   C. for every other block j: poll AG sub-slot [parity][AG][j], copy the
-//      payload into `recv`.
+//      contribution in the direct order (AllReduce me+1, ..., me; Reduce
+//      root+1, ..., root — bitwise the direct path's result), then AllReduce:
+//      store it to `recv` and push the folded lines into every peer's
+//      all-gather sub-slot [parity][AG][me]; Reduce: the root stores it, the
+//      others push it into the root's sub-slot only;
+//   C. (AllReduce: every rank; Reduce: the root) for every other block j:
+//      poll AG sub-slot [parity][AG][j], copy the payload into `recv`.
 // The LL128 buffer's per-parity region (n slots of l128SlotLines lines) is
 // split into 2n sub-slots of subSlotLines lines ([RS][source], [AG][source]).
 // Credits, sequencing and done words are the LL family's (llBegin / llEnd).
@@ -455,7 +459,8 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
     uint64_t off, len;
     l128BlockRange(a, me, eb, &off, &len);
     const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
-    const int first = (me + 1) % n;
+    const bool reduce = a.mode == kLLReduce;
+    const int first = ((reduce ? a.root : me) + 1) % n;
     for (uint64_t i = g0; i < lines; i += groups) {
       u32x4 v[kL128MaxRanks];
       uint32_t need = 0;
@@ -517,17 +522,17 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
           }
         }
         w[k] = acc.u;
-        llStoreBytes(recv + off, i * kL128DataBytes + (uint64_t)t * 16 + 8 * k, len, acc.u);
+        if (!reduce || me == a.root) llStoreBytes(recv + off, i * kL128DataBytes + (uint64_t)t * 16 + 8 * k, len, acc.u);
       }
       const u32x4 line = {(uint32_t)w[0], (uint32_t)(w[0] >> 32), (uint32_t)w[1], (uint32_t)(w[1] >> 32)};
       for (int j = 0; j < n; j++) {
-        if (j == me || failed) continue;
+        if (j == me || failed || (reduce && j != a.root)) continue;
         l128StoreLine16(a.peerL128[j] + (subSlot(1, me) + i) * (kL128LineBytes / 8) + 2 * t, line);
       }
     }
   }
   // C. the other blocks arrive folded: copy them into recv
-  for (int j = 0; j < n; j++) {
+  for (int j = 0; j < n && (a.mode != kLLReduce || me == a.root); j++) {
     if (j == me) continue;
     uint64_t off, len;
     l128BlockRange(a, j, eb, &off, &len);

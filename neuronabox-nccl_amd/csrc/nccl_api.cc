@@ -579,10 +579,11 @@ int protoFromString(const char* v) {
 int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
 
 // Per message: LL up to the LL max; LL128 one-shot (every rank pushes the
-// whole message to every target) up to the LL128 max — for AllReduce with more
-// than 2 ranks only up to the one-shot max; above that LL128 two-shot
-// AllReduce (reduce-scatter + all-gather hops, 2 (n-1)/n x M per rank) while
-// a rank's block fits half an LL128 slot; else Simple.
+// whole message to every target) up to the LL128 max — for AllReduce / Reduce
+// with more than 2 ranks only up to the one-shot max; above that the LL128
+// two-shot AllReduce / Reduce (reduce-scatter + gather hops) while a rank's
+// block fits half an LL128 slot; else Simple. ReduceScatter is one hop by
+// nature: one-shot up to the LL128 max.
 enum MpProto { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2, kMpLL128x2 = 3 };
 // Lines per (parity, source) slot: holds maxBytes one-shot, and each half (a
 // two-shot sub-slot) holds maxBytes / 2.
@@ -590,12 +591,12 @@ uint64_t l128SlotLinesFor(uint64_t maxBytes) {
   const uint64_t half = (maxBytes + 1) / 2;
   return 2 * ((half + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost);
 }
-MpProto chooseProtoFor(int mask, bool allReduce, uint64_t slotBytes, uint64_t blockBytes, int n, uint64_t llMax,
+MpProto chooseProtoFor(int mask, bool twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int n, uint64_t llMax,
                        uint64_t l128Max, uint64_t oneShotMax) {
   if (slotBytes == 0 || n > 64) return kMpSimple;
   if ((mask & kProtoLL) && slotBytes <= llMax) return kMpLL;
   if ((mask & kProtoLL128) && l128Max != 0 && n <= nbx::kL128MaxRanksHost) {
-    if (!allReduce || n <= 2 || slotBytes <= oneShotMax) {
+    if (!twoShotKind || n <= 2 || slotBytes <= oneShotMax) {
       if (slotBytes <= l128Max) return kMpLL128;
     } else if (blockBytes <= (l128SlotLinesFor(l128Max) / 2) * nbx::kL128DataBytesHost) {
       return kMpLL128x2;
@@ -832,7 +833,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   const uint64_t slotBytes = (uint64_t)count * (uint64_t)eb;   // RS: recvcount per block
   size_t off0, per;
   blockRange(count, eb, n, 0, &off0, &per);   // the direct schedule's AllReduce block
-  const MpProto proto = chooseProtoFor(mp->protoMask, kind == kAllReduce, slotBytes, (uint64_t)per * (uint64_t)eb, n,
+  const MpProto proto = chooseProtoFor(mp->protoMask, kind != kReduceScatter, slotBytes, (uint64_t)per * (uint64_t)eb, n,
                                        mp->llMaxBytes, mp->l128MaxBytes, mp->l128OneShotMax);
   if (proto != kMpSimple) {
     if (send == nullptr || (recv == nullptr && (kind != kReduce || me == root))) {
@@ -1366,9 +1367,9 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
 
 NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
 
-NBX_EXPORT int nbxDebugChooseProto(int protoMask, int allReduce, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
+NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
                                    uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax) {
-  return (int)chooseProtoFor(protoMask, allReduce != 0, slotBytes, blockBytes, nRanks, llMaxBytes, ll128MaxBytes,
+  return (int)chooseProtoFor(protoMask, twoShotKind != 0, slotBytes, blockBytes, nRanks, llMaxBytes, ll128MaxBytes,
                              ll128OneShotMax);
 }
 

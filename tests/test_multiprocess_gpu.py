@@ -221,9 +221,10 @@ LL_CASES = [
     # LL128 one-shot range: odd lengths so 56-byte lines straddle 16-byte blocks
     ("ar", 7, 0, 50003, 0), ("ar", 6, 4, 77777, 2), ("ar", 4, 2, 30000, 8), ("rs", 7, 0, 30001, 4),
     ("rs", 2, 2, 131072, 0), ("red", 7, 0, 99999, 0), ("red", 8, 4, 100000, 8),
-    # LL128 two-shot AllReduce (> 256 KiB with > 2 ranks; one-shot with 2 ranks)
+    # LL128 two-shot AllReduce / Reduce (> 256 KiB with > 2 ranks; one-shot with 2 ranks)
     ("ar", 7, 4, 262144, 0), ("ar", 9, 0, 300001, 0), ("ar", 11, 0, 600001, 1), ("ar", 7, 0, 300000, 4),
-    ("ar", 2, 2, 1000003, 0), ("ar", 8, 0, 200001, 0),
+    ("ar", 2, 2, 1000003, 0), ("ar", 8, 0, 200001, 0), ("red", 7, 0, 300001, 0), ("red", 9, 4, 200003, 2),
+    ("red", 2, 3, 500000, 0),
     # direct (Simple) path interleaved: > 4 MiB per slot
     ("ar", 7, 0, 1100000, 0), ("rs", 7, 4, 1048577, 0),
 ]
