@@ -41,6 +41,7 @@
 #include "../../include/nbx_debug.h"
 #include "../../include/nbx_reduce.h"
 #include "nbx_bootstrap.h"
+#include "nbx_shmx.h"
 #include "nbx_sync.h"
 #include "nbx_internal.h"
 #include "nbx_ll_args.h"
@@ -501,6 +502,7 @@ enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kSlotRing = 3, kNumSlots
 
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
+  nbx::ShmExchange* shmx = nullptr;     // per-call exchange through /dev/shm (nullptr: TCP bootstrap)
   uint64_t* flags = nullptr;           // own phase flags (device memory, IPC-exported)
   uint64_t** peerFlagsDev = nullptr;   // device table: rank -> flags (self = flags)
   std::vector<void*> peerFlagMaps;     // IPC mappings to close
@@ -613,6 +615,54 @@ struct MpCallInfo {
   hipIpcMemHandle_t sendH, recvH;
   uint64_t sendOff, recvOff;
 };
+
+// The Simple path's per-call allgather: shared memory when every rank could
+// attach the segment at init, the TCP bootstrap otherwise.
+ncclResult_t mpExchange(MpState* mp, uint64_t seq, const void* mine, size_t len, void* all) {
+  if (mp->shmx) return nbx::shmxAllGather(mp->shmx, seq, mine, len, all, mp->timeoutSec, mp->hostWords);
+  return nbx::bootstrapAllGather(mp->bs, mine, len, all);
+}
+
+// Name of the communicator's exchange segment, derived from its unique id.
+std::string shmxName(const ncclUniqueId& id) {
+  uint64_t h = 1469598103934665603ull;   // FNV-1a over the id bytes
+  for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; i++) h = (h ^ (uint8_t)id.internal[i]) * 1099511628211ull;
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), "/nbx-shmx-%016llx", (unsigned long long)h);
+  return buf;
+}
+
+// Collective: rank 0 creates the segment, the others attach; used only if
+// every rank succeeded (NBX_HOST_EXCHANGE=tcp on any rank keeps TCP).
+ncclResult_t mpSetupShmx(ncclComm* c, const ncclUniqueId& id) {
+  MpState* mp = c->mp;
+  const char* env = std::getenv("NBX_HOST_EXCHANGE");
+  const bool want = !(env && strcasecmp(env, "tcp") == 0);
+  const std::string name = shmxName(id);
+  std::vector<int32_t> ok(c->nRanks);
+  int32_t mine = 0;
+  if (c->rank == 0 && want) {
+    nbx::shmxUnlink(name.c_str());   // a stale segment of a crashed run with the same id (practically never)
+    mp->shmx = nbx::shmxOpen(name.c_str(), 0, c->nRanks, sizeof(MpCallInfo), true);
+    mine = mp->shmx != nullptr;
+  }
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), ok.data()));   // created?
+  const bool created = ok[0] != 0;
+  if (c->rank != 0) {
+    if (created && want) mp->shmx = nbx::shmxOpen(name.c_str(), c->rank, c->nRanks, sizeof(MpCallInfo), false);
+    mine = mp->shmx != nullptr;
+  }
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), ok.data()));   // everyone attached?
+  if (c->rank == 0 && created) nbx::shmxUnlink(name.c_str());
+  bool all = true;
+  for (int32_t v : ok) all &= v != 0;
+  if (!all && mp->shmx) {
+    nbx::shmxClose(mp->shmx);
+    mp->shmx = nullptr;
+  }
+  info("comm %p rank %d: per-call exchange over %s", (void*)c, c->rank, mp->shmx ? "shared memory" : "TCP");
+  return ncclSuccess;
+}
 
 ncclResult_t ipcHandleOf(const void* p, hipIpcMemHandle_t* h, uint64_t* off) {
   hipDeviceptr_t base = nullptr;
@@ -794,6 +844,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   int dummy = 0;
   std::vector<int> sink(c->nRanks);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), sink.data()));
+  NCCLCHECK(mpSetupShmx(c, id));
   info("comm %p rank %d nranks %d device %d: multi-process communicator ready", (void*)c, c->rank, c->nRanks,
        c->device);
   return ncclSuccess;
@@ -817,6 +868,7 @@ void mpFree(ncclComm* c) {
   if (mp->llState) (void)hipFree(mp->llState);
   if (mp->flags) (void)hipFree(mp->flags);
   if (mp->hostWords) (void)hipHostFree(mp->hostWords);
+  nbx::shmxClose(mp->shmx);
   nbx::bootstrapClose(mp->bs);
   delete mp;
   c->mp = nullptr;
@@ -889,7 +941,7 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   if (mine.hasSend) NCCLCHECK(ipcHandleOf(send, &mine.sendH, &mine.sendOff));
   if (mine.hasRecv) NCCLCHECK(ipcHandleOf(recv, &mine.recvH, &mine.recvOff));
   std::vector<MpCallInfo> all(n);
-  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
+  NCCLCHECK(mpExchange(mp, seq, &mine, sizeof(mine), all.data()));
   for (int j = 0; j < n; j++) {
     const MpCallInfo& a = all[j];
     if (a.seq != seq || a.kind != mine.kind || a.dt != mine.dt || a.op != mine.op || a.root != root ||
@@ -1371,6 +1423,35 @@ NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slot
                                    uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax) {
   return (int)chooseProtoFor(protoMask, twoShotKind != 0, slotBytes, blockBytes, nRanks, llMaxBytes, ll128MaxBytes,
                              ll128OneShotMax);
+}
+
+NBX_EXPORT ncclResult_t nbxShmxSelfTest(const char* name, int rank, int nranks, int rounds, int jitterUs) {
+  if (name == nullptr || nranks < 1 || rank < 0 || rank >= nranks || rounds < 0) return ncclInvalidArgument;
+  constexpr size_t kMax = 256;
+  nbx::ShmExchange* x = nullptr;
+  if (rank == 0) {
+    x = nbx::shmxOpen(name, 0, nranks, kMax, true);
+  } else {
+    for (int i = 0; i < 20000 && x == nullptr; i++) {   // wait for rank 0's segment (<= ~20 s)
+      x = nbx::shmxOpen(name, rank, nranks, kMax, false);
+      if (!x) usleep(1000);
+    }
+  }
+  if (!x) return ncclSystemError;
+  std::mt19937 rng(1234u + (unsigned)rank);
+  std::vector<unsigned char> mine(kMax), all(kMax * (size_t)nranks);
+  ncclResult_t r = ncclSuccess;
+  for (int k = 1; k <= rounds && r == ncclSuccess; k++) {
+    const size_t len = 1 + (size_t)(k * 37) % kMax;
+    for (size_t i = 0; i < len; i++) mine[i] = (unsigned char)(rank * 31 + k * 7 + (int)i);
+    if (jitterUs > 0) usleep(rng() % (unsigned)jitterUs);
+    r = nbx::shmxAllGather(x, (uint64_t)(3 * k + (k % 2)), mine.data(), len, all.data(), 60.0, nullptr);
+    for (int j = 0; r == ncclSuccess && j < nranks; j++)
+      for (size_t i = 0; i < len; i++)
+        if (all[(size_t)j * len + i] != (unsigned char)(j * 31 + k * 7 + (int)i)) r = ncclInternalError;
+  }
+  nbx::shmxClose(x);
+  return r;
 }
 
 NBX_EXPORT ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds) {
