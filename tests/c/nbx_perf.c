@@ -6,9 +6,14 @@
  *
  *   nbx_perf [-c allreduce|reducescatter|reduce] [-d dev,dev,...] [-b minbytes]
  *            [-e maxbytes] [-f factor] [-n iters] [-w warmup] [-t float|half|bfloat16|int32|int64|double]
- *            [-o sum|prod|max|min|avg]
+ *            [-o sum|prod|max|min|avg] [-p 0|1]
  *
  * -d lists the device of each rank (a device may repeat: ranks sharing one GPU).
+ * -p 1 runs one process per rank instead (fork after ncclGetUniqueId, each
+ * child ncclCommInitRank on its device — the multi-process communicator with
+ * its LL / LL128 / Simple protocols); times and #wrong are reduced over the
+ * ranks with the library's own ncclAllReduce (max / sum), as nccl-tests does
+ * with MPI.
  * Sizes are the per-rank send size in bytes (nccl-tests' convention for
  * all_reduce; reduce_scatter sends nranks x recvcount). Each size is checked:
  * rank r's input element i is ((i * 7 + r * 13) % 61) - 30 (exact in every
@@ -18,6 +23,8 @@
 #define _POSIX_C_SOURCE 200809L
 #include <hip/hip_runtime_api.h>
 #include <math.h>
+#include <sys/wait.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -132,8 +139,27 @@ static double expect(size_t i, int n, ncclRedOp_t op, ncclDataType_t t) {
   return acc;
 }
 
+/* max over ranks of a double and sum of an int64 through ncclAllReduce (process mode) */
+static void reduceStats(ncclComm_t comm, hipStream_t st, double* t, long* wrong) {
+  double* dt;
+  int64_t* dw;
+  HIPT(hipMalloc((void**)&dt, sizeof(double)));
+  HIPT(hipMalloc((void**)&dw, sizeof(int64_t)));
+  int64_t w = *wrong;
+  HIPT(hipMemcpy(dt, t, sizeof(double), hipMemcpyHostToDevice));
+  HIPT(hipMemcpy(dw, &w, sizeof(int64_t), hipMemcpyHostToDevice));
+  NCCLT(ncclAllReduce(dt, dt, 1, ncclFloat64, ncclMax, comm, st));
+  NCCLT(ncclAllReduce(dw, dw, 1, ncclInt64, ncclSum, comm, st));
+  HIPT(hipStreamSynchronize(st));
+  HIPT(hipMemcpy(t, dt, sizeof(double), hipMemcpyDeviceToHost));
+  HIPT(hipMemcpy(&w, dw, sizeof(int64_t), hipMemcpyDeviceToHost));
+  *wrong = (long)w;
+  HIPT(hipFree(dt));
+  HIPT(hipFree(dw));
+}
+
 int main(int argc, char** argv) {
-  int coll = kAllReduce, n = 0, devs[MAXR], iters = 20, warm = 5;
+  int coll = kAllReduce, n = 0, devs[MAXR], iters = 20, warm = 5, procMode = 0;
   size_t minB = 4096, maxB = 16u << 20;
   double factor = 4.0;
   ncclDataType_t type = ncclFloat32;
@@ -160,7 +186,7 @@ int main(int argc, char** argv) {
     } else if (!strcmp(k, "-o")) {
       op = !strcmp(v, "prod") ? ncclProd : !strcmp(v, "max") ? ncclMax : !strcmp(v, "min") ? ncclMin
            : !strcmp(v, "avg") ? ncclAvg : ncclSum;
-    }
+    } else if (!strcmp(k, "-p")) procMode = atoi(v);
   }
   if (n == 0) {
     int cnt = 0;
@@ -169,21 +195,57 @@ int main(int argc, char** argv) {
   }
   const int eb = tsize(type);
   ncclComm_t comms[MAXR];
-  NCCLT(ncclCommInitAll(comms, n, devs));
+  /* local ranks [lo, hi): every rank in clique mode, this process's rank in process mode */
+  int lo = 0, hi = n;
+  if (procMode) {
+    ncclUniqueId id;
+    NCCLT(ncclGetUniqueId(&id));   /* bootstrap root thread in this (parent) process; no HIP yet */
+    fflush(stdout);
+    int me = -1;
+    pid_t pids[MAXR];
+    for (int r = 0; r < n; r++) {
+      pids[r] = fork();
+      if (pids[r] < 0) return 2;
+      if (pids[r] == 0) {
+        me = r;
+        break;
+      }
+    }
+    if (me < 0) {   /* parent: wait for every rank, exit with the worst status */
+      int worst = 0;
+      for (int r = 0; r < n; r++) {
+        int status = 0;
+        waitpid(pids[r], &status, 0);
+        const int rc = WIFEXITED(status) ? WEXITSTATUS(status) : 3;
+        if (rc > worst) worst = rc;
+      }
+      return worst;
+    }
+    lo = me;
+    hi = me + 1;
+    HIPT(hipSetDevice(devs[me]));
+    NCCLT(ncclCommInitRank(&comms[me], n, id, me));
+  } else {
+    NCCLT(ncclCommInitAll(comms, n, devs));
+  }
+  const int printer = lo == 0;
   hipStream_t st[MAXR];
   void *sb[MAXR], *rb[MAXR];
   const size_t sendMax = maxB, recvMax = coll == kReduceScatter ? maxB / (size_t)n + 16 : maxB;
-  for (int r = 0; r < n; r++) {
+  for (int r = lo; r < hi; r++) {
     HIPT(hipSetDevice(devs[r]));
     HIPT(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking));
     HIPT(hipMalloc(&sb[r], sendMax));
     HIPT(hipMalloc(&rb[r], recvMax > sendMax ? recvMax : sendMax));
   }
   void* host = malloc(sendMax);
-  printf("# nbx_perf: %s, %d ranks, devices", cname, n);
-  for (int r = 0; r < n; r++) printf(" %d", devs[r]);
-  printf("\n#\n# %12s %12s %8s %6s   %9s %8s %8s %6s   %9s %8s %8s %6s\n", "size", "count", "type", "redop",
-         "time(us)", "algbw", "busbw", "#wrong", "time(us)", "algbw", "busbw", "#wrong");
+  if (printer) {
+    printf("# nbx_perf: %s, %d ranks (%s), devices", cname, n,
+           procMode ? "one process per rank" : "one process, ncclCommInitAll");
+    for (int r = 0; r < n; r++) printf(" %d", devs[r]);
+    printf("\n#\n# %12s %12s %8s %6s   %9s %8s %8s %6s   %9s %8s %8s %6s\n", "size", "count", "type", "redop",
+           "time(us)", "algbw", "busbw", "#wrong", "time(us)", "algbw", "busbw", "#wrong");
+  }
   long totalWrong = 0;
   for (size_t bytes = minB; bytes <= maxB; bytes = (size_t)((double)bytes * factor) > bytes ? (size_t)((double)bytes * factor) : bytes + 1) {
     size_t sendCount = bytes / (size_t)eb;
@@ -194,25 +256,28 @@ int main(int argc, char** argv) {
     double us[2];
     long wrong[2];
     for (int inplace = 0; inplace < 2; inplace++) {
-      for (int r = 0; r < n; r++) {   /* inputs */
+      for (int r = lo; r < hi; r++) {   /* inputs */
         for (size_t i = 0; i < sendCount; i++) put(host, i, type, input(i, r));
         HIPT(hipSetDevice(devs[r]));
         void* dst = inplace ? rb[r] : sb[r];
-        HIPT(hipMemcpy(dst, host, sendCount * (size_t)eb, hipMemcpyHostToDevice));
-        if (!inplace) HIPT(hipMemset(rb[r], 0, outCount * (size_t)eb));
+        /* on the rank's own (non-blocking) stream: a null-stream hipMemset would not be
+         * ordered before the collective */
+        HIPT(hipMemcpyAsync(dst, host, sendCount * (size_t)eb, hipMemcpyHostToDevice, st[r]));
+        if (!inplace) HIPT(hipMemsetAsync(rb[r], 0, outCount * (size_t)eb, st[r]));
+        HIPT(hipStreamSynchronize(st[r]));
       }
       const int root = 0;
       /* in place: AllReduce / Reduce send == recv; ReduceScatter recv = send + rank * recvcount */
       for (int it = -1; it < warm + iters; it++) {
         if (it == warm) {
-          for (int r = 0; r < n; r++) {
+          for (int r = lo; r < hi; r++) {
             HIPT(hipSetDevice(devs[r]));
             HIPT(hipStreamSynchronize(st[r]));
           }
           us[inplace] = now_s();
         }
         NCCLT(ncclGroupStart());
-        for (int r = 0; r < n; r++) {
+        for (int r = lo; r < hi; r++) {
           const void* s = inplace ? rb[r] : sb[r];
           void* d = rb[r];
           if (coll == kReduceScatter && inplace) d = (char*)rb[r] + (size_t)r * count * (size_t)eb;
@@ -223,15 +288,16 @@ int main(int argc, char** argv) {
         NCCLT(ncclGroupEnd());
         if (it == -1) {   /* check the first call's result (later calls re-reduce in-place data) */
           wrong[inplace] = 0;
-          for (int r = 0; r < n; r++) {
+          for (int r = lo; r < hi; r++) {
             HIPT(hipSetDevice(devs[r]));
             HIPT(hipStreamSynchronize(st[r]));
           }
-          for (int r = 0; r < n; r++) {
+          for (int r = lo; r < hi; r++) {
             if (coll == kReduce && r != root) continue;
             HIPT(hipSetDevice(devs[r]));
             const char* d = (const char*)rb[r] + ((coll == kReduceScatter && inplace) ? (size_t)r * count * (size_t)eb : 0);
-            HIPT(hipMemcpy(host, d, outCount * (size_t)eb, hipMemcpyDeviceToHost));
+            HIPT(hipMemcpyAsync(host, d, outCount * (size_t)eb, hipMemcpyDeviceToHost, st[r]));
+            HIPT(hipStreamSynchronize(st[r]));
             const size_t base = coll == kReduceScatter ? (size_t)r * count : 0;
             /* exact, except ncclAvg on floats: a PreMulSum by a rounded 1/n and a
              * rounded sum of rounded products — bounded relative to sum_r |x_r| / n
@@ -249,19 +315,21 @@ int main(int argc, char** argv) {
           }
           /* restore in-place inputs consumed by the checked call */
           if (inplace) {
-            for (int r = 0; r < n; r++) {
+            for (int r = lo; r < hi; r++) {
               for (size_t i = 0; i < sendCount; i++) put(host, i, type, input(i, r));
               HIPT(hipSetDevice(devs[r]));
-              HIPT(hipMemcpy(rb[r], host, sendCount * (size_t)eb, hipMemcpyHostToDevice));
+              HIPT(hipMemcpyAsync(rb[r], host, sendCount * (size_t)eb, hipMemcpyHostToDevice, st[r]));
+              HIPT(hipStreamSynchronize(st[r]));
             }
           }
         }
       }
-      for (int r = 0; r < n; r++) {
+      for (int r = lo; r < hi; r++) {
         HIPT(hipSetDevice(devs[r]));
         HIPT(hipStreamSynchronize(st[r]));
       }
       us[inplace] = (now_s() - us[inplace]) * 1e6 / iters;
+      if (procMode) reduceStats(comms[lo], st[lo], &us[inplace], &wrong[inplace]);
       totalWrong += wrong[inplace];
     }
     const double algFactor = coll == kReduceScatter ? (double)n : 1.0;   /* bytes = recv x nranks for RS */
@@ -270,16 +338,18 @@ int main(int argc, char** argv) {
     const char* tn = type == ncclFloat16 ? "half" : type == ncclBfloat16 ? "bfloat16" : type == ncclInt32 ? "int32"
                      : type == ncclInt64 ? "int64" : type == ncclFloat64 ? "double" : "float";
     const char* on = op == ncclProd ? "prod" : op == ncclMax ? "max" : op == ncclMin ? "min" : op == ncclAvg ? "avg" : "sum";
-    printf("  %12zu %12zu %8s %6s", (size_t)sz, count, tn, on);
-    for (int k = 0; k < 2; k++) {
-      const double alg = sz / (us[k] * 1e-6) / 1e9;
-      printf("   %9.2f %8.2f %8.2f %6ld", us[k], alg, alg * bus, wrong[k]);
+    if (printer) {
+      printf("  %12zu %12zu %8s %6s", (size_t)sz, count, tn, on);
+      for (int k = 0; k < 2; k++) {
+        const double alg = sz / (us[k] * 1e-6) / 1e9;
+        printf("   %9.2f %8.2f %8.2f %6ld", us[k], alg, alg * bus, wrong[k]);
+      }
+      printf("\n");
+      fflush(stdout);
     }
-    printf("\n");
-    fflush(stdout);
   }
-  printf("# Out of bounds values : %ld %s\n", totalWrong, totalWrong ? "FAILED" : "OK");
-  for (int r = 0; r < n; r++) {
+  if (printer) printf("# Out of bounds values : %ld %s\n", totalWrong, totalWrong ? "FAILED" : "OK");
+  for (int r = lo; r < hi; r++) {
     HIPT(hipSetDevice(devs[r]));
     HIPT(hipFree(sb[r]));
     HIPT(hipFree(rb[r]));
