@@ -252,6 +252,31 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     return out
 
 
+def vs_rccl(coll, rccl):
+    """libnbxccl time / RCCL time ratios on the same shapes (< 1: libnbxccl faster)."""
+    if not coll or not rccl or not rccl.get("ok"):
+        return None
+    out = {}
+
+    def ratio(ours, theirs):
+        return None if ours is None or not theirs else round(ours / theirs, 3)
+    ar, rs = coll.get("allreduce_direct"), coll.get("reduce_scatter")
+    out["allreduce_1GiB"] = ratio(ar and ar["ms"], rccl.get("allreduce", {}).get("ms"))
+    out["reduce_scatter_1GiB"] = ratio(rs and rs["ms"], rccl.get("reduce_scatter", {}).get("ms"))
+    out["allreduce_1MiB"] = ratio(coll.get("ll128_allreduce_1MiB_us"), rccl.get("allreduce_1MiB_us"))
+    out["allreduce_4KiB"] = ratio(coll.get("ll_allreduce_4KiB_us"), rccl.get("allreduce_4KiB_us"))
+    sw, rsw = coll.get("protocol_sweep") or {}, rccl.get("sweep_allreduce_us")
+    if sw.get("bytes") and rsw:
+        best = []
+        for i, b in enumerate(sw["bytes"]):
+            cands = [sw[k][i] for k in ("LL", "LL128", "LL128_oneshot", "Simple") if sw.get(k) and i < len(sw[k])]
+            j = SWEEP_BYTES.index(b) if b in SWEEP_BYTES else None
+            best.append(None if not cands or j is None else round(min(cands) / rsw[j], 3))
+        out["sweep_best_protocol"] = best
+    out["what"] = "libnbxccl time / RCCL time (< 1: libnbxccl faster)"
+    return out
+
+
 def rccl_leg(world: int):
     """RCCL (torch.distributed "nccl" on ROCm) on the same config-D shapes, in
     this process after the collective leg: the vendor library's all-reduce /
@@ -405,6 +430,7 @@ def main():
             rccl = rccl_leg(world)
             if coll is not None:
                 coll["rccl"] = rccl
+                coll["vs_rccl"] = vs_rccl(coll, rccl)
         result["collective"] = coll
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if child is None:
