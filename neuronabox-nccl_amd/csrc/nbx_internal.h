@@ -6,6 +6,13 @@
 
 namespace nbx {
 struct LLArgs;
+// nbxReduceMulti with internal flags: kReduceAcquireSystem makes every
+// workgroup issue a system-scope acquire before its first load (sources in
+// peer GPU memory, written before the launch and ordered by a flag barrier).
+constexpr int kReduceAcquireSystem = 1;
+ncclResult_t reduceMultiEx(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs, size_t count,
+                           ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
+                           ncclStream_t stream, int flags);
 // Launch the LL collective kernel of (datatype, op) (nbx_ll.h); sequencing is
 // device-resident (args.state).
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);

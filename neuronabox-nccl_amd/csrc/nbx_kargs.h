@@ -23,6 +23,7 @@ struct KArgs {
   int32_t postOp;
   int32_t headElts;   // elements before the 16-B aligned body
   int32_t variant;    // 0 = small tile (U = 1), 1 = big tile
+  int32_t acquireSystem;  // 1: system-scope acquire at kernel start (sources include peer GPU memory)
 };
 
 // Launch table for one functor (kernel entry points as host handles).

@@ -102,10 +102,20 @@ __device__ __forceinline__ void loadTile(u32x4 (&v)[NSRC][U], const u32x4* const
 // before folding. (A software-pipelined variant — next tile's loads issued
 // before the current tile is stored — measured neutral to -5 % in-process on
 // MI355X, profiles/r1/sweep_lib_r1d.jsonl, and was dropped.)
+// Reading another GPU's memory (the collectives' direct schedules): drop any
+// line of peer memory this XCD's L2 / this CU's L1 may still hold from an
+// earlier call before the first load — the peers wrote it after that, and
+// ordered their writes before this launch through the flag barrier. Every
+// workgroup does it (one per CU at the big tile: every XCD's L2 is covered).
+__device__ __forceinline__ void acquirePeerData(const KArgs& a) {
+  if (a.acquireSystem) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 template <class Fn, int NSRC, int U>
 __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
+  acquirePeerData(a);
   const Fn fn(loadArg<Fn>(a));
   const uint64_t headBytes = (uint64_t)a.headElts * sizeof(E);
   const u32x4* src[NSRC];
@@ -125,6 +135,9 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
       // full tile: issue every load first, then fold
       u32x4 v[NSRC][U];
       loadTile<NSRC, U>(v, src, p);
+      // keep every load of the tile ahead of the fold: left to itself the
+      // scheduler waits on the first few loads before issuing the rest
+      __builtin_amdgcn_sched_barrier(0);
       foldStore<Fn, NSRC, U>(fn, v, preMask, doPost, dst, nDsts, p);
     } else {
       // last, partial tile
@@ -155,6 +168,7 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
 // Element kernel: pointers with different alignments modulo 16.
 template <class Fn>
 __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
+  acquirePeerData(a);
   const Fn fn(loadArg<Fn>(a));
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < a.nElts; i += stride)

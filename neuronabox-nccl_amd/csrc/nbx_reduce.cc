@@ -107,9 +107,10 @@ bool overlaps(const void* a, const void* b, size_t bytes) {
 // One kernel pass over <= kMaxKSrcs sources.
 ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const void* const* srcs,
                         int nSrcs, size_t count, const nbxDevRedOpFull& op, uint32_t preMask,
-                        int postOp, hipStream_t stream) {
+                        int postOp, int acquireSystem, hipStream_t stream) {
   KArgs a;
   std::memset(&a, 0, sizeof(a));
+  a.acquireSystem = acquireSystem;
   for (int s = 0; s < nSrcs; s++) a.src[s] = srcs[s];
   for (int d = 0; d < kMaxKDsts; d++) a.dst[d] = dsts[d < nDsts ? d : 0];
   a.nElts = count;
@@ -316,10 +317,11 @@ __attribute__((visibility("default"))) ncclResult_t nbxHostToDevRedOp(nbxDevRedO
   }
 }
 
-__attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
-                                                                    const void* const* srcs, int nSrcs, size_t count,
-                                                                    ncclDataType_t datatype, nbxDevRedOpFull op,
-                                                                    int nPreOpSrcs, int postOp, ncclStream_t stream) {
+namespace {
+ncclResult_t reduceMultiImpl(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs, size_t count,
+                             ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
+                             ncclStream_t stream, int flags) {
+  const int acq = (flags & nbx::kReduceAcquireSystem) ? 1 : 0;
   const int dt = (int)datatype;
   if (dt < 0 || dt >= kNumTypes) return ncclInvalidArgument;
   if (op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
@@ -345,7 +347,7 @@ __attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* 
     if (pre)
       for (int s = 0; s < nSrcs; s++)
         if (s < nPreOpSrcs) mask |= 1u << s;
-    return launchPass(ks, dsts, nDsts, srcs, nSrcs, count, op, mask, post, st);
+    return launchPass(ks, dsts, nDsts, srcs, nSrcs, count, op, mask, post, acq, st);
   }
 
   // > 8 sources: ordered multi-pass left fold through dsts[0]:
@@ -358,7 +360,7 @@ __attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* 
   if (pre)
     for (int s = 0; s < kMaxKSrcs; s++)
       if (s < nPreOpSrcs) mask |= 1u << s;
-  ncclResult_t r = launchPass(ks, dsts, 1, srcs, kMaxKSrcs, count, op, mask, 0, st);
+  ncclResult_t r = launchPass(ks, dsts, 1, srcs, kMaxKSrcs, count, op, mask, 0, acq, st);
   if (r != ncclSuccess) return r;
   int next = kMaxKSrcs;
   while (next < nSrcs) {
@@ -371,10 +373,30 @@ __attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* 
       ps[n++] = srcs[next++];
     }
     const bool last = next >= nSrcs;
-    r = launchPass(ks, dsts, last ? nDsts : 1, ps, n, count, op, m, last ? post : 0, st);
+    r = launchPass(ks, dsts, last ? nDsts : 1, ps, n, count, op, m, last ? post : 0, acq, st);
     if (r != ncclSuccess) return r;
   }
   return ncclSuccess;
+}
+}  // namespace
+
+}  // extern "C"
+
+namespace nbx {
+ncclResult_t reduceMultiEx(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs, size_t count,
+                           ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
+                           ncclStream_t stream, int flags) {
+  return reduceMultiImpl(dsts, nDsts, srcs, nSrcs, count, datatype, op, nPreOpSrcs, postOp, stream, flags);
+}
+}  // namespace nbx
+
+extern "C" {
+
+__attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
+                                                                    const void* const* srcs, int nSrcs, size_t count,
+                                                                    ncclDataType_t datatype, nbxDevRedOpFull op,
+                                                                    int nPreOpSrcs, int postOp, ncclStream_t stream) {
+  return reduceMultiImpl(dsts, nDsts, srcs, nSrcs, count, datatype, op, nPreOpSrcs, postOp, stream, 0);
 }
 
 __attribute__((visibility("default"))) ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int variant) {

@@ -403,8 +403,8 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
       for (int k = 0; k < n; k++) dsts.push_back((char*)parts[(r + k) % n].recv + off * (size_t)eb);
     nbxDevRedOpFull op = parts[r].op;
     NBX_TRACE("clique reduce rank %d off=%zu len=%zu dst=%p src0=%p", r, off, len, dsts[0], srcs[0]);
-    NCCLCHECK(nbxReduceMulti(dsts.data(), (int)dsts.size(), srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n, postOp,
-                             (ncclStream_t)parts[r].stream));
+    NCCLCHECK(nbx::reduceMultiEx(dsts.data(), (int)dsts.size(), srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n,
+                                 postOp, (ncclStream_t)parts[r].stream, nbx::kReduceAcquireSystem));
   }
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
@@ -1027,8 +1027,9 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
                                        : (const void*)(recvP[left] + off * (size_t)eb)};
         void* dsts[1] = {recvP[me] + off * (size_t)eb};
         const bool last = st == n - 2;
-        NCCLCHECK(nbxReduceMulti(last && push ? allOutputs(off) : dsts, last && push ? n : 1, srcs, 2, len, dt, op,
-                                 st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream));
+        NCCLCHECK(nbx::reduceMultiEx(last && push ? allOutputs(off) : dsts, last && push ? n : 1, srcs, 2, len, dt,
+                                     op, st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream,
+                                     nbx::kReduceAcquireSystem));
       }
       if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, 1ull << left, stream));
     }
@@ -1050,8 +1051,8 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
                 : kind == kReduce      ? (void*)(recvP[root] + off * (size_t)eb)
                                        : (void*)(recvP[me] + off * (size_t)eb);
     void* dsts[1] = {dst};
-    NCCLCHECK(nbxReduceMulti(push ? allOutputs(off) : dsts, push ? n : 1, srcs.data(), n, len, dt, op, n, 1,
-                             (ncclStream_t)stream));
+    NCCLCHECK(nbx::reduceMultiEx(push ? allOutputs(off) : dsts, push ? n : 1, srcs.data(), n, len, dt, op, n, 1,
+                                 (ncclStream_t)stream, nbx::kReduceAcquireSystem));
   }
   }
   // 3. AllReduce with n > NBX_MAX_DSTS: gather the peers' reduced blocks
@@ -1065,7 +1066,8 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
       if (l == 0) continue;
       void* d[1] = {recvP[me] + o * (size_t)eb};
       const void* s1[1] = {recvP[j] + o * (size_t)eb};
-      NCCLCHECK(nbxReduceMulti(d, 1, s1, 1, l * (size_t)eb, ncclUint8, copyOp, 0, 0, (ncclStream_t)stream));
+      NCCLCHECK(nbx::reduceMultiEx(d, 1, s1, 1, l * (size_t)eb, ncclUint8, copyOp, 0, 0, (ncclStream_t)stream,
+                                   nbx::kReduceAcquireSystem));
     }
   }
   // 4. nobody reuses its buffers while a peer may still read them
