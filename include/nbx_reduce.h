@@ -49,7 +49,7 @@ typedef struct {
   uint64_t scalarArg;
 } nbxDevRedOpFull;
 
-#define NBX_MAX_SRCS 32   /* > 8 sources run as ordered multi-pass folds */
+#define NBX_MAX_SRCS 64   /* > 8 sources run as ordered multi-pass folds (one source per rank up to 64) */
 #define NBX_MAX_DSTS 8    /* NCCL_MAX_DIRECT_ARITY + 1 (device.h:147): local output + 7 peers */
 
 /* Host-side op encoding: replaces hostToDevRedOp, enqueue.cc:1436-1512, for

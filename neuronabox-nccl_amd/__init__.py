@@ -87,7 +87,7 @@ TYPE_SIZE = {
 }
 
 NCCL_UNIQUE_ID_BYTES = 128
-NBX_MAX_SRCS = 32
+NBX_MAX_SRCS = 64
 NBX_MAX_DSTS = 8
 
 

@@ -499,6 +499,7 @@ ncclResult_t flushPendingImpl() {
 // one-shot direct exchange as the in-process clique.
 
 enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kSlotRing = 3, kNumSlots = 4 };
+constexpr int kMaxMpRanks = 64;
 
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
@@ -1154,6 +1155,11 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
     warn("ncclCommInitRank : unique id was not produced by ncclGetUniqueId");
     return ncclInvalidArgument;
   }
+  if (nranks > kMaxMpRanks) {   // 64-bit rank masks in the barrier kernel, one source per rank
+    warn("ncclCommInitRank : %d ranks requested, this build supports up to %d per communicator", nranks,
+         kMaxMpRanks);
+    return ncclInvalidArgument;
+  }
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
   if (nranks == 1) return newComm(newcomm, 1, 0, dev, config);
@@ -1185,7 +1191,7 @@ NBX_API(ncclResult_t, ncclCommInitRank, ncclComm_t* newcomm, int nranks, ncclUni
 
 NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* devlist) {
   // init.cc:1678-1734. Several ranks may share one device (emulation / testing).
-  if (comms == nullptr || ndev < 1) {
+  if (comms == nullptr || ndev < 1 || ndev > kMaxMpRanks) {
     warn("ncclCommInitAll : invalid arguments");
     return ncclInvalidArgument;
   }

@@ -121,6 +121,7 @@ def test_comm_api_errors_without_device(nbx):
     assert lib.ncclCommInitRank(ctypes.byref(h), 0, uid, 0) == 4
     bad = nbx.ncclUniqueId()
     assert lib.ncclCommInitRank(ctypes.byref(h), 1, bad, 0) == 4      # not from ncclGetUniqueId
+    assert lib.ncclCommInitRank(ctypes.byref(h), 65, uid, 0) == 4     # > 64 ranks per communicator
     assert lib.ncclAllReduce(None, None, 0, 7, 0, None, None) == 4    # NULL comm (argcheck.cc:28-34)
     assert lib.ncclRedOpDestroy(0, ctypes.c_void_p(1)) == 4           # builtin op
     assert lib.ncclRedOpDestroy(-1, ctypes.c_void_p(1)) == 4          # garbage

@@ -188,7 +188,7 @@ def test_many_destinations(nbx, oracle, torch_gpu, dtype, ndst, nsrc):
              dst_off=[(off + eb * d) % 16 for d in range(ndst)])   # mixed alignments: element kernel
 
 
-@pytest.mark.parametrize("nsrc", [9, 15, 16, 20, 32])
+@pytest.mark.parametrize("nsrc", [9, 15, 16, 20, 32, 64])
 def test_many_sources_multipass(nbx, oracle, torch_gpu, nsrc):
     srcs = oracle.random_inputs(7, nsrc, 30011, seed=nsrc)
     run_case(nbx, oracle, torch_gpu, srcs, 7, 0, 0)
@@ -226,7 +226,7 @@ def test_invalid_arguments(nbx, torch_gpu):
     op = nbx.DevRedOpFull()
     E = nbx.ncclResult.ncclInvalidArgument
     assert nbx.reduce_multi_raw([p], [], 16, 7, op) == E                       # no sources
-    assert nbx.reduce_multi_raw([p], [p] * 33, 16, 7, op) == E                 # > NBX_MAX_SRCS
+    assert nbx.reduce_multi_raw([p], [p] * 65, 16, 7, op) == E                 # > NBX_MAX_SRCS (64)
     assert nbx.reduce_multi_raw([p] * 9, [p], 16, 7, op) == E                  # > NBX_MAX_DSTS (8)
     assert nbx.reduce_multi_raw([p], [p], 16, 12, op) == E                     # bad datatype
     op.op = 4
