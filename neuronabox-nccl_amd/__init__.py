@@ -348,6 +348,12 @@ class Communicator:
             _check(load_library().ncclCommDestroy(self.handle), "ncclCommDestroy")
             self.handle = ctypes.c_void_p()
 
+    def abort(self) -> None:
+        """ncclCommAbort: ends every spinning wait of this communicator, frees it."""
+        if self.handle:
+            _check(load_library().ncclCommAbort(self.handle), "ncclCommAbort")
+            self.handle = ctypes.c_void_p()
+
 
 # ---------------------------------------------------------------------------
 # torch helpers (torch is plumbing only: device memory and streams)

@@ -462,3 +462,117 @@ def test_multiprocess_graph_capture(nbx, n, monkeypatch):
         for p in procs:
             if p.is_alive():
                 p.terminate()
+
+
+def _child_failure(uid_bytes, rank, q, evq):
+    """Rank 0 meets an absent peer: the LL kernel's bounded spin times out
+    (ncclRemoteError via ncclCommGetAsyncError), the Simple path's host
+    exchange times out (the call returns ncclRemoteError), and ncclCommAbort
+    ends a spinning kernel at once. Rank 1 joins the communicator and then
+    issues nothing until rank 0 is done."""
+    try:
+        import time
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(2, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        if rank == 1:
+            evq.get(timeout=240)   # rank 0 finished
+            comm.destroy()
+            q.put((rank, "ok", None))
+            return
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        x = torch.ones(1024, device="cuda")
+        y = torch.empty_like(x)
+        t0 = time.perf_counter()
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), 1024, 7, 0, st)   # LL: the kernel spins, then times out
+        torch.cuda.synchronize()
+        out["ll_timeout_s"] = time.perf_counter() - t0
+        out["ll_async_error"] = comm.async_error()
+        big = torch.ones(4 << 20, device="cuda")   # 16 MiB: Simple path, host exchange
+        t0 = time.perf_counter()
+        try:
+            comm.all_reduce(big.data_ptr(), big.data_ptr(), big.numel(), 7, 0, st)
+            out["simple_error"] = 0
+        except nbx.NcclError as e:
+            out["simple_error"] = int(e.code)
+        out["simple_timeout_s"] = time.perf_counter() - t0
+        comm.abort()
+        # a fresh communicator whose peer never calls: abort ends the spinning kernel
+        evq.put("next")
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def _child_abort(uid_bytes, rank, q, evq):
+    try:
+        import threading
+        import time
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(2, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        if rank == 1:
+            evq.get(timeout=240)
+            comm.destroy()
+            q.put((rank, "ok", None))
+            return
+        st = torch.cuda.current_stream().cuda_stream
+        x = torch.ones(1024, device="cuda")
+        comm.all_reduce(x.data_ptr(), x.data_ptr(), 1024, 7, 0, st)   # spins: the peer never arrives
+        time.sleep(0.5)
+        t0 = time.perf_counter()
+        comm.abort()   # sets the abort word, waits for the device, frees
+        torch.cuda.synchronize()
+        evq.put("done")
+        q.put((rank, "ok", {"abort_s": time.perf_counter() - t0}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_timeout_and_abort(nbx, monkeypatch):
+    """Failure handling with a peer that never arrives: bounded spins end with
+    ncclRemoteError (kernel path: async error; host exchange: the call's return
+    code) after NBX_TIMEOUT_SEC, and ncclCommAbort ends a spinning kernel in
+    well under that timeout."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "3")
+    ctx = mp.get_context("spawn")
+    for child, check in ((_child_failure, "failure"), (_child_abort, "abort")):
+        if check == "abort":
+            monkeypatch.setenv("NBX_TIMEOUT_SEC", "120")
+        uid = nbx.get_unique_id()
+        q, evq = ctx.Queue(), ctx.Queue()
+        procs = [ctx.Process(target=child, args=(bytes(uid), r, q, evq), daemon=True) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = {}
+        try:
+            for _ in range(2):
+                rank, status, payload = q.get(timeout=300)
+                assert status == "ok", f"{check} rank {rank}:\n{payload}"
+                res[rank] = payload
+            for p in procs:
+                p.join(timeout=60)
+        finally:
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+        r0 = res[0]
+        if check == "failure":
+            assert r0["ll_async_error"] == 6, r0          # ncclRemoteError
+            assert 2.5 < r0["ll_timeout_s"] < 30, r0
+            assert r0["simple_error"] == 6, r0
+            assert 2.5 < r0["simple_timeout_s"] < 30, r0
+        else:
+            assert r0["abort_s"] < 20, r0                 # not the 120 s timeout
