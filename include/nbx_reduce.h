@@ -72,6 +72,32 @@ ncclResult_t nbxReduceMulti(void* const* dsts, int nDsts,
                             nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
                             ncclStream_t stream);
 
+/* One bucket of a batched reduction (same meaning as nbxReduceMulti's arguments). */
+typedef struct {
+  void* const* dsts;
+  int nDsts;
+  const void* const* srcs;
+  int nSrcs;
+  size_t count;
+} nbxReduceTask;
+
+/* Batched form: nTasks independent buckets with one datatype and op, as if
+ * nbxReduceMulti were called for each — the analogue of NCCL packing grouped
+ * collectives into one kernel's work list (enqueue.cc:67-91
+ * appendWorkElemColl, NCCL_MAX_WORK_ELEMENTS, device.h:230). Buckets with the
+ * same source count (<= 8) and one shared pointer alignment run together
+ * (46 to 101 single-destination buckets per launch, from 8 down to 2
+ * sources), their tiles in one index space, so many small buckets fill the
+ * GPU like one large one; large buckets of 3+ sources, > 8 sources or mixed
+ * alignments run as single-bucket launches. Buckets must be independent: no bucket's destinations
+ * may overlap another bucket's sources or destinations (they may run
+ * concurrently, in any order). Every bucket is checked before anything is
+ * enqueued; errors as nbxReduceMulti (nTasks < 0 or tasks == NULL with
+ * nTasks > 0: ncclInvalidArgument). nTasks == 0 is a no-op. */
+ncclResult_t nbxReduceMultiBatch(const nbxReduceTask* tasks, int nTasks,
+                                 ncclDataType_t datatype, nbxDevRedOpFull op,
+                                 int nPreOpSrcs, int postOp, ncclStream_t stream);
+
 /* Host-staged form of nbxReduceMulti: sources and destinations in HOST memory
  * (pinned for full speed; pageable works), the path NCCL's NET/SHM transports
  * stage through (host-pinned proxy FIFOs net.cc:735/883, /dev/shm buffers
@@ -88,7 +114,7 @@ ncclResult_t nbxReduceMultiHost(void* const* hostDsts, int nDsts,
 
 /* Launch knobs (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues, tuning.cc:12,
  * connect.cc:314): blocksPerCU caps the grid at CUs x blocksPerCU workgroups
- * (0 = default: 1 for big tiles, 8 for small; env NBX_BLOCKS_PER_CU);
+ * (0 = default: 1 for big tiles, 3-5 for small; env NBX_BLOCKS_PER_CU);
  * variant 0 = auto tile choice, 1 = force small tiles, 2 = force big tiles. */
 ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int variant);
 ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* variant);

@@ -118,6 +118,13 @@ class NcclError(RuntimeError):
 
 _lib: Optional[ctypes.CDLL] = None
 
+class ReduceTask(ctypes.Structure):
+    """nbxReduceTask (include/nbx_reduce.h): one bucket of nbxReduceMultiBatch."""
+    _fields_ = [("dsts", ctypes.POINTER(ctypes.c_void_p)), ("nDsts", ctypes.c_int),
+                ("srcs", ctypes.POINTER(ctypes.c_void_p)), ("nSrcs", ctypes.c_int),
+                ("count", ctypes.c_size_t)]
+
+
 _SIGS = {
     # public ABI (include/nccl.h)
     "ncclGetVersion": [ctypes.POINTER(ctypes.c_int)],
@@ -150,6 +157,8 @@ _SIGS = {
     "nbxReduceMultiHost": [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
                            ctypes.c_int, ctypes.c_size_t, ctypes.c_int, DevRedOpFull, ctypes.c_int, ctypes.c_int,
                            ctypes.c_void_p],
+    "nbxReduceMultiBatch": [ctypes.POINTER(ReduceTask), ctypes.c_int, ctypes.c_int, DevRedOpFull, ctypes.c_int,
+                            ctypes.c_int, ctypes.c_void_p],
     "nbxSetLaunchConfig": [ctypes.c_int, ctypes.c_int],
     "nbxGetLaunchConfig": [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
     "nbxKernelCount": [],
@@ -265,6 +274,27 @@ def reduce_multi(dsts: Sequence[int], srcs: Sequence[int], count: int, dtype: in
                  n_pre_op_srcs: int = 0, post_op: bool = False, stream: int = 0) -> None:
     """The hot path: ordered left fold of `srcs` into every `dsts` (reduceCopy semantics)."""
     _check(reduce_multi_raw(dsts, srcs, count, dtype, op, n_pre_op_srcs, post_op, stream), "nbxReduceMulti")
+
+
+def reduce_multi_batch_raw(buckets: Sequence[tuple], dtype: int, op: DevRedOpFull, n_pre_op_srcs: int = 0,
+                           post_op: bool = False, stream: int = 0) -> int:
+    """Call nbxReduceMultiBatch over buckets [(dsts, srcs, count), ...]; returns the code."""
+    keep = []
+    tasks = (ReduceTask * max(1, len(buckets)))()
+    for i, (dsts, srcs, count) in enumerate(buckets):
+        d = (ctypes.c_void_p * max(1, len(dsts)))(*[ctypes.c_void_p(int(x)) for x in dsts])
+        s = (ctypes.c_void_p * max(1, len(srcs)))(*[ctypes.c_void_p(int(x)) for x in srcs])
+        keep += [d, s]
+        tasks[i] = ReduceTask(ctypes.cast(d, ctypes.POINTER(ctypes.c_void_p)), len(dsts),
+                              ctypes.cast(s, ctypes.POINTER(ctypes.c_void_p)), len(srcs), int(count))
+    return load_library().nbxReduceMultiBatch(tasks, len(buckets), int(dtype), op, int(n_pre_op_srcs),
+                                              int(bool(post_op)), ctypes.c_void_p(int(stream)))
+
+
+def reduce_multi_batch(buckets: Sequence[tuple], dtype: int, op: DevRedOpFull, n_pre_op_srcs: int = 0,
+                       post_op: bool = False, stream: int = 0) -> None:
+    """Independent buckets [(dsts, srcs, count), ...] reduced as batched launches."""
+    _check(reduce_multi_batch_raw(buckets, dtype, op, n_pre_op_srcs, post_op, stream), "nbxReduceMultiBatch")
 
 
 def reduce_multi_host(dsts: Sequence[int], srcs: Sequence[int], count: int, dtype: int, op: DevRedOpFull,

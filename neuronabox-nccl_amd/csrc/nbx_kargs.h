@@ -26,6 +26,33 @@ struct KArgs {
   int32_t acquireSystem;  // 1: system-scope acquire at kernel start (sources include peer GPU memory)
 };
 
+// Batched reduce (nbxReduceMultiBatch): several independent buckets with the
+// same functor and source count in one launch — the analogue of NCCL packing
+// grouped collectives into one ncclWork (enqueue.cc:67-91 appendWorkElemColl,
+// up to NCCL_MAX_WORK_ELEMENTS = 9 elements, device.h:230). Every bucket's
+// pointers share one alignment modulo 16. The bucket table travels in the
+// kernel-argument segment (4 KiB, read with scalar loads), packed with
+// variable-length records so a launch holds 46 (8 sources) to 101 (2 sources)
+// single-destination buckets:
+//   w[o]          tileEnd: running total of tiles through this bucket
+//   w[o+1]        nElts | headElts << 56 | nDsts << 60
+//   w[o+2 ..]     NSRC source pointers, then nDsts destination pointers
+constexpr int kBatchTilePacks = 256;   // one 16-B pack per lane per tile (kBlock lanes)
+constexpr int kBatchHeaderBytes = 40;
+constexpr int kBatchWords = (4096 - kBatchHeaderBytes) / 8;
+constexpr uint64_t kBatchCountMask = (1ull << 56) - 1;
+
+struct BatchArgs {
+  uint64_t arg;
+  const void* argPtr;
+  uint64_t totalTiles;
+  uint32_t preMask;
+  int32_t postOp;
+  int32_t nTasks;
+  int32_t acquireSystem;
+  uint64_t w[kBatchWords];
+};
+
 // Launch table for one functor (kernel entry points as host handles).
 
 struct KernelSet {
@@ -34,6 +61,7 @@ struct KernelSet {
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)
+  const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;
   int valid;

@@ -176,6 +176,92 @@ __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Batched buckets (nbxReduceMultiBatch). The tiles of every bucket form one
+// index space (bucket k owns the tiles between the previous record's tileEnd
+// and its own); workgroups grid-stride over it, so a batch of small buckets
+// fills the chip like one big bucket instead of one under-filled launch per
+// bucket. A workgroup's tiles only move forward, so its record cursor only
+// advances: a bucket's pointers are read (scalar loads from the
+// kernel-argument segment) only when the cursor moves. The workgroup that
+// owns a bucket's last tile also folds its < 16-B head and tail elements.
+template <class Fn, int NSRC>
+__device__ __forceinline__ void batchElt(const Fn& fn, const typename Fn::Elt* const (&src)[NSRC],
+                                         typename Fn::Elt* const (&dst)[kMaxKDsts], int nDsts, uint32_t preMask,
+                                         bool doPost, uint64_t i) {
+  using E = typename Fn::Elt;
+  E acc = src[0][i];
+  if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.pre(acc);
+#pragma unroll
+  for (int s = 1; s < NSRC; s++) {
+    E v = src[s][i];
+    if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) v = fn.pre(v);
+    acc = fn.red(acc, v);
+  }
+  if constexpr (Fn::kHasPost) if (doPost) acc = fn.post(acc);
+#pragma unroll
+  for (int d = 0; d < kMaxKDsts; d++)
+    if (d < nDsts) dst[d][i] = acc;
+}
+
+template <class Fn, int NSRC>
+__global__ __launch_bounds__(kBlock) void kReduceBatch(BatchArgs a) {
+  using E = typename Fn::Elt;
+  constexpr int EPP = 16 / (int)sizeof(E);
+  if (a.acquireSystem) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
+  const bool doPost = Fn::kHasPost && a.postOp;
+  const uint32_t preMask = a.preMask;
+  const uint64_t total = a.totalTiles;
+  int off = 0, len = 0, nDsts = 1, head = 0;
+  uint64_t tBegin = 0, tEnd = 0, nElts = 0, n = 0;
+  const E* sb[NSRC];
+  E* db[kMaxKDsts];
+  const u32x4* src[NSRC];
+  u32x4* dst[kMaxKDsts];
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    if (tile >= tEnd) {   // advance the bucket cursor (uniform across the workgroup)
+      uint64_t meta;
+      do {
+        off += len;
+        tBegin = tEnd;
+        tEnd = a.w[off];
+        meta = a.w[off + 1];
+        nDsts = (int)(meta >> 60);
+        len = 2 + NSRC + nDsts;
+      } while (tile >= tEnd);
+      nElts = meta & kBatchCountMask;
+      head = (int)((meta >> 56) & 15u);
+      n = (nElts - (uint64_t)head) / EPP;
+#pragma unroll
+      for (int s = 0; s < NSRC; s++) {
+        sb[s] = (const E*)a.w[off + 2 + s];
+        src[s] = (const u32x4*)(sb[s] + head);
+      }
+#pragma unroll
+      for (int d = 0; d < kMaxKDsts; d++) {
+        db[d] = (E*)a.w[off + 2 + NSRC + (d < nDsts ? d : 0)];
+        dst[d] = (u32x4*)(db[d] + head);
+      }
+    }
+    const uint64_t p = (tile - tBegin) * kBatchTilePacks + threadIdx.x;
+    if (p < n) {
+      u32x4 v[NSRC][1];
+#pragma unroll
+      for (int s = 0; s < NSRC; s++) v[s][0] = ldPack(src[s] + p);
+      foldStore<Fn, NSRC, 1>(fn, v, preMask, doPost, dst, nDsts, p);
+    }
+    if (tile == tEnd - 1) {   // the bucket's last tile: its head and tail elements
+      const uint64_t tailStart = (uint64_t)head + n * EPP;
+      const int tail = (int)(nElts - tailStart);
+      const int th = (int)threadIdx.x;
+      if (th < head) batchElt<Fn, NSRC>(fn, sb, db, nDsts, preMask, doPost, (uint64_t)th);
+      else if (th < head + tail)
+        batchElt<Fn, NSRC>(fn, sb, db, nDsts, preMask, doPost, tailStart + (uint64_t)(th - head));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Launch table for one functor.
 
 
@@ -195,10 +281,12 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   KernelSet ks{};
   const void* small[] = {(const void*)&kReducePacks<Fn, I + 1, 1>...};
   const void* big[] = {(const void*)&kReducePacks<Fn, I + 1, bigUnroll<I + 1, Fn::kUnrollCap>()>...};
+  const void* batch[] = {(const void*)&kReduceBatch<Fn, I + 1>...};
   int un[] = {bigUnroll<I + 1, Fn::kUnrollCap>()...};
   for (int i = 0; i < kMaxKSrcs; i++) {
     ks.packs[0][i] = small[i];
     ks.packs[1][i] = big[i];
+    ks.batch[i] = batch[i];
     ks.unroll[i] = un[i];
   }
   ks.elts = (const void*)&kReduceElts<Fn>;

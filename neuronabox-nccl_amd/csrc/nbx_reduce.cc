@@ -15,9 +15,11 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 
 #include "../../include/nbx_reduce.h"
@@ -72,14 +74,17 @@ int cuCount(int dev) {
 
 // Workgroups per CU: big tiles keep ~32 dwordx4 loads in flight per lane
 // slot — one 256-thread workgroup per CU (4 waves, ~128 KiB in flight per CU)
-// when nSrcs x U >= 32, proportionally more when the unroll is capped; small
-// tiles up to 8.
+// when nSrcs x U >= 32, proportionally more when the unroll is capped. Small
+// tiles (one pack per lane per source): 5 / 4 / 3 workgroups per CU for 1 / 2
+// / 3 sources, 4 above — measured on MI355X (profiles/r1/tiles_sweep_r1n.jsonl:
+// 2 sources at 256 MiB 6.80 TB/s with 4 per CU vs 6.12 with 8 and 5.91 with
+// one big-tile workgroup; 3 sources 6.58 vs 6.38 big-tile).
 int maxBlocksPerCU(bool big, int loadsPerLane) {
   int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
   if (v > 0) return v;
   static const int envBig = envInt("NBX_BLOCKS_PER_CU", 0);
   if (envBig > 0) return envBig;
-  if (!big) return 8;
+  if (!big) return loadsPerLane <= 1 ? 5 : loadsPerLane == 2 ? 4 : loadsPerLane == 3 ? 3 : 4;
   int b = (32 + loadsPerLane - 1) / loadsPerLane;
   return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
@@ -140,11 +145,14 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     const size_t nPacks = (count - head) / (size_t)epp;
     a.headElts = (int)head;
     a.nPacks = nPacks;
-    // big tiles once every CU gets at least one; small tiles below that
+    // big tiles once every CU gets at least one, for 4+ sources; small tiles
+    // below that, and always for 1-3 sources (more workgroups per CU beat
+    // deeper unrolling when a quarter or more of the traffic is stores:
+    // profiles/r1/tiles_sweep_r1n.jsonl)
     const size_t bigTile = (size_t)ks.unroll[nSrcs - 1] * kBlock;
     const size_t bigTiles = (nPacks + bigTile - 1) / bigTile;
     const int force = g_variant.load(std::memory_order_relaxed);
-    const bool big = force == 2 || (force == 0 && bigTiles >= (size_t)cus);
+    const bool big = force == 2 || (force == 0 && nSrcs > 3 && bigTiles >= (size_t)cus);
     const size_t tile = big ? bigTile : (size_t)kBlock;
     const size_t tiles = (nPacks + tile - 1) / tile;
     const size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(big, nSrcs * (big ? ks.unroll[nSrcs - 1] : 1));
@@ -318,25 +326,49 @@ __attribute__((visibility("default"))) ncclResult_t nbxHostToDevRedOp(nbxDevRedO
 }
 
 namespace {
-ncclResult_t reduceMultiImpl(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs, size_t count,
-                             ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
-                             ncclStream_t stream, int flags) {
-  const int acq = (flags & nbx::kReduceAcquireSystem) ? 1 : 0;
+// Datatype / op checks shared by the single and batched entry points; on
+// success *ks is the functor's kernel set.
+ncclResult_t checkOp(ncclDataType_t datatype, const nbxDevRedOpFull& op, const KernelSet** ks) {
   const int dt = (int)datatype;
   if (dt < 0 || dt >= kNumTypes) return ncclInvalidArgument;
   if (op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
+  const KernelSet& k = table()[dt][op.op];
+  if (!k.valid) return ncclInvalidArgument;   // e.g. SumPostDiv on floats
+  if (op.op == nbxDevSumPostDiv && !op.scalarArgIsPtr && (int)op.scalarArg == 0) return ncclInvalidArgument;
+  if (op.scalarArgIsPtr && op.scalarArg == 0) return ncclInvalidArgument;
+  *ks = &k;
+  return ncclSuccess;
+}
+
+// Per-bucket checks: counts of sources and destinations, non-null pointers
+// aligned to the element size (count == 0 accepts anything but NULL arrays).
+ncclResult_t checkBucket(const KernelSet& ks, void* const* dsts, int nDsts, const void* const* srcs, int nSrcs,
+                         size_t count) {
   if (nSrcs < 1 || nSrcs > NBX_MAX_SRCS || nDsts < 1 || nDsts > NBX_MAX_DSTS) return ncclInvalidArgument;
   if (srcs == nullptr || dsts == nullptr) return ncclInvalidArgument;
-  const KernelSet& ks = table()[dt][op.op];
-  if (!ks.valid) return ncclInvalidArgument;   // e.g. SumPostDiv on floats
-  if (op.op == nbxDevSumPostDiv && !op.scalarArgIsPtr && (int)op.scalarArg == 0) return ncclInvalidArgument;
   if (count == 0) return ncclSuccess;
   const int eb = ks.eltBytes;
   for (int s = 0; s < nSrcs; s++)
     if (srcs[s] == nullptr || ((uintptr_t)srcs[s] % (uintptr_t)eb) != 0) return ncclInvalidArgument;
   for (int d = 0; d < nDsts; d++)
     if (dsts[d] == nullptr || ((uintptr_t)dsts[d] % (uintptr_t)eb) != 0) return ncclInvalidArgument;
-  if (op.scalarArgIsPtr && op.scalarArg == 0) return ncclInvalidArgument;
+  return ncclSuccess;
+}
+
+ncclResult_t reduceMultiImpl(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs, size_t count,
+                             ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
+                             ncclStream_t stream, int flags) {
+  const int acq = (flags & nbx::kReduceAcquireSystem) ? 1 : 0;
+  const KernelSet* ksp = nullptr;
+  if (nSrcs < 1 || nSrcs > NBX_MAX_SRCS || nDsts < 1 || nDsts > NBX_MAX_DSTS) return ncclInvalidArgument;
+  if (srcs == nullptr || dsts == nullptr) return ncclInvalidArgument;
+  ncclResult_t cr = checkOp(datatype, op, &ksp);
+  if (cr != ncclSuccess) return cr;
+  const KernelSet& ks = *ksp;
+  if (count == 0) return ncclSuccess;
+  cr = checkBucket(ks, dsts, nDsts, srcs, nSrcs, count);
+  if (cr != ncclSuccess) return cr;
+  const int eb = ks.eltBytes;
   if (nPreOpSrcs < 0) nPreOpSrcs = 0;
   hipStream_t st = (hipStream_t)stream;
   const bool pre = op.op == nbxDevPreMulSum;
@@ -378,6 +410,145 @@ ncclResult_t reduceMultiImpl(void* const* dsts, int nDsts, const void* const* sr
   }
   return ncclSuccess;
 }
+
+// Shared misalignment modulo 16 of every pointer of a bucket (-1: mixed).
+int sharedMisalignment(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs) {
+  const unsigned mis = (unsigned)((uintptr_t)srcs[0] & 15u);
+  for (int s = 1; s < nSrcs; s++)
+    if (((uintptr_t)srcs[s] & 15u) != mis) return -1;
+  for (int d = 0; d < nDsts; d++)
+    if (((uintptr_t)dsts[d] & 15u) != mis) return -1;
+  return (int)mis;
+}
+
+// Packs bucket records (nbx_kargs.h BatchArgs) for kReduceBatch launches of
+// one source count; a launch goes out when the table is full, or on flush().
+struct BatchPacker {
+  const KernelSet& ks;
+  int nSrcs;
+  const nbxDevRedOpFull& op;
+  uint32_t preMask;
+  int postOp, acquireSystem;
+  hipStream_t stream;
+  BatchArgs a;
+  int used = 0;
+
+  BatchPacker(const KernelSet& k, int ns, const nbxDevRedOpFull& o, uint32_t pm, int post, int acq, hipStream_t st)
+      : ks(k), nSrcs(ns), op(o), preMask(pm), postOp(post), acquireSystem(acq), stream(st) {
+    static_assert(sizeof(BatchArgs) <= 4096, "batch table must fit the kernel-argument segment");
+    reset();
+  }
+  void reset() {
+    std::memset(&a, 0, offsetof(BatchArgs, w));
+    used = 0;
+  }
+  // appends one bucket (count > 0, one shared misalignment)
+  ncclResult_t add(const nbxReduceTask& t) {
+    const int len = 2 + nSrcs + t.nDsts;
+    if (used + len > kBatchWords) {
+      ncclResult_t r = flush();
+      if (r != ncclSuccess) return r;
+    }
+    const int eb = ks.eltBytes;
+    const uint64_t epp = (uint64_t)(16 / eb);
+    const unsigned mis = (unsigned)((uintptr_t)t.srcs[0] & 15u);
+    uint64_t head = mis ? (uint64_t)((16u - mis) / (unsigned)eb) : 0;
+    if (head > t.count) head = t.count;
+    const uint64_t nPacks = (t.count - head) / epp;
+    const uint64_t tiles = (nPacks + kBatchTilePacks - 1) / kBatchTilePacks;
+    a.totalTiles += tiles ? tiles : 1;   // a bucket below one pack still owns a tile (its elements)
+    uint64_t* w = a.w + used;
+    w[0] = a.totalTiles;
+    w[1] = (uint64_t)t.count | head << 56 | (uint64_t)t.nDsts << 60;
+    for (int s = 0; s < nSrcs; s++) w[2 + s] = (uint64_t)(uintptr_t)t.srcs[s];
+    for (int d = 0; d < t.nDsts; d++) w[2 + nSrcs + d] = (uint64_t)(uintptr_t)t.dsts[d];
+    used += len;
+    a.nTasks++;
+    return ncclSuccess;
+  }
+  ncclResult_t flush() {
+    if (a.nTasks == 0) return ncclSuccess;
+    a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+    a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+    a.preMask = preMask;
+    a.postOp = postOp;
+    a.acquireSystem = acquireSystem;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint64_t maxBlocks = (uint64_t)cuCount(dev) * (uint64_t)maxBlocksPerCU(false, nSrcs);
+    const uint64_t grid = a.totalTiles < maxBlocks ? a.totalTiles : maxBlocks;
+    void* args[] = {&a};
+    hipError_t err = hipLaunchKernel(ks.batch[nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
+    reset();
+    if (err != hipSuccess) {
+      std::fprintf(stderr, "nbx: batch kernel launch failed: %s\n", hipGetErrorString(err));
+      return ncclUnhandledCudaError;
+    }
+    return ncclSuccess;
+  }
+};
+
+ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDataType_t datatype,
+                                  nbxDevRedOpFull op, int nPreOpSrcs, int postOp, ncclStream_t stream, int flags) {
+  if (nTasks < 0 || (nTasks > 0 && tasks == nullptr)) return ncclInvalidArgument;
+  const KernelSet* ksp = nullptr;
+  ncclResult_t r = checkOp(datatype, op, &ksp);
+  if (r != ncclSuccess) return r;
+  const KernelSet& ks = *ksp;
+  // every bucket is checked before anything is enqueued
+  for (int i = 0; i < nTasks; i++) {
+    r = checkBucket(ks, tasks[i].dsts, tasks[i].nDsts, tasks[i].srcs, tasks[i].nSrcs, tasks[i].count);
+    if (r != ncclSuccess) return r;
+  }
+  if (nPreOpSrcs < 0) nPreOpSrcs = 0;
+  const bool pre = op.op == nbxDevPreMulSum;
+  const int post = (op.op == nbxDevSumPostDiv && postOp) ? 1 : 0;
+  const int acq = (flags & nbx::kReduceAcquireSystem) ? 1 : 0;
+  hipStream_t st = (hipStream_t)stream;
+  // buckets with <= 8 sources and one shared alignment go into batches per
+  // source count, in order; the rest (mixed alignment, > 8 sources) take the
+  // single-bucket path, and so do buckets of 4+ sources big enough to give
+  // every CU a big tile on their own (they fill the GPU alone, at the big
+  // tile's higher rate; 1-3 sources use the batch kernel's tile shape anyway). Launch variant 1 (force small tiles) batches those too; variant 2
+  // (force big tiles) batches nothing.
+  const int force = g_variant.load(std::memory_order_relaxed);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const uint64_t cus = (uint64_t)cuCount(dev);
+  std::unique_ptr<BatchPacker> packers[kMaxKSrcs];
+  for (int i = 0; i < nTasks; i++) {
+    const nbxReduceTask& t = tasks[i];
+    if (t.count == 0) continue;
+    bool single = force == 2 || t.nSrcs > kMaxKSrcs || t.count > kBatchCountMask ||
+                  sharedMisalignment(t.dsts, t.nDsts, t.srcs, t.nSrcs) < 0;
+    if (!single && force == 0 && t.nSrcs > 3) {
+      const uint64_t bigTile = (uint64_t)ks.unroll[t.nSrcs - 1] * kBlock;
+      single = t.count / (uint64_t)(16 / ks.eltBytes) >= bigTile * cus;
+    }
+    if (single) {
+      r = reduceMultiImpl(t.dsts, t.nDsts, t.srcs, t.nSrcs, t.count, datatype, op, nPreOpSrcs, postOp, stream,
+                          flags);
+      if (r != ncclSuccess) return r;
+      continue;
+    }
+    std::unique_ptr<BatchPacker>& pk = packers[t.nSrcs - 1];
+    if (!pk) {
+      uint32_t mask = 0;
+      if (pre)
+        for (int s = 0; s < t.nSrcs; s++)
+          if (s < nPreOpSrcs) mask |= 1u << s;
+      pk.reset(new BatchPacker(ks, t.nSrcs, op, mask, post, acq, st));
+    }
+    r = pk->add(t);
+    if (r != ncclSuccess) return r;
+  }
+  for (int q = 0; q < kMaxKSrcs; q++) {
+    if (!packers[q]) continue;
+    r = packers[q]->flush();
+    if (r != ncclSuccess) return r;
+  }
+  return ncclSuccess;
+}
 }  // namespace
 
 }  // extern "C"
@@ -397,6 +568,13 @@ __attribute__((visibility("default"))) ncclResult_t nbxReduceMulti(void* const* 
                                                                     ncclDataType_t datatype, nbxDevRedOpFull op,
                                                                     int nPreOpSrcs, int postOp, ncclStream_t stream) {
   return reduceMultiImpl(dsts, nDsts, srcs, nSrcs, count, datatype, op, nPreOpSrcs, postOp, stream, 0);
+}
+
+__attribute__((visibility("default"))) ncclResult_t nbxReduceMultiBatch(const nbxReduceTask* tasks, int nTasks,
+                                                                         ncclDataType_t datatype, nbxDevRedOpFull op,
+                                                                         int nPreOpSrcs, int postOp,
+                                                                         ncclStream_t stream) {
+  return reduceMultiBatchImpl(tasks, nTasks, datatype, op, nPreOpSrcs, postOp, stream, 0);
 }
 
 __attribute__((visibility("default"))) ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int variant) {

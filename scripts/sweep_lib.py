@@ -6,10 +6,13 @@ GPU box. Not the bench: feeds DESIGN.md and the launch-default choice.
   sweep   config C: fp16 / bf16 (and fp32, fp8) sum, nSrcs in {2, 8}, 1..64 MiB per input
   e2e     host-staged path: pinned host -> hipMemcpy H2D -> reduce -> D2H (BASELINE asks for it)
   small   latency of small buckets (4 KiB .. 1 MiB), nSrcs 2
+  tiles   single-bucket tile choice: auto / small (U=1, 8 per CU) / big per nSrcs, dtype, size
+  batch   config C bucket sets through nbxReduceMultiBatch vs one nbxReduceMulti per bucket
 
 Prints one JSON object per line.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -39,6 +42,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="knobs,pipe,sweep,e2e,small")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--tiles-nsrc", type=lambda v: [int(x) for x in v.split(",")], default=[1, 2, 3, 4, 6, 8])
+    ap.add_argument("--tiles-settings", default="0:0,0:1,4:1,0:2,2:2", help="blocksPerCU:variant,...")
     args = ap.parse_args()
     import torch
     from __graft_entry__ import _load_package
@@ -147,6 +152,95 @@ def main():
                               "pipelined_host_ms": round(pms, 4), "pipelined_host_alg_GBps": round(gbps(alg, pms), 1),
                               "pcie_bytes": alg}), flush=True)
             del hs, ho, ds, do
+
+    if "tiles" in what:
+        for dt, name, tdt in ((6, "fp16", torch.float16), (7, "fp32", torch.float32)):
+            for nsrc in args.tiles_nsrc:
+                for mib in (4, 16, 64, 256):
+                    if nsrc * mib > 2048:
+                        continue
+                    esz = torch.tensor([], dtype=tdt).element_size()
+                    n = (mib << 20) // esz
+                    srcs = [torch.rand(n, device="cuda").to(tdt) for _ in range(nsrc)]
+                    out = torch.empty_like(srcs[0])
+                    sp = [t.data_ptr() for t in srcs]
+                    op = op_for(dt)
+                    settings = [tuple(int(v) for v in x.split(":")) for x in args.tiles_settings.split(",")]
+                    res = {x: [] for x in settings}
+                    for _ in range(args.rounds):
+                        for x in settings:
+                            nbx.set_launch_config(*x)
+                            res[x].append(timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, dt, op, 0,
+                                                                                False, st), 10))
+                    nbx.set_launch_config(0, 0)
+                    alg = (nsrc + 1) * n * esz
+                    row = {"what": "tiles", "dtype": name, "nsrc": nsrc, "MiB_per_input": mib}
+                    for x, v in res.items():
+                        v.sort()
+                        row[f"bpc{x[0]}_v{x[1]}_GBps"] = round(gbps(alg, v[len(v) // 2]), 1)
+                    print(json.dumps(row), flush=True)
+                    del srcs, out
+
+    if "batch" in what:
+        # bucket sets (MiB per input): 16 x 1 MiB, 64 x 256 KiB, the mixed 1..64 MiB sweep
+        sets = {"16x1MiB": [1 << 20] * 16, "64x256KiB": [256 << 10] * 64, "128x64KiB": [64 << 10] * 128,
+                "mixed_1_64MiB": [m << 20 for m in (1, 2, 4, 8, 16, 32, 64)]}
+        for dt, name, tdt in ((6, "fp16", torch.float16), (9, "bf16", torch.bfloat16)):
+            for nsrc in (2, 8):
+                for sname, sizes in sets.items():
+                    bufs = []
+                    for b in sizes:
+                        n = b // 2
+                        srcs = [torch.rand(n, device="cuda").to(tdt) for _ in range(nsrc)]
+                        bufs.append((srcs, torch.empty_like(srcs[0]), n))
+                    calls = [([o.data_ptr()], [t.data_ptr() for t in ss], n) for ss, o, n in bufs]
+                    alg = sum((nsrc + 1) * b for b in sizes)
+                    op = op_for(dt)
+                    iters = max(5, min(100, (2 << 30) // alg))
+                    lib = nbx.load_library()
+                    keep = []
+                    tasks = (nbx.ReduceTask * len(calls))()
+                    singles = []
+                    for i, (d, s_, n) in enumerate(calls):
+                        da = (ctypes.c_void_p * 1)(*d)
+                        sa = (ctypes.c_void_p * nsrc)(*s_)
+                        keep += [da, sa]
+                        tasks[i] = nbx.ReduceTask(da, 1, sa, nsrc, n)
+                        singles.append((da, sa, n))
+
+                    def enqueue(mode, stream):
+                        # raw ctypes calls on prebuilt arrays: the GPU time, not Python's
+                        if mode == "single":
+                            for da, sa, n in singles:
+                                lib.nbxReduceMulti(da, 1, sa, nsrc, n, dt, op, 0, 0, ctypes.c_void_p(stream))
+                        else:
+                            lib.nbxReduceMultiBatch(tasks, len(calls), dt, op, 0, 0, ctypes.c_void_p(stream))
+
+                    res = {}
+                    for mode in ("single", "batch_auto", "batch_all"):
+                        nbx.set_launch_config(0, 1 if mode == "batch_all" else 0)
+                        # eager (host launch rate included) and graph-replayed (device time)
+                        t = [timed(torch, lambda: enqueue(mode, st), iters) for _ in range(args.rounds)]
+                        g = torch.cuda.CUDAGraph()
+                        cs = torch.cuda.Stream()
+                        with torch.cuda.stream(cs):
+                            enqueue(mode, cs.cuda_stream)
+                            torch.cuda.synchronize()
+                            with torch.cuda.graph(g, stream=cs):
+                                for _ in range(10):
+                                    enqueue(mode, cs.cuda_stream)
+                        tg = [timed(torch, g.replay, max(1, iters // 10)) / 10 for _ in range(args.rounds)]
+                        nbx.set_launch_config(0, 0)
+                        t.sort()
+                        tg.sort()
+                        res[mode] = t[len(t) // 2]
+                        res[mode + "_graph"] = tg[len(tg) // 2]
+                        del g
+                    print(json.dumps({"what": "batch", "dtype": name, "nsrc": nsrc, "set": sname,
+                                      "n_buckets": len(sizes), "alg_bytes": alg,
+                                      **{f"{m}_ms": round(v, 4) for m, v in res.items()},
+                                      **{f"{m}_GBps": round(gbps(alg, v), 1) for m, v in res.items()}}), flush=True)
+                    del bufs
 
     if "small" in what:
         for kib in (4, 16, 64, 256, 1024):

@@ -112,6 +112,28 @@ def test_reduce_multi_argument_checks_before_device(nbx):
     assert nbx.reduce_multi_raw([0], [fake], 16, 7, op) == E         # NULL
 
 
+def test_reduce_multi_batch_argument_checks_before_device(nbx):
+    """nbxReduceMultiBatch checks every bucket before enqueuing anything."""
+    op = nbx.DevRedOpFull()
+    E = 4
+    fake = 0x10000
+    good = ([fake + 64], [fake, fake + 128], 16)
+    assert nbx.reduce_multi_batch_raw([], 7, op) == 0                          # no buckets: no-op
+    assert nbx.reduce_multi_batch_raw([([fake], [fake], 0)] * 3, 7, op) == 0   # empty buckets: no-op
+    assert nbx.reduce_multi_batch_raw([good, ([fake], [], 16)], 7, op) == E    # a bucket with no source
+    assert nbx.reduce_multi_batch_raw([good, ([], [fake], 16)], 7, op) == E    # ... no destination
+    assert nbx.reduce_multi_batch_raw([good, ([fake], [fake] * 65, 16)], 7, op) == E
+    assert nbx.reduce_multi_batch_raw([good, ([fake], [fake + 2], 16)], 7, op) == E   # misaligned element
+    assert nbx.reduce_multi_batch_raw([good, ([0], [fake], 16)], 7, op) == E   # NULL destination
+    assert nbx.reduce_multi_batch_raw([good], -1, op) == E
+    op.op = 4
+    op.scalarArg = 2
+    assert nbx.reduce_multi_batch_raw([good], 7, op) == E                      # SumPostDiv on floats
+    lib = nbx.load_library()
+    assert lib.nbxReduceMultiBatch(None, 2, 7, nbx.DevRedOpFull(), 0, 0, None) == E
+    assert lib.nbxReduceMultiBatch(None, -1, 7, nbx.DevRedOpFull(), 0, 0, None) == E
+
+
 def test_comm_api_errors_without_device(nbx):
     lib = nbx.load_library()
     uid = nbx.get_unique_id()

@@ -219,6 +219,90 @@ def test_in_place(nbx, oracle, torch_gpu):
     assert_same(ts[0].cpu().numpy(), exp, 7)
 
 
+def run_batch(nbx, oracle, torch, dtype, devop, arg, buckets, npre=0, post=False):
+    """nbxReduceMultiBatch over buckets [(nsrc, ndst, count, src_off, dst_off, seed)], each
+    checked bit-exact against the oracle's single-bucket fold, guard bytes untouched."""
+    dev = Dev(torch)
+    st = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st).itemsize
+    calls, cases = [], []
+    for nsrc, ndst, count, so, do, seed in buckets:
+        srcs = oracle.random_inputs(dtype, nsrc, count, seed=seed)
+        sp = [dev.upload(x, so) for x in srcs]
+        outs = [dev.alloc(count * eb, do) for _ in range(ndst)]
+        calls.append(([p for _, p in outs], sp, count))
+        cases.append((srcs, outs, do, count))
+    op = nbx.DevRedOpFull()
+    op.op = devop
+    op.scalarArg = arg
+    nbx.reduce_multi_batch(calls, dtype, op, npre, post, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for srcs, outs, do, count in cases:
+        exp = oracle.reduce_multi(srcs, dtype, devop, arg, npre, post, n_dsts=1, threads=8)[0]
+        for t, _ in outs:
+            assert_same(Dev.download(t, do, count * eb, st), exp, dtype)
+            assert (t[do + count * eb:].cpu().numpy() == 0xA5).all() and (t[:do].cpu().numpy() == 0xA5).all()
+
+
+@pytest.mark.parametrize("dtype", ALL_TYPES)
+def test_batch_all_types_ops(nbx, oracle, torch_gpu, dtype):
+    """Batched buckets: every op, ragged sizes (below one pack, one tile +- 1,
+    several tiles), 1-8 sources and 1-3 destinations in one call."""
+    rng = np.random.default_rng(dtype)
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    epp = 16 // eb
+    for devop in devops_for(dtype):
+        arg = op_arg(oracle, dtype, devop, rng)
+        buckets = []
+        for i, count in enumerate([1, epp - 1, epp, 256 * epp - 1, 256 * epp + 1, 3001, 70001]):
+            nsrc = 1 + (i + devop) % 8
+            buckets.append((nsrc, 1 + i % 3, count, 0, 0, 100 * dtype + 10 * devop + i))
+        run_batch(nbx, oracle, torch_gpu, dtype, devop, arg, buckets, npre=2 if devop == 3 else 0,
+                  post=devop == 4)
+
+
+@pytest.mark.parametrize("dtype", [6, 9, 7, 4])
+def test_batch_many_buckets_and_alignments(nbx, oracle, torch_gpu, dtype):
+    """More buckets than one launch holds (> 16 per source count), shared
+    misalignments (head elements), mixed alignments and > 8 sources (the
+    single-bucket fallbacks) in one call."""
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    rng = np.random.default_rng(7)
+    buckets = []
+    for i in range(40):
+        nsrc = 8 if i < 20 else int(rng.integers(1, 9))
+        off = int(rng.integers(0, 16 // eb)) * eb
+        buckets.append((nsrc, 1 + i % 2, int(rng.integers(1, 40000)), off, off, 1000 + i))
+    buckets.append((3, 1, 5000, 0, eb % 16 if eb < 16 else 0, 77))   # mixed alignment
+    buckets.append((12, 2, 9000, 0, 0, 78))                           # multi-pass
+    run_batch(nbx, oracle, torch_gpu, dtype, 0, 0, buckets)
+
+
+def test_batch_table_overflow(nbx, oracle, torch_gpu):
+    """More buckets than one kernel-argument table holds (101 two-source or 28
+    eight-source/eight-destination records): the table is launched when full
+    and packing resumes."""
+    rng = np.random.default_rng(11)
+    buckets = [(2, 1, int(rng.integers(1, 3000)), 0, 0, 2000 + i) for i in range(150)]
+    buckets += [(8, 8, int(rng.integers(1, 3000)), 4, 4, 3000 + i) for i in range(35)]
+    run_batch(nbx, oracle, torch_gpu, 7, 0, 0, buckets)
+    run_batch(nbx, oracle, torch_gpu, 2, 4, 3, buckets[140:160], post=True)
+
+
+def test_batch_mixed_bucket_sweep_fp16_bf16(nbx, oracle, torch_gpu):
+    """Config C shape: 8-source fp16 and bf16 sums over 1..16 MiB buckets in one
+    batch — by default the buckets that fill the GPU alone take the big-tile
+    single-bucket kernel; launch variant 1 puts every bucket in the batch kernel."""
+    try:
+        for variant in (0, 1):
+            nbx.set_launch_config(0, variant)
+            for dtype in (6, 9):
+                buckets = [(8, 1, (mib << 20) // 2, 0, 0, mib + variant) for mib in (1, 2, 4, 8, 16)]
+                run_batch(nbx, oracle, torch_gpu, dtype, 0, 0, buckets)
+    finally:
+        nbx.set_launch_config(0, 0)
+
+
 def test_invalid_arguments(nbx, torch_gpu):
     torch = torch_gpu
     a = torch.zeros(64, device="cuda")
