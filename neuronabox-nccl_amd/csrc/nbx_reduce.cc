@@ -78,13 +78,20 @@ int cuCount(int dev) {
 // tiles (one pack per lane per source): 5 / 4 / 3 workgroups per CU for 1 / 2
 // / 3 sources, 4 above — measured on MI355X (profiles/r1/tiles_sweep_r1n.jsonl:
 // 2 sources at 256 MiB 6.80 TB/s with 4 per CU vs 6.12 with 8 and 5.91 with
-// one big-tile workgroup; 3 sources 6.58 vs 6.38 big-tile).
-int maxBlocksPerCU(bool big, int loadsPerLane) {
+// one big-tile workgroup; 3 sources 6.58 vs 6.38 big-tile). classic = true
+// keeps 8 small workgroups per CU: the element kernel, and passes that read
+// peer GPUs' memory (the collectives' direct and ring schedules) — xGMI
+// latency wants more bytes in flight, and the local-HBM measurement does not
+// carry over (no multi-GPU box to measure it on).
+int maxBlocksPerCU(bool big, int loadsPerLane, bool classic = false) {
   int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
   if (v > 0) return v;
   static const int envBig = envInt("NBX_BLOCKS_PER_CU", 0);
   if (envBig > 0) return envBig;
-  if (!big) return loadsPerLane <= 1 ? 5 : loadsPerLane == 2 ? 4 : loadsPerLane == 3 ? 3 : 4;
+  if (!big) {
+    if (classic) return 8;
+    return loadsPerLane <= 1 ? 5 : loadsPerLane == 2 ? 4 : loadsPerLane == 3 ? 3 : 4;
+  }
   int b = (32 + loadsPerLane - 1) / loadsPerLane;
   return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
@@ -152,10 +159,11 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     const size_t bigTile = (size_t)ks.unroll[nSrcs - 1] * kBlock;
     const size_t bigTiles = (nPacks + bigTile - 1) / bigTile;
     const int force = g_variant.load(std::memory_order_relaxed);
-    const bool big = force == 2 || (force == 0 && nSrcs > 3 && bigTiles >= (size_t)cus);
+    const bool big = force == 2 || (force == 0 && (nSrcs > 3 || acquireSystem) && bigTiles >= (size_t)cus);
     const size_t tile = big ? bigTile : (size_t)kBlock;
     const size_t tiles = (nPacks + tile - 1) / tile;
-    const size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(big, nSrcs * (big ? ks.unroll[nSrcs - 1] : 1));
+    const size_t maxBlocks =
+        (size_t)cus * (size_t)maxBlocksPerCU(big, nSrcs * (big ? ks.unroll[nSrcs - 1] : 1), acquireSystem != 0);
     size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
     if (grid == 0) grid = 1;
     a.variant = big ? 1 : 0;
@@ -163,7 +171,7 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
                           0, stream);
   } else {
     size_t blocks = (count + kBlock - 1) / kBlock;
-    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs);
+    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs, /*classic=*/true);
     size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
     err = hipLaunchKernel((const void*)ks.elts, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
   }
@@ -475,7 +483,8 @@ struct BatchPacker {
     a.acquireSystem = acquireSystem;
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const uint64_t maxBlocks = (uint64_t)cuCount(dev) * (uint64_t)maxBlocksPerCU(false, nSrcs);
+    const uint64_t maxBlocks =
+        (uint64_t)cuCount(dev) * (uint64_t)maxBlocksPerCU(false, nSrcs, acquireSystem != 0);
     const uint64_t grid = a.totalTiles < maxBlocks ? a.totalTiles : maxBlocks;
     void* args[] = {&a};
     hipError_t err = hipLaunchKernel(ks.batch[nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
@@ -521,7 +530,7 @@ ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDa
     if (t.count == 0) continue;
     bool single = force == 2 || t.nSrcs > kMaxKSrcs || t.count > kBatchCountMask ||
                   sharedMisalignment(t.dsts, t.nDsts, t.srcs, t.nSrcs) < 0;
-    if (!single && force == 0 && t.nSrcs > 3) {
+    if (!single && force == 0 && (t.nSrcs > 3 || acq)) {
       const uint64_t bigTile = (uint64_t)ks.unroll[t.nSrcs - 1] * kBlock;
       single = t.count / (uint64_t)(16 / ks.eltBytes) >= bigTile * cus;
     }
