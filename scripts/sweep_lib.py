@@ -111,7 +111,9 @@ def main():
                     sp = [t.data_ptr() for t in srcs]
                     op = op_for(dt)
                     iters = max(5, min(200, (256 << 20) // (mib << 20) * 4))
-                    ms = timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, dt, op, 0, False, st), iters)
+                    ts = sorted(timed(torch, lambda: nbx.reduce_multi([out.data_ptr()], sp, n, dt, op, 0, False, st),
+                                      iters) for _ in range(args.rounds))
+                    ms = ts[len(ts) // 2]   # median of rounds
                     print(json.dumps({"what": "sweep", "dtype": name, "nsrc": nsrc, "MiB_per_input": mib,
                                       "ms": round(ms, 5), "GBps": round(gbps((nsrc + 1) * n * esz, ms), 1)}),
                           flush=True)
