@@ -13,6 +13,9 @@ constexpr int kReduceAcquireSystem = 1;
 ncclResult_t reduceMultiEx(void* const* dsts, int nDsts, const void* const* srcs, int nSrcs, size_t count,
                            ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
                            ncclStream_t stream, int flags);
+// nbxReduceMultiBatch with the same internal flags.
+ncclResult_t reduceMultiBatchEx(const nbxReduceTask* tasks, int nTasks, ncclDataType_t datatype, nbxDevRedOpFull op,
+                                int nPreOpSrcs, int postOp, ncclStream_t stream, int flags);
 // Launch the LL collective kernel of (datatype, op) (nbx_ll.h); sequencing is
 // device-resident (args.state).
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);

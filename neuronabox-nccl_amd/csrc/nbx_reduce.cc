@@ -185,6 +185,13 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
 }  // namespace
 
 namespace nbx {
+// Workgroup cap of the LL-family kernels from an env knob, clamped to [1, 1024].
+size_t gridCapFromEnv(const char* name, long dflt) {
+  const char* v = std::getenv(name);
+  long g = (v && *v) ? std::atol(v) : dflt;
+  return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
+}
+
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
@@ -194,11 +201,7 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
   // one 8-byte pack per thread; NBX_LL_MAX_GRID caps the workgroups (default
   // 1024), e.g. when several ranks share one GPU and every rank's grid must
   // stay co-resident for the ranks' spinning blocks to make progress
-  static const size_t maxGrid = [] {
-    const char* v = std::getenv("NBX_LL_MAX_GRID");
-    long g = (v && *v) ? std::atol(v) : 1024;
-    return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
-  }();
+  static const size_t maxGrid = gridCapFromEnv("NBX_LL_MAX_GRID", 1024);
   size_t grid = (a.nPacks + 255) / 256;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
@@ -218,11 +221,7 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   // CU by default (every block of the grid co-resident on its GPU, so a block
   // waiting for its peers' lines never holds back a block they wait for).
   // NBX_LL128_MAX_GRID lowers the cap, e.g. when several ranks share one GPU.
-  static const size_t maxGrid = [] {
-    const char* v = std::getenv("NBX_LL128_MAX_GRID");
-    long g = (v && *v) ? std::atol(v) : 256;
-    return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
-  }();
+  static const size_t maxGrid = gridCapFromEnv("NBX_LL128_MAX_GRID", 256);
   const size_t linesPerBlock = 256 / kL128LanesHost;
   size_t grid = (a.nLines + linesPerBlock - 1) / linesPerBlock;
   if (grid < 1) grid = 1;
@@ -240,11 +239,7 @@ ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op,
   if (!ks.valid || ks.ll128x2 == nullptr) return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
-  static const size_t maxGrid = [] {   // as launchLL128Coll
-    const char* v = std::getenv("NBX_LL128_MAX_GRID");
-    long g = (v && *v) ? std::atol(v) : 256;
-    return (size_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
-  }();
+  static const size_t maxGrid = gridCapFromEnv("NBX_LL128_MAX_GRID", 256);
   const size_t linesPerBlock = 256 / kL128LanesHost;
   size_t grid = (blockLines + linesPerBlock - 1) / linesPerBlock;
   if (grid < 1) grid = 1;
@@ -567,6 +562,10 @@ ncclResult_t reduceMultiEx(void* const* dsts, int nDsts, const void* const* srcs
                            ncclDataType_t datatype, nbxDevRedOpFull op, int nPreOpSrcs, int postOp,
                            ncclStream_t stream, int flags) {
   return reduceMultiImpl(dsts, nDsts, srcs, nSrcs, count, datatype, op, nPreOpSrcs, postOp, stream, flags);
+}
+ncclResult_t reduceMultiBatchEx(const nbxReduceTask* tasks, int nTasks, ncclDataType_t datatype, nbxDevRedOpFull op,
+                                int nPreOpSrcs, int postOp, ncclStream_t stream, int flags) {
+  return reduceMultiBatchImpl(tasks, nTasks, datatype, op, nPreOpSrcs, postOp, stream, flags);
 }
 }  // namespace nbx
 

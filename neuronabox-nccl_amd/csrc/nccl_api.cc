@@ -345,16 +345,61 @@ void blockRange(size_t count, int eb, int n, int b, size_t* off, size_t* len) {
   *len = hi - lo;
 }
 
+// Every rank of the clique enqueued the same collective.
+bool sameCollective(const std::vector<PendingColl>& parts) {
+  const PendingColl& p0 = parts[0];
+  for (size_t r = 1; r < parts.size(); r++)
+    if (parts[r].kind != p0.kind || parts[r].count != p0.count || parts[r].dt != p0.dt ||
+        parts[r].root != p0.root || parts[r].op.op != p0.op.op)
+      return false;
+  return true;
+}
+
+// Rank r's share of one clique collective: block r of every send buffer, in
+// fold order, and where the folded block goes.
+struct CliqueBlock {
+  std::vector<const void*> srcs;
+  std::vector<void*> dsts;
+  size_t len = 0;
+};
+
+CliqueBlock cliqueBlock(const std::vector<PendingColl>& parts, int n, int r) {
+  const PendingColl& p0 = parts[0];
+  const int eb = typeSize(p0.dt);
+  const size_t total = p0.kind == kReduceScatter ? p0.count * (size_t)n : p0.count;
+  CliqueBlock cb;
+  size_t off;
+  if (p0.kind == kReduceScatter) {
+    off = (size_t)r * p0.count;
+    cb.len = p0.count;
+  } else {
+    blockRange(total, eb, n, r, &off, &cb.len);
+  }
+  if (cb.len == 0) return cb;
+  // fold order: AllReduce / ReduceScatter block r as NCCL's ring accumulates it
+  // (r+1, ..., r); Reduce as NCCL's chain toward the root (root+1, ..., root,
+  // reduce.h:44-67) for every block.
+  const int first = (p0.kind == kReduce ? p0.root : r) + 1;
+  cb.srcs.resize(n);
+  for (int k = 0; k < n; k++) cb.srcs[k] = (const char*)parts[(first + k) % n].send + off * (size_t)eb;
+  // AllReduce with n <= NBX_MAX_DSTS: push-gather — the fold stores block r
+  // into every rank's output at once (all peer links busy in one kernel,
+  // the CollNet-direct scatter shape, all_reduce.h:343-360)
+  if (p0.kind == kReduceScatter) cb.dsts.push_back(parts[r].recv);
+  else if (p0.kind == kReduce) cb.dsts.push_back((char*)parts[p0.root].recv + off * (size_t)eb);
+  else if (n > NBX_MAX_DSTS) cb.dsts.push_back((char*)parts[r].recv + off * (size_t)eb);
+  else
+    for (int k = 0; k < n; k++) cb.dsts.push_back((char*)parts[(r + k) % n].recv + off * (size_t)eb);
+  return cb;
+}
+
 // Run one collective across every rank of an in-process clique.
 ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   const int n = c->n;
   const PendingColl& p0 = parts[0];
-  for (int r = 1; r < n; r++) {
-    if (parts[r].kind != p0.kind || parts[r].count != p0.count || parts[r].dt != p0.dt ||
-        parts[r].root != p0.root || parts[r].op.op != p0.op.op) {
-      warn("collective mismatch across ranks of the clique");
-      return ncclInvalidUsage;
-    }
+  if (!sameCollective(parts)) {
+    warn("collective mismatch across ranks of the clique");
+    return ncclInvalidUsage;
   }
   const int eb = typeSize(p0.dt);
   NBX_TRACE("clique coll kind=%d n=%d count=%zu dt=%d op=%d", (int)p0.kind, n, p0.count, (int)p0.dt, p0.op.op);
@@ -369,42 +414,18 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
       if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evEnter[j], 0));
   }
   NBX_TRACE("clique enter events done");
-  // 2. reduce: rank r folds block r of every send buffer in ring order r+1..r
+  // 2. reduce: rank r folds block r of every send buffer (postOp here: the fold
+  //    is complete in one pass)
   const size_t total = p0.kind == kReduceScatter ? p0.count * (size_t)n : p0.count;
-  const int postOp = 1;   // the fold is complete in one pass: apply SumPostDiv here
   const bool push = n <= NBX_MAX_DSTS;
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
-    size_t off, len;
-    if (p0.kind == kReduceScatter) {
-      off = (size_t)r * p0.count;
-      len = p0.count;
-    } else {
-      blockRange(total, eb, n, r, &off, &len);
-    }
-    if (len == 0) continue;
-    // fold order: AllReduce / ReduceScatter block r as NCCL's ring accumulates it
-    // (r+1, ..., r); Reduce as NCCL's chain toward the root (root+1, ..., root,
-    // reduce.h:44-67) for every block.
-    const int first = (p0.kind == kReduce ? p0.root : r) + 1;
-    std::vector<const void*> srcs(n);
-    for (int k = 0; k < n; k++) {
-      int j = (first + k) % n;
-      srcs[k] = (const char*)parts[j].send + off * (size_t)eb;
-    }
-    // AllReduce with n <= NBX_MAX_DSTS: push-gather — the fold stores block r
-    // into every rank's output at once (all peer links busy in one kernel,
-    // the CollNet-direct scatter shape, all_reduce.h:343-360)
-    std::vector<void*> dsts;
-    if (p0.kind == kReduceScatter) dsts.push_back(parts[r].recv);
-    else if (p0.kind == kReduce) dsts.push_back((char*)parts[p0.root].recv + off * (size_t)eb);
-    else if (!push) dsts.push_back((char*)parts[r].recv + off * (size_t)eb);
-    else
-      for (int k = 0; k < n; k++) dsts.push_back((char*)parts[(r + k) % n].recv + off * (size_t)eb);
-    nbxDevRedOpFull op = parts[r].op;
-    NBX_TRACE("clique reduce rank %d off=%zu len=%zu dst=%p src0=%p", r, off, len, dsts[0], srcs[0]);
-    NCCLCHECK(nbx::reduceMultiEx(dsts.data(), (int)dsts.size(), srcs.data(), n, len, p0.dt, op, /*nPreOpSrcs=*/n,
-                                 postOp, (ncclStream_t)parts[r].stream, nbx::kReduceAcquireSystem));
+    CliqueBlock cb = cliqueBlock(parts, n, r);
+    if (cb.len == 0) continue;
+    NBX_TRACE("clique reduce rank %d len=%zu dst=%p src0=%p", r, cb.len, cb.dsts[0], cb.srcs[0]);
+    NCCLCHECK(nbx::reduceMultiEx(cb.dsts.data(), (int)cb.dsts.size(), cb.srcs.data(), n, cb.len, p0.dt, parts[r].op,
+                                 /*nPreOpSrcs=*/n, /*postOp=*/1, (ncclStream_t)parts[r].stream,
+                                 nbx::kReduceAcquireSystem));
   }
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
@@ -447,6 +468,124 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   return ncclSuccess;
 }
 
+// Byte ranges one clique collective reads and writes (every rank's buffers).
+struct Span {
+  uintptr_t lo, hi;
+  bool write;
+};
+
+void collSpans(const std::vector<PendingColl>& parts, std::vector<Span>* out) {
+  const size_t n = parts.size();
+  for (const PendingColl& p : parts) {
+    const size_t eb = (size_t)typeSize(p.dt);
+    const size_t sendBytes = (p.kind == kReduceScatter ? p.count * n : p.count) * eb;
+    const size_t recvBytes = p.count * eb;
+    out->push_back({(uintptr_t)p.send, (uintptr_t)p.send + sendBytes, false});
+    if (p.recv != nullptr) out->push_back({(uintptr_t)p.recv, (uintptr_t)p.recv + recvBytes, true});
+  }
+}
+
+bool spansConflict(const std::vector<Span>& a, const std::vector<Span>& b) {
+  for (const Span& x : a)
+    for (const Span& y : b)
+      if ((x.write || y.write) && x.lo < y.hi && y.lo < x.hi) return true;
+  return false;
+}
+
+// Several collectives of one group as ONE exchange: a single enter / leave
+// event exchange, and per rank one batched launch (nbxReduceMultiBatch) for
+// the blocks of every collective — NCCL likewise packs a group's collectives
+// into one kernel's work list (enqueue.cc:67-91 appendWorkElemColl). Only
+// for independent collectives on one stream per rank that need no gather step.
+ncclResult_t runCliqueBatch(Clique* c, const std::vector<std::vector<PendingColl>>& rounds, size_t lo, size_t hi) {
+  const int n = c->n;
+  NBX_TRACE("clique batch of %zu collectives", hi - lo);
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    HIPCHECK(hipEventRecord(c->evEnter[r], rounds[lo][r].stream));
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    for (int j = 0; j < n; j++)
+      if (j != r) HIPCHECK(hipStreamWaitEvent(rounds[lo][r].stream, c->evEnter[j], 0));
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    std::vector<CliqueBlock> blocks;
+    blocks.reserve(hi - lo);
+    std::vector<size_t> which;
+    for (size_t k = lo; k < hi; k++) {
+      blocks.push_back(cliqueBlock(rounds[k], n, r));
+      which.push_back(k);
+    }
+    // one batched call per (datatype, op) run of consecutive collectives
+    size_t i = 0;
+    while (i < blocks.size()) {
+      const PendingColl& pi = rounds[which[i]][r];
+      std::vector<nbxReduceTask> tasks;
+      size_t j = i;
+      for (; j < blocks.size(); j++) {
+        const PendingColl& pj = rounds[which[j]][r];
+        if (pj.dt != pi.dt || pj.op.op != pi.op.op || pj.op.scalarArg != pi.op.scalarArg ||
+            pj.op.scalarArgIsPtr != pi.op.scalarArgIsPtr)
+          break;
+        const CliqueBlock& cb = blocks[j];
+        if (cb.len == 0) continue;
+        tasks.push_back({cb.dsts.data(), (int)cb.dsts.size(), cb.srcs.data(), n, cb.len});
+      }
+      NCCLCHECK(nbx::reduceMultiBatchEx(tasks.data(), (int)tasks.size(), pi.dt, pi.op, /*nPreOpSrcs=*/n,
+                                        /*postOp=*/1, (ncclStream_t)pi.stream, nbx::kReduceAcquireSystem));
+      i = j;
+    }
+    HIPCHECK(hipEventRecord(c->evDone[r], rounds[lo][r].stream));
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(c->devs[r]);
+    for (int j = 0; j < n; j++)
+      if (j != r) HIPCHECK(hipStreamWaitEvent(rounds[lo][r].stream, c->evDone[j], 0));
+  }
+  return ncclSuccess;
+}
+
+// Run a group's queued collectives in order: maximal runs of batchable ones
+// (same collective on every rank, same per-rank streams, no gather step, no
+// buffer dependency on an earlier member of the run, at most kMaxCliqueBatch)
+// as one batch, the rest one by one.
+constexpr size_t kMaxCliqueBatch = 64;
+
+ncclResult_t runCliqueRounds(Clique* c, const std::vector<std::vector<PendingColl>>& rounds) {
+  const int n = c->n;
+  auto batchable = [&](const std::vector<PendingColl>& parts) {
+    return sameCollective(parts) && !(parts[0].kind == kAllReduce && n > NBX_MAX_DSTS);
+  };
+  size_t i = 0;
+  while (i < rounds.size()) {
+    size_t j = i;
+    std::vector<Span> spans;
+    if (batchable(rounds[i])) {
+      collSpans(rounds[i], &spans);
+      for (j = i + 1; j < rounds.size() && j - i < kMaxCliqueBatch; j++) {
+        if (!batchable(rounds[j])) break;
+        bool sameStreams = true;
+        for (int r = 0; r < n; r++) sameStreams &= rounds[j][r].stream == rounds[i][r].stream;
+        if (!sameStreams) break;
+        std::vector<Span> sj;
+        collSpans(rounds[j], &sj);
+        if (spansConflict(spans, sj)) break;
+        spans.insert(spans.end(), sj.begin(), sj.end());
+      }
+    }
+    if (j <= i + 1) {
+      NCCLCHECK(runCliqueColl(c, rounds[i]));
+      i++;
+    } else {
+      NCCLCHECK(runCliqueBatch(c, rounds, i, j));
+      i = j;
+    }
+  }
+  return ncclSuccess;
+}
+
 // Launch every complete collective queued for every clique (called when the
 // outermost group ends, or immediately outside a group).
 ncclResult_t flushPendingImpl();
@@ -470,6 +609,7 @@ ncclResult_t flushPendingImpl() {
       continue;
     }
     auto& pr = c->pending;
+    std::vector<std::vector<PendingColl>> rounds;
     for (;;) {
       bool ready = true;
       for (int r = 0; r < c->n; r++) ready &= !pr[r].empty();
@@ -480,8 +620,9 @@ ncclResult_t flushPendingImpl() {
         parts.push_back(pr[r].front());
         pr[r].pop_front();
       }
-      NCCLCHECK(runCliqueColl(c.get(), parts));
+      rounds.push_back(std::move(parts));
     }
+    NCCLCHECK(runCliqueRounds(c.get(), rounds));
     i++;
   }
   return ncclSuccess;

@@ -212,6 +212,60 @@ def test_clique_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, nranks):
             c.destroy()
 
 
+@pytest.mark.parametrize("nranks", [2, 3, 9])
+def test_clique_grouped_collectives_batched(nbx, oracle, torch_gpu, nranks):
+    """A group of independent collectives runs as one batched exchange (one
+    enter/leave, one nbxReduceMultiBatch per rank and (datatype, op)); a
+    collective that reads an earlier one's output, a change of stream, and
+    AllReduce past 8 ranks (gather step) split the batch — results identical
+    to running them one by one."""
+    torch = torch_gpu
+    comms = nbx.Communicator.init_all([0] * nranks)
+    try:
+        specs = [(F32, 0, 5000), (F32, 0, 77), (F16, 0, 30000), (BF16, 4, 12345), (I32, 2, 999), (I32, 4, 4096),
+                 (F32, 0, 1), (F64, 3, 2500)]
+        cases = []
+        nbx.group_start()
+        for k, (dt, op, count) in enumerate(specs):
+            xs = oracle.random_inputs(dt, nranks, count, seed=1000 + 10 * nranks + k)
+            txs = [t_of(torch, x) for x in xs]
+            tys = [torch.zeros_like(t) for t in txs]
+            for r in range(nranks):
+                comms[r].all_reduce(txs[r].data_ptr(), tys[r].data_ptr(), count, dt, op, 0)
+            cases.append((dt, op, count, xs, tys, txs))   # inputs stay alive until the group ends
+        # a reduce-scatter in the same group
+        rc = 3001
+        rxs = oracle.random_inputs(F32, nranks, rc * nranks, seed=77)
+        trx = [t_of(torch, x) for x in rxs]
+        rout = [torch.zeros(rc, dtype=torch.float32, device="cuda") for _ in range(nranks)]
+        for r in range(nranks):
+            comms[r].reduce_scatter(trx[r].data_ptr(), rout[r].data_ptr(), rc, F32, 0, 0)
+        # dependent: AllReduce of the first collective's output (must see it complete)
+        dt0, op0, c0, _, tys0, _ = cases[0]
+        dep = [torch.zeros_like(t) for t in tys0]
+        for r in range(nranks):
+            comms[r].all_reduce(tys0[r].data_ptr(), dep[r].data_ptr(), c0, dt0, op0, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        for dt, op, count, xs, tys, _ in cases:
+            devop, arg = oracle.host_to_dev_redop(op, dt, nranks)
+            eb = np.dtype(oracle.NP_STORAGE[dt]).itemsize
+            exp = _ring_order_reduce(oracle, xs, dt, devop, arg, devop == 4, nranks, _blocks(count, eb, nranks))
+            for r in range(nranks):
+                got = np_of(tys[r], exp.dtype)
+                assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), f"dt {dt} op {op} n {count} rank {r}"
+        exp_rs = _ring_order_reduce(oracle, rxs, F32, 0, 0, False, nranks, lambda b: (b * rc, (b + 1) * rc))
+        for r in range(nranks):
+            assert np.array_equal(np_of(rout[r], np.float32), exp_rs[r * rc:(r + 1) * rc]), f"rs rank {r}"
+        first = [np_of(t, np.float32) for t in tys0]
+        exp_dep = _ring_order_reduce(oracle, first, F32, 0, 0, False, nranks, _blocks(c0, 4, nranks))
+        for r in range(nranks):
+            assert np.array_equal(np_of(dep[r], np.float32), exp_dep), f"dependent rank {r}"
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_graph_capture_one_rank_kernel(nbx, oracle, torch_gpu, comm1):
     """The launch path does no allocation or sync, so it captures into a graph."""
     torch = torch_gpu
