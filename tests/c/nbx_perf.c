@@ -6,7 +6,7 @@
  *
  *   nbx_perf [-c allreduce|reducescatter|reduce] [-d dev,dev,...] [-b minbytes]
  *            [-e maxbytes] [-f factor] [-n iters] [-w warmup] [-t float|half|bfloat16|int32|int64|double]
- *            [-o sum|prod|max|min|avg] [-p 0|1]
+ *            [-o sum|prod|max|min|avg] [-p 0|1] [-m agg]
  *
  * -d lists the device of each rank (a device may repeat: ranks sharing one GPU).
  * -p 1 runs one process per rank instead (fork after ncclGetUniqueId, each
@@ -19,7 +19,10 @@
  * rank r's input element i is ((i * 7 + r * 13) % 61) - 30 (exact in every
  * type for sum/max/min/prod with few ranks), the output is compared on the
  * host with the exact expected value, and #wrong counts differing elements.
- * Out-of-place then in-place, like nccl-tests. Exit status 1 if any wrong. */
+ * Out-of-place then in-place, like nccl-tests. -m aggregates agg operations per
+ * iteration in one ncclGroupStart/End (nccl-tests' -m), each on its own slice
+ * of the buffers so they are independent; time is per operation, every
+ * slice is checked. Exit status 1 if any wrong. */
 #define _POSIX_C_SOURCE 200809L
 #include <hip/hip_runtime_api.h>
 #include <math.h>
@@ -159,7 +162,7 @@ static void reduceStats(ncclComm_t comm, hipStream_t st, double* t, long* wrong)
 }
 
 int main(int argc, char** argv) {
-  int coll = kAllReduce, n = 0, devs[MAXR], iters = 20, warm = 5, procMode = 0;
+  int coll = kAllReduce, n = 0, devs[MAXR], iters = 20, warm = 5, procMode = 0, agg = 1;
   size_t minB = 4096, maxB = 16u << 20;
   double factor = 4.0;
   ncclDataType_t type = ncclFloat32;
@@ -187,6 +190,7 @@ int main(int argc, char** argv) {
       op = !strcmp(v, "prod") ? ncclProd : !strcmp(v, "max") ? ncclMax : !strcmp(v, "min") ? ncclMin
            : !strcmp(v, "avg") ? ncclAvg : ncclSum;
     } else if (!strcmp(k, "-p")) procMode = atoi(v);
+    else if (!strcmp(k, "-m")) agg = atoi(v) < 1 ? 1 : atoi(v);
   }
   if (n == 0) {
     int cnt = 0;
@@ -232,16 +236,19 @@ int main(int argc, char** argv) {
   hipStream_t st[MAXR];
   void *sb[MAXR], *rb[MAXR];
   const size_t sendMax = maxB, recvMax = coll == kReduceScatter ? maxB / (size_t)n + 16 : maxB;
+  /* per-operation slices (-m): 256-byte aligned strides */
+  const size_t sStride = (sendMax + 255) / 256 * 256;
+  const size_t rStride = ((recvMax > sendMax ? recvMax : sendMax) + 255) / 256 * 256;
   for (int r = lo; r < hi; r++) {
     HIPT(hipSetDevice(devs[r]));
     HIPT(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking));
-    HIPT(hipMalloc(&sb[r], sendMax));
-    HIPT(hipMalloc(&rb[r], recvMax > sendMax ? recvMax : sendMax));
+    HIPT(hipMalloc(&sb[r], sStride * (size_t)agg));
+    HIPT(hipMalloc(&rb[r], rStride * (size_t)agg));
   }
   void* host = malloc(sendMax);
   if (printer) {
-    printf("# nbx_perf: %s, %d ranks (%s), devices", cname, n,
-           procMode ? "one process per rank" : "one process, ncclCommInitAll");
+    printf("# nbx_perf: %s, %d ranks (%s), %d op(s) per group, devices", cname, n,
+           procMode ? "one process per rank" : "one process, ncclCommInitAll", agg);
     for (int r = 0; r < n; r++) printf(" %d", devs[r]);
     printf("\n#\n# %12s %12s %8s %6s   %9s %8s %8s %6s   %9s %8s %8s %6s\n", "size", "count", "type", "redop",
            "time(us)", "algbw", "busbw", "#wrong", "time(us)", "algbw", "busbw", "#wrong");
@@ -259,11 +266,13 @@ int main(int argc, char** argv) {
       for (int r = lo; r < hi; r++) {   /* inputs */
         for (size_t i = 0; i < sendCount; i++) put(host, i, type, input(i, r));
         HIPT(hipSetDevice(devs[r]));
-        void* dst = inplace ? rb[r] : sb[r];
-        /* on the rank's own (non-blocking) stream: a null-stream hipMemset would not be
-         * ordered before the collective */
-        HIPT(hipMemcpyAsync(dst, host, sendCount * (size_t)eb, hipMemcpyHostToDevice, st[r]));
-        if (!inplace) HIPT(hipMemsetAsync(rb[r], 0, outCount * (size_t)eb, st[r]));
+        for (int k = 0; k < agg; k++) {
+          char* dst = inplace ? (char*)rb[r] + (size_t)k * rStride : (char*)sb[r] + (size_t)k * sStride;
+          /* on the rank's own (non-blocking) stream: a null-stream hipMemset would not be
+           * ordered before the collective */
+          HIPT(hipMemcpyAsync(dst, host, sendCount * (size_t)eb, hipMemcpyHostToDevice, st[r]));
+          if (!inplace) HIPT(hipMemsetAsync((char*)rb[r] + (size_t)k * rStride, 0, outCount * (size_t)eb, st[r]));
+        }
         HIPT(hipStreamSynchronize(st[r]));
       }
       const int root = 0;
@@ -277,14 +286,16 @@ int main(int argc, char** argv) {
           us[inplace] = now_s();
         }
         NCCLT(ncclGroupStart());
-        for (int r = lo; r < hi; r++) {
-          const void* s = inplace ? rb[r] : sb[r];
-          void* d = rb[r];
-          if (coll == kReduceScatter && inplace) d = (char*)rb[r] + (size_t)r * count * (size_t)eb;
-          if (coll == kAllReduce) NCCLT(ncclAllReduce(s, d, count, type, op, comms[r], st[r]));
-          else if (coll == kReduceScatter) NCCLT(ncclReduceScatter(s, d, count, type, op, comms[r], st[r]));
-          else NCCLT(ncclReduce(s, d, count, type, op, root, comms[r], st[r]));
-        }
+        for (int k = 0; k < agg; k++)
+          for (int r = lo; r < hi; r++) {
+            char* rk = (char*)rb[r] + (size_t)k * rStride;
+            const void* s = inplace ? (const void*)rk : (const void*)((char*)sb[r] + (size_t)k * sStride);
+            void* d = rk;
+            if (coll == kReduceScatter && inplace) d = rk + (size_t)r * count * (size_t)eb;
+            if (coll == kAllReduce) NCCLT(ncclAllReduce(s, d, count, type, op, comms[r], st[r]));
+            else if (coll == kReduceScatter) NCCLT(ncclReduceScatter(s, d, count, type, op, comms[r], st[r]));
+            else NCCLT(ncclReduce(s, d, count, type, op, root, comms[r], st[r]));
+          }
         NCCLT(ncclGroupEnd());
         if (it == -1) {   /* check the first call's result (later calls re-reduce in-place data) */
           wrong[inplace] = 0;
@@ -292,10 +303,12 @@ int main(int argc, char** argv) {
             HIPT(hipSetDevice(devs[r]));
             HIPT(hipStreamSynchronize(st[r]));
           }
+          for (int k = 0; k < agg; k++)
           for (int r = lo; r < hi; r++) {
             if (coll == kReduce && r != root) continue;
             HIPT(hipSetDevice(devs[r]));
-            const char* d = (const char*)rb[r] + ((coll == kReduceScatter && inplace) ? (size_t)r * count * (size_t)eb : 0);
+            const char* d = (const char*)rb[r] + (size_t)k * rStride +
+                            ((coll == kReduceScatter && inplace) ? (size_t)r * count * (size_t)eb : 0);
             HIPT(hipMemcpyAsync(host, d, outCount * (size_t)eb, hipMemcpyDeviceToHost, st[r]));
             HIPT(hipStreamSynchronize(st[r]));
             const size_t base = coll == kReduceScatter ? (size_t)r * count : 0;
@@ -318,7 +331,9 @@ int main(int argc, char** argv) {
             for (int r = lo; r < hi; r++) {
               for (size_t i = 0; i < sendCount; i++) put(host, i, type, input(i, r));
               HIPT(hipSetDevice(devs[r]));
-              HIPT(hipMemcpyAsync(rb[r], host, sendCount * (size_t)eb, hipMemcpyHostToDevice, st[r]));
+              for (int k = 0; k < agg; k++)
+                HIPT(hipMemcpyAsync((char*)rb[r] + (size_t)k * rStride, host, sendCount * (size_t)eb,
+                                    hipMemcpyHostToDevice, st[r]));
               HIPT(hipStreamSynchronize(st[r]));
             }
           }
@@ -328,7 +343,7 @@ int main(int argc, char** argv) {
         HIPT(hipSetDevice(devs[r]));
         HIPT(hipStreamSynchronize(st[r]));
       }
-      us[inplace] = (now_s() - us[inplace]) * 1e6 / iters;
+      us[inplace] = (now_s() - us[inplace]) * 1e6 / iters / agg;   /* per operation */
       if (procMode) reduceStats(comms[lo], st[lo], &us[inplace], &wrong[inplace]);
       totalWrong += wrong[inplace];
     }

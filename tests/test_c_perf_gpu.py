@@ -23,6 +23,10 @@ EXE = os.path.join(ROOT, "neuronabox-nccl_amd", "lib", "nbx_perf")
     ["-c", "reducescatter", "-d", "0,0,0", "-t", "float", "-o", "sum"],
     ["-c", "reducescatter", "-d", "0,0", "-t", "int64", "-o", "min"],
     ["-c", "reduce", "-d", "0,0,0", "-t", "double", "-o", "sum"],
+    # -m: 6 independent operations per group (the clique's batched exchange)
+    ["-c", "allreduce", "-d", "0,0,0", "-t", "half", "-o", "sum", "-m", "6"],
+    ["-c", "reducescatter", "-d", "0,0", "-t", "int32", "-o", "avg", "-m", "4"],
+    ["-c", "reduce", "-d", "0,0,0", "-t", "float", "-o", "max", "-m", "3"],
 ])
 def test_nbx_perf_sweep(args):
     _run(args)
@@ -36,6 +40,7 @@ def test_nbx_perf_sweep(args):
     ["-p", "1", "-c", "allreduce", "-d", "0,0,0", "-t", "int32", "-o", "avg"],
     ["-p", "1", "-c", "reducescatter", "-d", "0,0,0", "-t", "float", "-o", "sum"],
     ["-p", "1", "-c", "reduce", "-d", "0,0,0", "-t", "half", "-o", "sum"],
+    ["-p", "1", "-c", "allreduce", "-d", "0,0", "-t", "float", "-o", "sum", "-m", "3"],
 ])
 def test_nbx_perf_multiprocess(args):
     env = dict(os.environ, NBX_LL128_MAX_GRID="16", NBX_LL_MAX_GRID="64", NBX_TIMEOUT_SEC="60",
