@@ -28,6 +28,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -642,6 +643,18 @@ ncclResult_t flushPendingImpl() {
 enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kSlotRing = 3, kNumSlots = 4 };
 constexpr int kMaxMpRanks = 64;
 
+// One reducing collective as enqueued on a multi-process communicator.
+struct MpCall {
+  CollKind kind;
+  const void* send;
+  void* recv;
+  size_t count;
+  ncclDataType_t dt;
+  nbxDevRedOpFull op;
+  int root;
+  hipStream_t stream;
+};
+
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
   nbx::ShmExchange* shmx = nullptr;     // per-call exchange through /dev/shm (nullptr: TCP bootstrap)
@@ -680,6 +693,7 @@ struct MpState {
   uint64_t l128Bytes = 0;
   int protoMask = 0;                // NCCL_PROTO at init: kProtoLL | kProtoLL128 | kProtoSimple
   bool ring = false;                // NCCL_ALGO=Ring at init
+  std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
 };
 
 struct MpInitInfo {
@@ -753,6 +767,7 @@ struct MpCallInfo {
   uint64_t seq;
   int32_t kind, dt, op, root;
   uint64_t count;
+  int32_t flags;   // kMpContig
   int32_t hasSend, hasRecv;
   hipIpcMemHandle_t sendH, recvH;
   uint64_t sendOff, recvOff;
@@ -1016,189 +1031,247 @@ void mpFree(ncclComm* c) {
   c->mp = nullptr;
 }
 
-ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* recv, size_t count, ncclDataType_t dt,
-                       const nbxDevRedOpFull& op, int root, hipStream_t stream) {
+// The protocol of a call. It depends only on arguments every rank passes
+// identically (and on the init-time settings checked equal), so every rank
+// picks the same one.
+MpProto mpProtoOf(const ncclComm* comm, const MpCall& c) {
+  const MpState* mp = comm->mp;
+  const int n = comm->nRanks;
+  const int eb = typeSize(c.dt);
+  const uint64_t slotBytes = (uint64_t)c.count * (uint64_t)eb;   // RS: recvcount per block
+  size_t off0, per;
+  blockRange(c.count, eb, n, 0, &off0, &per);   // the direct schedule's AllReduce block
+  return chooseProtoFor(mp->protoMask, c.kind != kReduceScatter, slotBytes, (uint64_t)per * (uint64_t)eb, n,
+                        mp->llMaxBytes, mp->l128MaxBytes, mp->l128OneShotMax);
+}
+
+// LL / LL128 protocols: small and medium collectives in one kernel, no host
+// exchange (nbx_ll.h).
+ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
-  const int eb = typeSize(dt);
-  // LL / LL128 protocols: small and medium collectives in one kernel, no host
-  // exchange (nbx_ll.h). The choice depends only on arguments every rank
-  // passes identically (and on the init-time settings checked equal).
-  const uint64_t slotBytes = (uint64_t)count * (uint64_t)eb;   // RS: recvcount per block
+  const int eb = typeSize(c.dt);
+  const uint64_t slotBytes = (uint64_t)c.count * (uint64_t)eb;
   size_t off0, per;
-  blockRange(count, eb, n, 0, &off0, &per);   // the direct schedule's AllReduce block
-  const MpProto proto = chooseProtoFor(mp->protoMask, kind != kReduceScatter, slotBytes, (uint64_t)per * (uint64_t)eb, n,
-                                       mp->llMaxBytes, mp->l128MaxBytes, mp->l128OneShotMax);
-  if (proto != kMpSimple) {
-    if (send == nullptr || (recv == nullptr && (kind != kReduce || me == root))) {
-      warn("rank %d passed a NULL buffer", me);
-      return ncclInvalidArgument;
-    }
-    ++mp->seq;
-    nbx::LLArgs la{};
-    la.send = send;
-    la.recv = recv;
-    la.count = count;
-    la.nPacks = (slotBytes + 7) / 8;
-    la.peerLL = mp->peerLLDev;
-    la.myLL = mp->ll;
-    la.slotLines = mp->llSlotLines;
-    la.doneOff = mp->llDoneOff;
-    la.state = mp->llState;
-    la.blockElts = per > 0 ? per : 1;
-    la.abortWord = mp->hostWordsDev;
-    la.errWord = mp->hostWordsDev + 1;
-    la.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
-    la.rank = me;
-    la.nRanks = n;
-    la.postOp = 1;
-    la.mode = kind == kAllReduce ? nbx::kLLAllReduce : kind == kReduceScatter ? nbx::kLLReduceScatter : nbx::kLLReduce;
-    la.root = root;
-    if (proto == kMpLL128 || proto == kMpLL128x2) {
-      la.peerL128 = mp->peerL128Dev;
-      la.myL128 = mp->l128;
-      la.l128SlotLines = mp->l128SlotLines;
-      la.l128Bytes = (uint32_t)mp->l128Bytes;
-      if (proto == kMpLL128x2) {
-        la.nLines = mp->l128SlotLines / 2;   // sub-slot lines: [parity][RS|AG][source]
-        const uint64_t blockLines = ((uint64_t)per * (uint64_t)eb + nbx::kL128DataBytesHost - 1) /
-                                    nbx::kL128DataBytesHost;
-        return nbx::launchLL128AllReduce2(dt, op, la, blockLines, stream);
-      }
-      la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
-      return nbx::launchLL128Coll(dt, op, la, stream);
-    }
-    return nbx::launchLLColl(dt, op, la, stream);
+  blockRange(c.count, eb, n, 0, &off0, &per);
+  if (c.send == nullptr || (c.recv == nullptr && (c.kind != kReduce || me == c.root))) {
+    warn("rank %d passed a NULL buffer", me);
+    return ncclInvalidArgument;
   }
+  ++mp->seq;
+  nbx::LLArgs la{};
+  la.send = c.send;
+  la.recv = c.recv;
+  la.count = c.count;
+  la.nPacks = (slotBytes + 7) / 8;
+  la.peerLL = mp->peerLLDev;
+  la.myLL = mp->ll;
+  la.slotLines = mp->llSlotLines;
+  la.doneOff = mp->llDoneOff;
+  la.state = mp->llState;
+  la.blockElts = per > 0 ? per : 1;
+  la.abortWord = mp->hostWordsDev;
+  la.errWord = mp->hostWordsDev + 1;
+  la.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
+  la.rank = me;
+  la.nRanks = n;
+  la.postOp = 1;
+  la.mode = c.kind == kAllReduce       ? nbx::kLLAllReduce
+            : c.kind == kReduceScatter ? nbx::kLLReduceScatter
+                                       : nbx::kLLReduce;
+  la.root = c.root;
+  if (proto == kMpLL128 || proto == kMpLL128x2) {
+    la.peerL128 = mp->peerL128Dev;
+    la.myL128 = mp->l128;
+    la.l128SlotLines = mp->l128SlotLines;
+    la.l128Bytes = (uint32_t)mp->l128Bytes;
+    if (proto == kMpLL128x2) {
+      la.nLines = mp->l128SlotLines / 2;   // sub-slot lines: [parity][RS|AG][source]
+      const uint64_t blockLines =
+          ((uint64_t)per * (uint64_t)eb + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+      return nbx::launchLL128AllReduce2(c.dt, c.op, la, blockLines, c.stream);
+    }
+    la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+    return nbx::launchLL128Coll(c.dt, c.op, la, c.stream);
+  }
+  return nbx::launchLLColl(c.dt, c.op, la, c.stream);
+}
+
+// Simple path, step 0: allgather the call (kind, type, op, count) and the IPC
+// handles of every rank's buffers, and check that the ranks agree.
+// `flags` is this rank's kMpContig bit, exchanged so that group batching
+// decisions are identical on every rank.
+constexpr int32_t kMpContig = 1;   // same stream as the previous call of the group
+ncclResult_t mpExchangeCall(ncclComm* comm, const MpCall& c, int32_t flags, std::vector<MpCallInfo>* all) {
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks, me = comm->rank;
   const uint64_t seq = ++mp->seq;
   MpCallInfo mine{};
   mine.seq = seq;
-  mine.kind = (int32_t)kind;
-  mine.dt = (int32_t)dt;
-  mine.op = op.op;
-  mine.root = root;
-  mine.count = count;
-  mine.hasSend = count > 0 && send != nullptr;
-  mine.hasRecv = count > 0 && recv != nullptr;
-  if (mine.hasSend) NCCLCHECK(ipcHandleOf(send, &mine.sendH, &mine.sendOff));
-  if (mine.hasRecv) NCCLCHECK(ipcHandleOf(recv, &mine.recvH, &mine.recvOff));
-  std::vector<MpCallInfo> all(n);
-  NCCLCHECK(mpExchange(mp, seq, &mine, sizeof(mine), all.data()));
+  mine.kind = (int32_t)c.kind;
+  mine.dt = (int32_t)c.dt;
+  mine.op = c.op.op;
+  mine.root = c.root;
+  mine.count = c.count;
+  mine.flags = flags;
+  mine.hasSend = c.count > 0 && c.send != nullptr;
+  mine.hasRecv = c.count > 0 && c.recv != nullptr;
+  if (mine.hasSend) NCCLCHECK(ipcHandleOf(c.send, &mine.sendH, &mine.sendOff));
+  if (mine.hasRecv) NCCLCHECK(ipcHandleOf(c.recv, &mine.recvH, &mine.recvOff));
+  all->assign(n, MpCallInfo{});
+  NCCLCHECK(mpExchange(mp, seq, &mine, sizeof(mine), all->data()));
   for (int j = 0; j < n; j++) {
-    const MpCallInfo& a = all[j];
-    if (a.seq != seq || a.kind != mine.kind || a.dt != mine.dt || a.op != mine.op || a.root != root ||
-        a.count != count) {
+    const MpCallInfo& a = (*all)[j];
+    if (a.seq != seq || a.kind != mine.kind || a.dt != mine.dt || a.op != mine.op || a.root != c.root ||
+        a.count != c.count) {
       warn("collective mismatch across ranks (rank %d vs %d)", j, me);
       return ncclInvalidUsage;
     }
   }
-  if (count == 0) return ncclSuccess;
-  // Bound the mapping cache: a peer's freed-and-reallocated buffers come back
-  // with new handles, and every open mapping pins the peer's old allocation.
-  // Past the bound, wait for this device's work (no kernel in flight uses a
-  // mapping), then close every mapping not used by the previous call.
-  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
-  HIPCHECK(hipStreamIsCapturing(stream, &capture));
-  const bool capturing = capture != hipStreamCaptureStatusNone;
-  if (mp->maps.size() > mp->mapsMax && !capturing) {
-    HIPCHECK(hipDeviceSynchronize());
-    for (auto it = mp->maps.begin(); it != mp->maps.end();) {
-      if (it->second.lastUse != MpState::kPinned && it->second.lastUse + 1 < seq) {
-        (void)hipIpcCloseMemHandle(it->second.base);
-        it = mp->maps.erase(it);
-      } else {
-        ++it;
-      }
+  return ncclSuccess;
+}
+
+// Bound the mapping cache: a peer's freed-and-reallocated buffers come back
+// with new handles, and every open mapping pins the peer's old allocation.
+// Past the bound, wait for this device's work (no kernel in flight uses a
+// mapping), then close every mapping not used since the call before `seq`.
+ncclResult_t mpEvictMappings(MpState* mp, uint64_t seq, bool capturing) {
+  if (mp->maps.size() <= mp->mapsMax || capturing) return ncclSuccess;
+  HIPCHECK(hipDeviceSynchronize());
+  for (auto it = mp->maps.begin(); it != mp->maps.end();) {
+    if (it->second.lastUse != MpState::kPinned && it->second.lastUse + 1 < seq) {
+      (void)hipIpcCloseMemHandle(it->second.base);
+      it = mp->maps.erase(it);
+    } else {
+      ++it;
     }
   }
-  std::vector<const char*> sendP(n, nullptr);
-  std::vector<char*> recvP(n, nullptr);
+  return ncclSuccess;
+}
+
+// Every rank's send / recv base for one call (own buffers as passed, peers'
+// through the IPC mapping cache).
+ncclResult_t mpMapCall(ncclComm* comm, const MpCall& c, const std::vector<MpCallInfo>& all, bool capturing,
+                       std::vector<const char*>* sendP, std::vector<char*>* recvP) {
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks, me = comm->rank;
+  sendP->assign(n, nullptr);
+  recvP->assign(n, nullptr);
   for (int j = 0; j < n; j++) {
     if (j == me) {
-      sendP[j] = (const char*)send;
-      recvP[j] = (char*)recv;
+      (*sendP)[j] = (const char*)c.send;
+      (*recvP)[j] = (char*)c.recv;
       continue;
     }
     void* b = nullptr;
     if (all[j].hasSend) {
       NCCLCHECK(mapPeer(mp, j, all[j].sendH, &b, capturing));
-      sendP[j] = (const char*)b + all[j].sendOff;
+      (*sendP)[j] = (const char*)b + all[j].sendOff;
     }
     if (all[j].hasRecv) {
       NCCLCHECK(mapPeer(mp, j, all[j].recvH, &b, capturing));
-      recvP[j] = (char*)b + all[j].recvOff;
+      (*recvP)[j] = (char*)b + all[j].recvOff;
     }
   }
   for (int j = 0; j < n; j++)
-    if (!sendP[j] || ((kind != kReduce || j == root) && !recvP[j])) {
+    if (!(*sendP)[j] || ((c.kind != kReduce || j == c.root) && !(*recvP)[j])) {
       warn("rank %d passed a NULL buffer", j);
       return ncclInvalidArgument;
     }
+  return ncclSuccess;
+}
+
+// This rank's block of the direct schedule: block `me` of every rank's send
+// buffer in fold order, and where the folded block goes. AllReduce /
+// ReduceScatter fold in ring order me+1, ..., me; Reduce in chain order
+// root+1, ..., root for every block (reduce.h:44-67). AllReduce with
+// n <= NBX_MAX_DSTS pushes the block into every rank's output (push-gather,
+// all_reduce.h:343-360), so there is no separate gather phase.
+void mpDirectBlock(const MpCall& c, int n, int me, const std::vector<const char*>& sendP,
+                   const std::vector<char*>& recvP, std::vector<const void*>* srcs, std::vector<void*>* dsts,
+                   size_t* len) {
+  const int eb = typeSize(c.dt);
+  const size_t total = c.kind == kReduceScatter ? c.count * (size_t)n : c.count;
+  size_t off;
+  if (c.kind == kReduceScatter) {
+    off = (size_t)me * c.count;
+    *len = c.count;
+  } else {
+    blockRange(total, eb, n, me, &off, len);
+  }
+  srcs->clear();
+  dsts->clear();
+  if (*len == 0) return;
+  const int first = (c.kind == kReduce ? c.root : me) + 1;
+  for (int k = 0; k < n; k++) srcs->push_back(sendP[(first + k) % n] + off * (size_t)eb);
+  if (c.kind == kReduceScatter) dsts->push_back(recvP[me]);
+  else if (c.kind == kReduce) dsts->push_back(recvP[c.root] + off * (size_t)eb);
+  else if (n > NBX_MAX_DSTS) dsts->push_back(recvP[me] + off * (size_t)eb);
+  else
+    for (int k = 0; k < n; k++) dsts->push_back(recvP[(me + k) % n] + off * (size_t)eb);
+}
+
+// Simple path, after the exchange: map, barriers, reduce (direct or ring), gather.
+ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCallInfo>& all) {
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks, me = comm->rank;
+  const int eb = typeSize(c.dt);
+  hipStream_t stream = c.stream;
+  if (c.count == 0) return ncclSuccess;
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(stream, &capture));
+  const bool capturing = capture != hipStreamCaptureStatusNone;
+  NCCLCHECK(mpEvictMappings(mp, all[me].seq, capturing));
+  std::vector<const char*> sendP;
+  std::vector<char*> recvP;
+  NCCLCHECK(mpMapCall(comm, c, all, capturing, &sendP, &recvP));
   // 1. every rank's stream has reached the collective (its inputs are written,
   //    its output may be written by peers)
   NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
-  const size_t total = kind == kReduceScatter ? count * (size_t)n : count;
-  // AllReduce with n <= NBX_MAX_DSTS: push-gather — the kernel completing a
-  // block stores it into every rank's output at once (all xGMI links busy in
-  // one kernel, the CollNet-direct scatter shape all_reduce.h:343-360), so
-  // there is no separate gather phase and no barrier before it
-  const bool push = kind == kAllReduce && n <= NBX_MAX_DSTS;
-  std::vector<void*> pushDsts;
-  auto allOutputs = [&](size_t o) {
-    pushDsts.clear();
-    for (int k = 0; k < n; k++) pushDsts.push_back(recvP[(me + k) % n] + o * (size_t)eb);
-    return pushDsts.data();
-  };
-  size_t off, len;
-  if (kind == kAllReduce && n > 2 && mp->ring) {
+  const size_t total = c.kind == kReduceScatter ? c.count * (size_t)n : c.count;
+  const bool push = c.kind == kAllReduce && n <= NBX_MAX_DSTS;
+  if (c.kind == kAllReduce && n > 2 && mp->ring) {
     // 2'. ring reduce-scatter (all_reduce.h:60-79): chunk c starts at rank c+1 and
     // visits c+2, ..., c; at step s this rank folds chunk c = me-2-s as
     // Fn(pre(local), received) — NCCL's operand order (recvReduceSend: srcs[0] is
     // the local input, srcs[1] the received partial) — into its own recv buffer,
     // where the right neighbour reads it at step s+1. Step 0 reads the left
     // neighbour's raw input (its `send`, PreOp applies to both sources); the last
-    // step (c == me) applies postOp. Every rank works on a different chunk at
-    // each step, so all ring links carry 1/n of the data concurrently.
+    // step (c == me) applies postOp and, with push, stores into every output.
+    // Every rank works on a different chunk at each step, so all ring links
+    // carry 1/n of the data concurrently.
     const int left = (me + n - 1) % n;
+    std::vector<void*> pushDsts;
     for (int st = 0; st < n - 1; st++) {
-      const int c = ((me - 2 - st) % n + n) % n;
-      blockRange(total, eb, n, c, &off, &len);
+      const int ch = ((me - 2 - st) % n + n) % n;
+      size_t off, len;
+      blockRange(total, eb, n, ch, &off, &len);
       if (len > 0) {
         const void* srcs[2] = {sendP[me] + off * (size_t)eb,
                                st == 0 ? (const void*)(sendP[left] + off * (size_t)eb)
                                        : (const void*)(recvP[left] + off * (size_t)eb)};
         void* dsts[1] = {recvP[me] + off * (size_t)eb};
         const bool last = st == n - 2;
-        NCCLCHECK(nbx::reduceMultiEx(last && push ? allOutputs(off) : dsts, last && push ? n : 1, srcs, 2, len, dt,
-                                     op, st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream,
+        pushDsts.clear();
+        for (int k = 0; k < n; k++) pushDsts.push_back(recvP[(me + k) % n] + off * (size_t)eb);
+        NCCLCHECK(nbx::reduceMultiEx(last && push ? pushDsts.data() : dsts, last && push ? n : 1, srcs, 2, len,
+                                     c.dt, c.op, st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream,
                                      nbx::kReduceAcquireSystem));
       }
       if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, 1ull << left, stream));
     }
   } else {
-  // 2. direct reduce of this rank's block
-  if (kind == kReduceScatter) {
-    off = (size_t)me * count;
-    len = count;
-  } else {
-    blockRange(total, eb, n, me, &off, &len);
-  }
-  if (len > 0) {
-    // AllReduce / ReduceScatter: ring order me+1, ..., me; Reduce: chain order
-    // root+1, ..., root for every block (reduce.h:44-67)
-    const int first = (kind == kReduce ? root : me) + 1;
-    std::vector<const void*> srcs(n);
-    for (int k = 0; k < n; k++) srcs[k] = sendP[(first + k) % n] + off * (size_t)eb;
-    void* dst = kind == kReduceScatter ? (void*)recvP[me]
-                : kind == kReduce      ? (void*)(recvP[root] + off * (size_t)eb)
-                                       : (void*)(recvP[me] + off * (size_t)eb);
-    void* dsts[1] = {dst};
-    NCCLCHECK(nbx::reduceMultiEx(push ? allOutputs(off) : dsts, push ? n : 1, srcs.data(), n, len, dt, op, n, 1,
-                                 (ncclStream_t)stream, nbx::kReduceAcquireSystem));
-  }
+    // 2. direct reduce of this rank's block
+    std::vector<const void*> srcs;
+    std::vector<void*> dsts;
+    size_t len;
+    mpDirectBlock(c, n, me, sendP, recvP, &srcs, &dsts, &len);
+    if (len > 0)
+      NCCLCHECK(nbx::reduceMultiEx(dsts.data(), (int)dsts.size(), srcs.data(), n, len, c.dt, c.op, n, 1,
+                                   (ncclStream_t)stream, nbx::kReduceAcquireSystem));
   }
   // 3. AllReduce with n > NBX_MAX_DSTS: gather the peers' reduced blocks
-  if (kind == kAllReduce && !push) {
+  if (c.kind == kAllReduce && !push) {
     NCCLCHECK(mpBarrier(comm, kSlotReduced, stream));
     nbxDevRedOpFull copyOp{nbxDevSum, 0, 0};
     for (int k = 1; k < n; k++) {
@@ -1217,6 +1290,184 @@ ncclResult_t runMpColl(ncclComm* comm, CollKind kind, const void* send, void* re
   return ncclSuccess;
 }
 
+ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
+  const MpProto proto = mpProtoOf(comm, c);
+  if (proto != kMpSimple) return mpLaunchLL(comm, c, proto);
+  std::vector<MpCallInfo> all;
+  NCCLCHECK(mpExchangeCall(comm, c, 0, &all));
+  return mpRunSimple(comm, c, all);
+}
+
+// ---------------------------------------------------------------------------
+// Groups on a multi-process communicator. Inside ncclGroupStart/End the calls
+// are queued and run at the outermost ncclGroupEnd, in order: every
+// Simple-protocol call is exchanged first (one allgather each, flags
+// included), then maximal runs of direct-schedule calls that every rank issued
+// on one stream and that touch no buffer an earlier member of the run writes
+// (or write one it reads) run as ONE exchange — one enter barrier, one
+// nbxReduceMultiBatch per (datatype, op), one done barrier — the way NCCL packs
+// a group's collectives into one kernel's work list (enqueue.cc:67-91
+// appendWorkElemColl). Every decision uses only exchanged data, so all ranks
+// make the same one. LL / LL128 calls and the ring / gather schedules run
+// one by one, in order. NBX_GROUP_BATCH=0 runs every call at enqueue instead.
+thread_local std::vector<ncclComm*> t_groupMpComms;
+constexpr size_t kMaxMpBatch = 64;
+
+bool groupBatchEnabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("NBX_GROUP_BATCH");
+    return !(v && std::strcmp(v, "0") == 0);
+  }();
+  return on;
+}
+
+// Bytes of every rank's buffers a call reads (send) and writes (recv),
+// identified by (IPC handle of the allocation, offset range).
+struct HSpan {
+  hipIpcMemHandle_t h;
+  uint64_t lo, hi;
+  bool write;
+};
+
+void callSpans(const MpCall& c, int n, const std::vector<MpCallInfo>& all, std::vector<HSpan>* out) {
+  const uint64_t eb = (uint64_t)typeSize(c.dt);
+  const uint64_t sendBytes = (c.kind == kReduceScatter ? (uint64_t)c.count * (uint64_t)n : c.count) * eb;
+  const uint64_t recvBytes = (uint64_t)c.count * eb;
+  for (const MpCallInfo& a : all) {
+    if (a.hasSend) out->push_back({a.sendH, a.sendOff, a.sendOff + sendBytes, false});
+    if (a.hasRecv) out->push_back({a.recvH, a.recvOff, a.recvOff + recvBytes, true});
+  }
+}
+
+bool hspansConflict(const std::vector<HSpan>& a, const std::vector<HSpan>& b) {
+  for (const HSpan& x : a)
+    for (const HSpan& y : b)
+      if ((x.write || y.write) && x.lo < y.hi && y.lo < x.hi && std::memcmp(&x.h, &y.h, sizeof(x.h)) == 0)
+        return true;
+  return false;
+}
+
+// One batched exchange over calls[lo, hi) (all Simple, direct schedule, one stream).
+ncclResult_t mpRunBatch(ncclComm* comm, const std::vector<MpCall>& calls,
+                        const std::vector<std::vector<MpCallInfo>>& alls, size_t lo, size_t hi) {
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks, me = comm->rank;
+  hipStream_t stream = calls[lo].stream;
+  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(stream, &capture));
+  const bool capturing = capture != hipStreamCaptureStatusNone;
+  NCCLCHECK(mpEvictMappings(mp, alls[lo][me].seq, capturing));
+  const size_t m = hi - lo;
+  std::vector<std::vector<const void*>> srcs(m);
+  std::vector<std::vector<void*>> dsts(m);
+  std::vector<size_t> lens(m);
+  for (size_t k = 0; k < m; k++) {
+    std::vector<const char*> sendP;
+    std::vector<char*> recvP;
+    NCCLCHECK(mpMapCall(comm, calls[lo + k], alls[lo + k], capturing, &sendP, &recvP));
+    mpDirectBlock(calls[lo + k], n, me, sendP, recvP, &srcs[k], &dsts[k], &lens[k]);
+  }
+  NBX_TRACE("mp group batch of %zu collectives", m);
+  NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
+  size_t i = 0;
+  while (i < m) {   // one batched launch set per run of equal (datatype, op)
+    const MpCall& ci = calls[lo + i];
+    std::vector<nbxReduceTask> tasks;
+    size_t j = i;
+    for (; j < m; j++) {
+      const MpCall& cj = calls[lo + j];
+      if (cj.dt != ci.dt || cj.op.op != ci.op.op || cj.op.scalarArg != ci.op.scalarArg ||
+          cj.op.scalarArgIsPtr != ci.op.scalarArgIsPtr)
+        break;
+      if (lens[j] == 0) continue;
+      tasks.push_back({dsts[j].data(), (int)dsts[j].size(), srcs[j].data(), n, lens[j]});
+    }
+    NCCLCHECK(nbx::reduceMultiBatchEx(tasks.data(), (int)tasks.size(), ci.dt, ci.op, /*nPreOpSrcs=*/n,
+                                      /*postOp=*/1, (ncclStream_t)stream, nbx::kReduceAcquireSystem));
+    i = j;
+  }
+  NCCLCHECK(mpBarrier(comm, kSlotDone, stream));
+  return ncclSuccess;
+}
+
+ncclResult_t runMpGroupImpl(ncclComm* comm) {
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks;
+  std::vector<MpCall> calls;
+  calls.swap(mp->group);
+  const size_t m = calls.size();
+  std::vector<MpProto> protos(m);
+  std::vector<std::vector<MpCallInfo>> alls(m);
+  for (size_t k = 0; k < m; k++) {
+    protos[k] = mpProtoOf(comm, calls[k]);
+    if (protos[k] != kMpSimple) continue;
+    const int32_t flags = (k > 0 && protos[k - 1] == kMpSimple && calls[k].stream == calls[k - 1].stream) ? kMpContig : 0;
+    NCCLCHECK(mpExchangeCall(comm, calls[k], flags, &alls[k]));
+  }
+  auto directSimple = [&](size_t k) {
+    const MpCall& c = calls[k];
+    return protos[k] == kMpSimple && c.count > 0 && !(c.kind == kAllReduce && n > NBX_MAX_DSTS) &&
+           !(c.kind == kAllReduce && n > 2 && mp->ring);
+  };
+  auto contigEverywhere = [&](size_t k) {
+    for (const MpCallInfo& a : alls[k])
+      if (!(a.flags & kMpContig)) return false;
+    return true;
+  };
+  size_t k = 0;
+  while (k < m) {
+    if (protos[k] != kMpSimple) {
+      NCCLCHECK(mpLaunchLL(comm, calls[k], protos[k]));
+      k++;
+      continue;
+    }
+    size_t j = k + 1;
+    if (directSimple(k)) {
+      std::vector<HSpan> spans;
+      callSpans(calls[k], n, alls[k], &spans);
+      for (; j < m && j - k < kMaxMpBatch; j++) {
+        if (!directSimple(j) || !contigEverywhere(j)) break;
+        std::vector<HSpan> sj;
+        callSpans(calls[j], n, alls[j], &sj);
+        if (hspansConflict(spans, sj)) break;
+        spans.insert(spans.end(), sj.begin(), sj.end());
+      }
+    }
+    if (j == k + 1) NCCLCHECK(mpRunSimple(comm, calls[k], alls[k]));
+    else NCCLCHECK(mpRunBatch(comm, calls, alls, k, j));
+    k = j;
+  }
+  return ncclSuccess;
+}
+
+ncclResult_t runMpGroup(ncclComm* comm) {
+  DevGuard g(comm->device);
+  ncclResult_t r;
+  try {
+    r = runMpGroupImpl(comm);
+  } catch (const std::exception& e) {
+    warn("internal exception: %s", e.what());
+    r = ncclInternalError;
+  }
+  comm->mp->group.clear();
+  if (r != ncclSuccess) comm->asyncError.store(r);
+  return r;
+}
+
+// Runs the queued calls of every multi-process communicator this thread used
+// in the group that just ended; the first error is returned.
+ncclResult_t flushMpGroups() {
+  std::vector<ncclComm*> comms;
+  comms.swap(t_groupMpComms);
+  ncclResult_t first = ncclSuccess;
+  for (ncclComm* c : comms) {
+    if (c->magic != kCommMagic || c->mp == nullptr) continue;
+    ncclResult_t r = runMpGroup(c);
+    if (first == ncclSuccess) first = r;
+  }
+  return first;
+}
+
 // ncclEnqueueCheck + taskAppend for the reducing collectives.
 ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff, void* recvbuff, size_t count,
                          ncclDataType_t dt, ncclRedOp_t op, int root, ncclComm* comm, hipStream_t stream) {
@@ -1233,10 +1484,16 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
     return r;
   }
   if (comm->mp) {
+    const MpCall call{kind, sendbuff, recvbuff, count, dt, opFull, root, stream};
+    if (t_groupDepth > 0 && groupBatchEnabled()) {   // run at the outermost ncclGroupEnd
+      if (comm->mp->group.empty()) t_groupMpComms.push_back(comm);
+      comm->mp->group.push_back(call);
+      return ncclSuccess;
+    }
     DevGuard g(comm->device);
     ncclResult_t r;
     try {
-      r = runMpColl(comm, kind, sendbuff, recvbuff, count, dt, opFull, root, stream);
+      r = runMpColl(comm, call);
     } catch (const std::exception& e) {
       warn("internal exception: %s", e.what());
       r = ncclInternalError;
@@ -1395,6 +1652,8 @@ NBX_API(ncclResult_t, ncclCommFinalize, ncclComm_t comm) {
 static ncclResult_t commFree(ncclComm* comm) {
   std::shared_ptr<Clique> c = comm->clique;
   comm->magic = 0;
+  // calls still queued in this thread's open group die with the communicator
+  t_groupMpComms.erase(std::remove(t_groupMpComms.begin(), t_groupMpComms.end(), comm), t_groupMpComms.end());
   mpFree(comm);
   if (c) {
     std::lock_guard<std::mutex> gp(g_pendMu);
@@ -1563,7 +1822,9 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
     return ncclInvalidUsage;
   }
   if (--t_groupDepth > 0) return ncclSuccess;
-  return flushPending();
+  ncclResult_t r = flushPending();
+  ncclResult_t r2 = flushMpGroups();
+  return r != ncclSuccess ? r : r2;
 }
 
 NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }

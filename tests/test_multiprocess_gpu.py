@@ -23,7 +23,12 @@ def _inputs(oracle, kind, dtype, n, r):
     return oracle.random_inputs(dtype, n, cnt, seed=1000 + 10 * dtype)[r]
 
 
-def _child(uid_bytes, rank, n, q):
+def _child(uid_bytes, rank, n, q, grouped=False):
+    """grouped: every round's CASES go into ONE ncclGroupStart/End (the
+    multi-process group batching: queued, exchanged, run as batched
+    exchanges), plus an AllReduce that reads the first case's output (a
+    dependency that must split the batch), with every buffer alive until the
+    group ends."""
     try:
         import torch
         from tests.conftest import load_package
@@ -36,7 +41,33 @@ def _child(uid_bytes, rank, n, q):
         assert comm.count() == n and comm.user_rank() == rank
         st = torch.cuda.Stream()
         out = {}
-        for it in range(2):   # twice: the second round hits the IPC mapping cache
+        if grouped:
+            for it in range(2):
+                live = []
+                nbx.group_start()
+                for kind, dtype, op in CASES:
+                    x = _inputs(oracle, kind, dtype, n, rank)
+                    tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+                    nbytes = (COUNT if kind == "reducescatter" else x.size) * x.itemsize
+                    ty = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+                    torch.cuda.synchronize()
+                    if kind == "allreduce":
+                        comm.all_reduce(tx.data_ptr(), ty.data_ptr(), x.size, dtype, op, st.cuda_stream)
+                    elif kind == "reducescatter":
+                        comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), COUNT, dtype, op, st.cuda_stream)
+                    else:
+                        comm.reduce(tx.data_ptr(), ty.data_ptr() if rank == 1 % n else 0, x.size, dtype, op,
+                                    1 % n, st.cuda_stream)
+                    live.append((kind, dtype, op, tx, ty))
+                first_out = live[0][4]   # ("allreduce", 7, 0)
+                dep = torch.zeros_like(first_out)
+                comm.all_reduce(first_out.data_ptr(), dep.data_ptr(), COUNT, 7, 0, st.cuda_stream)
+                nbx.group_end()
+                st.synchronize()
+                for kind, dtype, op, tx, ty in live:
+                    out[(it, kind, dtype, op)] = ty.cpu().numpy().copy()
+                out[(it, "dep")] = dep.cpu().numpy().copy()
+        for it in range(0 if grouped else 2):   # twice: the second round hits the IPC mapping cache
             for kind, dtype, op in CASES:
                 x = _inputs(oracle, kind, dtype, n, rank)
                 tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
@@ -84,10 +115,43 @@ def test_multiprocess_collectives(nbx, oracle, n, algo, proto, cache, monkeypatc
     monkeypatch.setenv("NCCL_PROTO", proto)
     monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
     monkeypatch.setenv("NBX_IPC_CACHE_MAX", cache)
+    res = _run_ranks(nbx, n, _child)
+    _check_cases(oracle, n, res)
+
+
+@pytest.mark.parametrize("n,proto", [(2, "LL,Simple"), (3, "LL,Simple"), (3, ""), (9, "LL,Simple")])
+def test_multiprocess_grouped_collectives(nbx, oracle, n, proto, monkeypatch):
+    """One ncclGroupStart/End around every case: the calls are queued and run
+    at ncclGroupEnd — independent Simple calls as one batched exchange, LL /
+    LL128 calls in order, the dependent AllReduce after the call it reads.
+    Results are the same as one call at a time (bit-exact); 9 ranks: AllReduce
+    needs the gather step there and runs alone."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
+    monkeypatch.setenv("NBX_LL_MAX_GRID", "64")
+    monkeypatch.setenv("NCCL_PROTO", proto)
+    monkeypatch.setenv("NCCL_ALGO", "")
+    res = _run_ranks(nbx, n, _child, True)
+    _check_cases(oracle, n, res)
+    # the dependent AllReduce summed n copies of case ("allreduce", 7, 0)'s result
+    first = [res[r][(0, "allreduce", 7, 0)].view(np.float32) for r in range(n)]
+    blocks = _blocks(COUNT, 4, n)
+    exp = np.empty(COUNT, dtype=np.float32)
+    for r, (lo, hi) in enumerate(blocks):
+        if hi > lo:
+            order = [(r + 1 + k) % n for k in range(n)]
+            exp[lo:hi] = oracle.reduce_multi([first[j][lo:hi] for j in order], 7, 0, 0, n_pre_op_srcs=n)[0]
+    for it in range(2):
+        for r in range(n):
+            assert np.array_equal(res[r][(it, "dep")].view(np.float32), exp), (it, r)
+
+
+def _run_ranks(nbx, n, target, *extra):
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_child, args=(bytes(uid), r, n, q), daemon=True) for r in range(n)]
+    procs = [ctx.Process(target=target, args=(bytes(uid), r, n, q, *extra), daemon=True) for r in range(n)]
     for p in procs:
         p.start()
     res = {}
@@ -102,6 +166,10 @@ def test_multiprocess_collectives(nbx, oracle, n, algo, proto, cache, monkeypatc
         for p in procs:
             if p.is_alive():
                 p.terminate()
+    return res
+
+
+def _check_cases(oracle, n, res):
     for kind, dtype, op in CASES:
         xs = [_inputs(oracle, kind, dtype, n, r) for r in range(n)]
         devop, arg = oracle.host_to_dev_redop(op, dtype, n)
