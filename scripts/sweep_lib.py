@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--what", default="knobs,pipe,sweep,e2e,small")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--tiles-nsrc", type=lambda v: [int(x) for x in v.split(",")], default=[1, 2, 3, 4, 6, 8])
+    ap.add_argument("--batch-sets", default="", help="comma-separated subset of the batch bucket sets")
     ap.add_argument("--tiles-settings", default="0:0,0:1,4:1,0:2,2:2", help="blocksPerCU:variant,...")
     args = ap.parse_args()
     import torch
@@ -186,13 +187,18 @@ def main():
     if "batch" in what:
         # bucket sets (MiB per input): 16 x 1 MiB, 64 x 256 KiB, the mixed 1..64 MiB sweep
         sets = {"16x1MiB": [1 << 20] * 16, "64x256KiB": [256 << 10] * 64, "128x64KiB": [64 << 10] * 128,
-                "mixed_1_64MiB": [m << 20 for m in (1, 2, 4, 8, 16, 32, 64)]}
-        for dt, name, tdt in ((6, "fp16", torch.float16), (9, "bf16", torch.bfloat16)):
+                "mixed_1_64MiB": [m << 20 for m in (1, 2, 4, 8, 16, 32, 64)],
+                "4x16MiB": [16 << 20] * 4, "1x64MiB": [64 << 20], "1x256MiB": [256 << 20]}
+        only = set(args.batch_sets.split(",")) if args.batch_sets else set(sets)
+        for dt, name, tdt in ((6, "fp16", torch.float16), (9, "bf16", torch.bfloat16), (7, "fp32", torch.float32)):
             for nsrc in (2, 8):
                 for sname, sizes in sets.items():
+                    if sname not in only or (dt == 7) != (sname == "1x256MiB"):
+                        continue   # fp32 only for the config-B-sized bucket
                     bufs = []
+                    esz = torch.tensor([], dtype=tdt).element_size()
                     for b in sizes:
-                        n = b // 2
+                        n = b // esz
                         srcs = [torch.rand(n, device="cuda").to(tdt) for _ in range(nsrc)]
                         bufs.append((srcs, torch.empty_like(srcs[0]), n))
                     calls = [([o.data_ptr()], [t.data_ptr() for t in ss], n) for ss, o, n in bufs]

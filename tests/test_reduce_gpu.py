@@ -289,6 +289,20 @@ def test_batch_table_overflow(nbx, oracle, torch_gpu):
     run_batch(nbx, oracle, torch_gpu, 2, 4, 3, buckets[140:160], post=True)
 
 
+@pytest.mark.parametrize("dtype,nsrc", [(7, 8), (6, 4), (9, 5), (4, 6)])
+def test_batch_large_sets(nbx, oracle, torch_gpu, dtype, nsrc):
+    """Large batches of 4-8 sources (more packs in total than one big tile per
+    CU): ragged bucket sizes, shared misalignments, several destinations."""
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    rng = np.random.default_rng(nsrc)
+    buckets = []
+    for i in range(24):
+        count = int(rng.integers(200000, 600000)) // eb   # bytes per input -> elements
+        off = int(rng.integers(0, 16 // eb)) * eb
+        buckets.append((nsrc, 1 + i % 3, count, off, off, 500 + i))
+    run_batch(nbx, oracle, torch_gpu, dtype, 0, 0, buckets)
+
+
 def test_batch_mixed_bucket_sweep_fp16_bf16(nbx, oracle, torch_gpu):
     """Config C shape: 8-source fp16 and bf16 sums over 1..16 MiB buckets in one
     batch — by default the buckets that fill the GPU alone take the big-tile
