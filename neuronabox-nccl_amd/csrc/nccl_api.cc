@@ -356,19 +356,19 @@ bool sameCollective(const std::vector<PendingColl>& parts) {
   return true;
 }
 
-// Rank r's share of one clique collective: block r of every send buffer, in
-// fold order, and where the folded block goes.
-struct CliqueBlock {
+// Rank r's share of one collective: block r of every send buffer, in fold
+// order, and where the folded block goes (both communicator kinds).
+struct RankBlock {
   std::vector<const void*> srcs;
   std::vector<void*> dsts;
   size_t len = 0;
 };
 
-CliqueBlock cliqueBlock(const std::vector<PendingColl>& parts, int n, int r) {
+RankBlock cliqueBlock(const std::vector<PendingColl>& parts, int n, int r) {
   const PendingColl& p0 = parts[0];
   const int eb = typeSize(p0.dt);
   const size_t total = p0.kind == kReduceScatter ? p0.count * (size_t)n : p0.count;
-  CliqueBlock cb;
+  RankBlock cb;
   size_t off;
   if (p0.kind == kReduceScatter) {
     off = (size_t)r * p0.count;
@@ -392,6 +392,32 @@ CliqueBlock cliqueBlock(const std::vector<PendingColl>& parts, int n, int r) {
   else
     for (int k = 0; k < n; k++) cb.dsts.push_back((char*)parts[(r + k) % n].recv + off * (size_t)eb);
   return cb;
+}
+
+// Fold this rank's blocks of several independent collectives: one batched
+// launch (nbxReduceMultiBatch) per run of consecutive collectives with the
+// same (datatype, op); PreOp on every source and PostOp, as one pass does.
+ncclResult_t foldBlocksBatched(const std::vector<const PendingColl*>& colls, const std::vector<RankBlock>& blocks,
+                               int n, hipStream_t stream) {
+  size_t i = 0;
+  while (i < blocks.size()) {
+    const PendingColl& pi = *colls[i];
+    std::vector<nbxReduceTask> tasks;
+    size_t j = i;
+    for (; j < blocks.size(); j++) {
+      const PendingColl& pj = *colls[j];
+      if (pj.dt != pi.dt || pj.op.op != pi.op.op || pj.op.scalarArg != pi.op.scalarArg ||
+          pj.op.scalarArgIsPtr != pi.op.scalarArgIsPtr)
+        break;
+      const RankBlock& b = blocks[j];
+      if (b.len == 0) continue;
+      tasks.push_back({b.dsts.data(), (int)b.dsts.size(), b.srcs.data(), n, b.len});
+    }
+    NCCLCHECK(nbx::reduceMultiBatchEx(tasks.data(), (int)tasks.size(), pi.dt, pi.op, /*nPreOpSrcs=*/n,
+                                      /*postOp=*/1, (ncclStream_t)stream, nbx::kReduceAcquireSystem));
+    i = j;
+  }
+  return ncclSuccess;
 }
 
 // Run one collective across every rank of an in-process clique.
@@ -421,7 +447,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   const bool push = n <= NBX_MAX_DSTS;
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
-    CliqueBlock cb = cliqueBlock(parts, n, r);
+    RankBlock cb = cliqueBlock(parts, n, r);
     if (cb.len == 0) continue;
     NBX_TRACE("clique reduce rank %d len=%zu dst=%p src0=%p", r, cb.len, cb.dsts[0], cb.srcs[0]);
     NCCLCHECK(nbx::reduceMultiEx(cb.dsts.data(), (int)cb.dsts.size(), cb.srcs.data(), n, cb.len, p0.dt, parts[r].op,
@@ -512,32 +538,13 @@ ncclResult_t runCliqueBatch(Clique* c, const std::vector<std::vector<PendingColl
   }
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
-    std::vector<CliqueBlock> blocks;
-    blocks.reserve(hi - lo);
-    std::vector<size_t> which;
+    std::vector<RankBlock> blocks;
+    std::vector<const PendingColl*> colls;
     for (size_t k = lo; k < hi; k++) {
       blocks.push_back(cliqueBlock(rounds[k], n, r));
-      which.push_back(k);
+      colls.push_back(&rounds[k][r]);
     }
-    // one batched call per (datatype, op) run of consecutive collectives
-    size_t i = 0;
-    while (i < blocks.size()) {
-      const PendingColl& pi = rounds[which[i]][r];
-      std::vector<nbxReduceTask> tasks;
-      size_t j = i;
-      for (; j < blocks.size(); j++) {
-        const PendingColl& pj = rounds[which[j]][r];
-        if (pj.dt != pi.dt || pj.op.op != pi.op.op || pj.op.scalarArg != pi.op.scalarArg ||
-            pj.op.scalarArgIsPtr != pi.op.scalarArgIsPtr)
-          break;
-        const CliqueBlock& cb = blocks[j];
-        if (cb.len == 0) continue;
-        tasks.push_back({cb.dsts.data(), (int)cb.dsts.size(), cb.srcs.data(), n, cb.len});
-      }
-      NCCLCHECK(nbx::reduceMultiBatchEx(tasks.data(), (int)tasks.size(), pi.dt, pi.op, /*nPreOpSrcs=*/n,
-                                        /*postOp=*/1, (ncclStream_t)pi.stream, nbx::kReduceAcquireSystem));
-      i = j;
-    }
+    NCCLCHECK(foldBlocksBatched(colls, blocks, n, rounds[lo][r].stream));
     HIPCHECK(hipEventRecord(c->evDone[r], rounds[lo][r].stream));
   }
   for (int r = 0; r < n; r++) {
@@ -643,17 +650,9 @@ ncclResult_t flushPendingImpl() {
 enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kSlotRing = 3, kNumSlots = 4 };
 constexpr int kMaxMpRanks = 64;
 
-// One reducing collective as enqueued on a multi-process communicator.
-struct MpCall {
-  CollKind kind;
-  const void* send;
-  void* recv;
-  size_t count;
-  ncclDataType_t dt;
-  nbxDevRedOpFull op;
-  int root;
-  hipStream_t stream;
-};
+// One reducing collective as enqueued on a multi-process communicator (the
+// same record the in-process clique queues).
+using MpCall = PendingColl;
 
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
@@ -1187,28 +1186,27 @@ ncclResult_t mpMapCall(ncclComm* comm, const MpCall& c, const std::vector<MpCall
 // root+1, ..., root for every block (reduce.h:44-67). AllReduce with
 // n <= NBX_MAX_DSTS pushes the block into every rank's output (push-gather,
 // all_reduce.h:343-360), so there is no separate gather phase.
-void mpDirectBlock(const MpCall& c, int n, int me, const std::vector<const char*>& sendP,
-                   const std::vector<char*>& recvP, std::vector<const void*>* srcs, std::vector<void*>* dsts,
-                   size_t* len) {
+RankBlock mpDirectBlock(const MpCall& c, int n, int me, const std::vector<const char*>& sendP,
+                        const std::vector<char*>& recvP) {
   const int eb = typeSize(c.dt);
   const size_t total = c.kind == kReduceScatter ? c.count * (size_t)n : c.count;
+  RankBlock b;
   size_t off;
   if (c.kind == kReduceScatter) {
     off = (size_t)me * c.count;
-    *len = c.count;
+    b.len = c.count;
   } else {
-    blockRange(total, eb, n, me, &off, len);
+    blockRange(total, eb, n, me, &off, &b.len);
   }
-  srcs->clear();
-  dsts->clear();
-  if (*len == 0) return;
+  if (b.len == 0) return b;
   const int first = (c.kind == kReduce ? c.root : me) + 1;
-  for (int k = 0; k < n; k++) srcs->push_back(sendP[(first + k) % n] + off * (size_t)eb);
-  if (c.kind == kReduceScatter) dsts->push_back(recvP[me]);
-  else if (c.kind == kReduce) dsts->push_back(recvP[c.root] + off * (size_t)eb);
-  else if (n > NBX_MAX_DSTS) dsts->push_back(recvP[me] + off * (size_t)eb);
+  for (int k = 0; k < n; k++) b.srcs.push_back(sendP[(first + k) % n] + off * (size_t)eb);
+  if (c.kind == kReduceScatter) b.dsts.push_back(recvP[me]);
+  else if (c.kind == kReduce) b.dsts.push_back(recvP[c.root] + off * (size_t)eb);
+  else if (n > NBX_MAX_DSTS) b.dsts.push_back(recvP[me] + off * (size_t)eb);
   else
-    for (int k = 0; k < n; k++) dsts->push_back(recvP[(me + k) % n] + off * (size_t)eb);
+    for (int k = 0; k < n; k++) b.dsts.push_back(recvP[(me + k) % n] + off * (size_t)eb);
+  return b;
 }
 
 // Simple path, after the exchange: map, barriers, reduce (direct or ring), gather.
@@ -1262,12 +1260,9 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
     }
   } else {
     // 2. direct reduce of this rank's block
-    std::vector<const void*> srcs;
-    std::vector<void*> dsts;
-    size_t len;
-    mpDirectBlock(c, n, me, sendP, recvP, &srcs, &dsts, &len);
-    if (len > 0)
-      NCCLCHECK(nbx::reduceMultiEx(dsts.data(), (int)dsts.size(), srcs.data(), n, len, c.dt, c.op, n, 1,
+    const RankBlock b = mpDirectBlock(c, n, me, sendP, recvP);
+    if (b.len > 0)
+      NCCLCHECK(nbx::reduceMultiEx(b.dsts.data(), (int)b.dsts.size(), b.srcs.data(), n, b.len, c.dt, c.op, n, 1,
                                    (ncclStream_t)stream, nbx::kReduceAcquireSystem));
   }
   // 3. AllReduce with n > NBX_MAX_DSTS: gather the peers' reduced blocks
@@ -1357,35 +1352,18 @@ ncclResult_t mpRunBatch(ncclComm* comm, const std::vector<MpCall>& calls,
   HIPCHECK(hipStreamIsCapturing(stream, &capture));
   const bool capturing = capture != hipStreamCaptureStatusNone;
   NCCLCHECK(mpEvictMappings(mp, alls[lo][me].seq, capturing));
-  const size_t m = hi - lo;
-  std::vector<std::vector<const void*>> srcs(m);
-  std::vector<std::vector<void*>> dsts(m);
-  std::vector<size_t> lens(m);
-  for (size_t k = 0; k < m; k++) {
+  std::vector<RankBlock> blocks;
+  std::vector<const PendingColl*> colls;
+  for (size_t k = lo; k < hi; k++) {
     std::vector<const char*> sendP;
     std::vector<char*> recvP;
-    NCCLCHECK(mpMapCall(comm, calls[lo + k], alls[lo + k], capturing, &sendP, &recvP));
-    mpDirectBlock(calls[lo + k], n, me, sendP, recvP, &srcs[k], &dsts[k], &lens[k]);
+    NCCLCHECK(mpMapCall(comm, calls[k], alls[k], capturing, &sendP, &recvP));
+    blocks.push_back(mpDirectBlock(calls[k], n, me, sendP, recvP));
+    colls.push_back(&calls[k]);
   }
-  NBX_TRACE("mp group batch of %zu collectives", m);
+  NBX_TRACE("mp group batch of %zu collectives", hi - lo);
   NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
-  size_t i = 0;
-  while (i < m) {   // one batched launch set per run of equal (datatype, op)
-    const MpCall& ci = calls[lo + i];
-    std::vector<nbxReduceTask> tasks;
-    size_t j = i;
-    for (; j < m; j++) {
-      const MpCall& cj = calls[lo + j];
-      if (cj.dt != ci.dt || cj.op.op != ci.op.op || cj.op.scalarArg != ci.op.scalarArg ||
-          cj.op.scalarArgIsPtr != ci.op.scalarArgIsPtr)
-        break;
-      if (lens[j] == 0) continue;
-      tasks.push_back({dsts[j].data(), (int)dsts[j].size(), srcs[j].data(), n, lens[j]});
-    }
-    NCCLCHECK(nbx::reduceMultiBatchEx(tasks.data(), (int)tasks.size(), ci.dt, ci.op, /*nPreOpSrcs=*/n,
-                                      /*postOp=*/1, (ncclStream_t)stream, nbx::kReduceAcquireSystem));
-    i = j;
-  }
+  NCCLCHECK(foldBlocksBatched(colls, blocks, n, stream));
   NCCLCHECK(mpBarrier(comm, kSlotDone, stream));
   return ncclSuccess;
 }
