@@ -104,6 +104,10 @@ ncclResult_t nbxReduceMultiBatch(const nbxReduceTask* tasks, int nTasks,
  * shm.cc:86-114) — where an emulator's proxy/net buffers live. Data is chunked
  * (NBX_HOST_CHUNK_BYTES per source, default 16 MiB) through a two-slot device
  * staging ring so H2D, the reduction and D2H of consecutive chunks overlap.
+ * When every buffer is pinned and device-mapped (hipHostMalloc /
+ * hipHostRegister), the kernel instead reads and writes them in place over
+ * PCIe (zero-copy; env NBX_HOST_MODE=auto|staged|zerocopy, zerocopy on
+ * pageable memory: ncclInvalidArgument).
  * Ordered after prior work on `stream`; BLOCKING: returns when every host
  * destination holds the result. Same semantics and errors as nbxReduceMulti. */
 ncclResult_t nbxReduceMultiHost(void* const* hostDsts, int nDsts,

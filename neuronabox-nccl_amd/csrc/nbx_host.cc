@@ -14,6 +14,8 @@
 // concurrently (PCIe is full duplex; the reduce runs at HBM speed). Events
 // guard slot reuse (inputs: reduce k-2 done; output: D2H k-2 done). The call
 // is blocking: it returns when the host destinations hold the result.
+// Pinned, device-mapped buffers skip the ring: the reduce kernel reads and
+// writes them in place over PCIe (NBX_HOST_MODE selects).
 #include <hip/hip_runtime_api.h>
 
 #include <cstdlib>
@@ -79,6 +81,30 @@ ncclResult_t stageInit(HostStage& st) {
   return ncclSuccess;
 }
 
+// NBX_HOST_MODE: "staged" (always the device staging ring), "zerocopy"
+// (the kernel reads and writes pinned host memory directly over PCIe when
+// every buffer is pinned and device-mapped), "auto" (default: zero-copy for
+// pinned buffers, staged otherwise).
+enum HostMode { kHostAuto, kHostStaged, kHostZeroCopy };
+HostMode hostMode() {   // read per call (a blocking, PCIe-bound call: getenv is noise)
+  const char* v = std::getenv("NBX_HOST_MODE");
+  if (v && std::strcmp(v, "staged") == 0) return kHostStaged;
+  if (v && std::strcmp(v, "zerocopy") == 0) return kHostZeroCopy;
+  return kHostAuto;
+}
+
+// Device address of pinned, device-mapped host memory (nullptr if `p` is
+// pageable or not mapped for this device).
+void* mappedAlias(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || a.devicePointer == nullptr || a.hostPointer == nullptr) return nullptr;
+  return (char*)a.devicePointer + ((const char*)p - (const char*)a.hostPointer);
+}
+
 }  // namespace
 
 extern "C" __attribute__((visibility("default"))) ncclResult_t nbxReduceMultiHost(
@@ -93,6 +119,23 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t nbxReduceMultiHos
     if (hostSrcs[s] == nullptr) return ncclInvalidArgument;
   for (int d = 0; d < nDsts; d++)
     if (hostDsts[d] == nullptr) return ncclInvalidArgument;
+  // zero-copy: every buffer pinned and mapped — one kernel reads the sources
+  // over PCIe and writes the destinations back over PCIe (full duplex), no
+  // staging copies
+  if (hostMode() != kHostStaged) {
+    const void* zs[NBX_MAX_SRCS];
+    void* zd[NBX_MAX_DSTS];
+    bool all = true;
+    for (int s = 0; s < nSrcs && all; s++) all = (zs[s] = mappedAlias(hostSrcs[s])) != nullptr;
+    for (int d = 0; d < nDsts && all; d++) all = (zd[d] = mappedAlias(hostDsts[d])) != nullptr;
+    if (all) {
+      ncclResult_t r = nbxReduceMulti(zd, nDsts, zs, nSrcs, count, datatype, op, nPreOpSrcs, postOp, stream);
+      if (r != ncclSuccess) return r;
+      HCHECK(hipStreamSynchronize((hipStream_t)stream));
+      return ncclSuccess;
+    }
+    if (hostMode() == kHostZeroCopy) return ncclInvalidArgument;   // zero-copy forced on unpinned memory
+  }
   int dev = 0;
   HCHECK(hipGetDevice(&dev));
   if (dev < 0 || dev >= kMaxDev) return ncclInternalError;

@@ -123,7 +123,7 @@ def main():
     if "e2e" in what:
         # host-staged: sources start in pinned host memory (the proxy/net staging
         # buffers), result returns to pinned host memory
-        for nsrc, mib in ((2, 4), (8, 256), (2, 256)):
+        for nsrc, mib in ((2, 4), (8, 256), (2, 256), (2, 1), (8, 16), (2, 64)):
             n = (mib << 20) // 4
             hs = [torch.rand(n).pin_memory() for _ in range(nsrc)]
             ho = torch.empty(n).pin_memory()
@@ -141,18 +141,26 @@ def main():
             ms = timed(torch, run, 5 if mib > 16 else 20)
             kms = timed(torch, lambda: nbx.reduce_multi([do.data_ptr()], sp, n, 7, op, 0, False, st), 10)
             alg = (nsrc + 1) * n * 4
-            # pipelined host-staged entry point (blocking call; wall clock)
+            # host entry point (blocking call; wall clock): the pipelined staging
+            # ring, and zero-copy (the kernel reads / writes the pinned buffers)
             hp = [h.data_ptr() for h in hs]
-            nbx.reduce_multi_host([ho.data_ptr()], hp, n, 7, op, 0, False, st)
             reps = 3 if mib > 16 else 20
-            t0 = time.perf_counter()
-            for _ in range(reps):
+            modes = {}
+            for mode in ("staged", "zerocopy"):
+                os.environ["NBX_HOST_MODE"] = mode
                 nbx.reduce_multi_host([ho.data_ptr()], hp, n, 7, op, 0, False, st)
-            pms = (time.perf_counter() - t0) * 1e3 / reps
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    nbx.reduce_multi_host([ho.data_ptr()], hp, n, 7, op, 0, False, st)
+                modes[mode] = (time.perf_counter() - t0) * 1e3 / reps
+            os.environ.pop("NBX_HOST_MODE")
+            pms = modes["staged"]
+            zms = modes["zerocopy"]
             print(json.dumps({"what": "e2e", "nsrc": nsrc, "MiB_per_input": mib, "e2e_ms": round(ms, 4),
                               "e2e_alg_GBps": round(gbps(alg, ms), 1), "kernel_ms": round(kms, 4),
                               "kernel_GBps": round(gbps(alg, kms), 1),
                               "pipelined_host_ms": round(pms, 4), "pipelined_host_alg_GBps": round(gbps(alg, pms), 1),
+                              "zerocopy_ms": round(zms, 4), "zerocopy_alg_GBps": round(gbps(alg, zms), 1),
                               "pcie_bytes": alg}), flush=True)
             del hs, ho, ds, do
 

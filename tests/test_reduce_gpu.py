@@ -422,6 +422,51 @@ def test_host_staged_reduce(nbx, oracle, torch_gpu, monkeypatch, dtype, devop, c
         assert_same(o, exp, dtype)
 
 
+@pytest.mark.parametrize("mode", ["auto", "zerocopy", "staged"])
+@pytest.mark.parametrize("dtype,devop,count", [(7, 0, (1 << 20) + 13), (6, 3, 5000), (4, 2, 3 << 20), (2, 4, 777)])
+def test_host_pinned_zero_copy(nbx, oracle, torch_gpu, monkeypatch, mode, dtype, devop, count):
+    """nbxReduceMultiHost on pinned (torch pin_memory) buffers: zero-copy — the
+    kernel reads and writes host memory over PCIe — under auto / zerocopy, the
+    staging ring under staged; a shared misalignment included (offset views)."""
+    torch = torch_gpu
+    monkeypatch.setenv("NBX_HOST_MODE", mode)
+    monkeypatch.setenv("NBX_HOST_CHUNK_BYTES", str(256 << 10))
+    rng = np.random.default_rng(count + dtype)
+    nsrc = 4
+    srcs = oracle.random_inputs(dtype, nsrc, count, seed=int(rng.integers(1 << 20)))
+    arg = op_arg(oracle, dtype, devop, rng)
+    npre = 2 if devop == 3 else 0
+    st = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st).itemsize
+    off = eb if eb < 16 else 0   # every pointer one element past 16-B alignment
+    pins = [torch.empty(count * eb + 64, dtype=torch.uint8).pin_memory() for _ in range(nsrc + 2)]
+    for p, x in zip(pins, srcs):
+        p.numpy()[off:off + count * eb] = x.view(np.uint8)
+    for p in pins[nsrc:]:
+        p.numpy()[:] = 0x5A
+    op = nbx.DevRedOpFull()
+    op.op, op.scalarArg = devop, arg
+    sp = [p.data_ptr() + off for p in pins[:nsrc]]
+    dp = [p.data_ptr() + off for p in pins[nsrc:]]
+    nbx.reduce_multi_host(dp, sp, count, dtype, op, npre, devop == 4, torch.cuda.current_stream().cuda_stream)
+    exp = oracle.reduce_multi(srcs, dtype, devop, arg, npre, devop == 4, threads=8)[0]
+    for p in pins[nsrc:]:
+        got = p.numpy()[off:off + count * eb].view(st)
+        assert_same(got, exp, dtype)
+        assert (p.numpy()[:off] == 0x5A).all() and (p.numpy()[off + count * eb:] == 0x5A).all()
+
+
+def test_host_zero_copy_refuses_pageable(nbx, torch_gpu, monkeypatch):
+    """NBX_HOST_MODE=zerocopy with a pageable buffer: ncclInvalidArgument, nothing run."""
+    monkeypatch.setenv("NBX_HOST_MODE", "zerocopy")
+    a = np.ones(1024, dtype=np.float32)
+    o = np.zeros(1024, dtype=np.float32)
+    with pytest.raises(nbx.NcclError):
+        nbx.reduce_multi_host([o.ctypes.data], [a.ctypes.data], 1024, 7, nbx.DevRedOpFull(), 0, False,
+                              torch_gpu.cuda.current_stream().cuda_stream)
+    assert (o == 0).all()
+
+
 def test_beyond_32bit_counts(nbx, torch_gpu):
     """Maximum sizes: element counts and byte offsets past 2^32 (u8 sum of
     4 GiB + 37 elements; f32 sum of 2^30 + 5 elements = 4 GiB + 20 B per
