@@ -111,6 +111,38 @@ def _pmc_traffic():
     return None
 
 
+def host_e2e_leg(torch, nbx, srcs, out, stream, op, reps: int = 2):
+    """BASELINE: the path starts and ends in host memory. Config B with the
+    8 inputs and the output in pinned host memory: nbxReduceMultiHost
+    (zero-copy: the kernel reads / writes the pinned buffers over PCIe) and
+    the naive H2D -> reduce -> D2H sequence. PCIe-inclusive; never `value`."""
+    f32 = int(nbx.ncclDataType.ncclFloat32)
+    hs = [s.cpu().pin_memory() for s in srcs]   # the same seeded inputs
+    ho = torch.empty(COUNT, dtype=torch.float32).pin_memory()
+    sh = stream.cuda_stream
+    hp = [h.data_ptr() for h in hs]
+    nbx.reduce_multi_host([ho.data_ptr()], hp, COUNT, f32, op, 0, False, sh)   # warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        nbx.reduce_multi_host([ho.data_ptr()], hp, COUNT, f32, op, 0, False, sh)
+    zms = (time.perf_counter() - t0) * 1e3 / reps
+    ok = bool(torch.equal(ho[:1 << 16], out[:1 << 16].cpu()))
+    dptr = [s.data_ptr() for s in srcs]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for h, d in zip(hs, srcs):
+            d.copy_(h, non_blocking=True)
+        nbx.reduce_multi([out.data_ptr()], dptr, COUNT, f32, op, 0, False, sh)
+        ho.copy_(out, non_blocking=True)
+        torch.cuda.synchronize()
+    nms = (time.perf_counter() - t0) * 1e3 / reps
+    return {"what": "config B with inputs and output in pinned host memory (PCIe-inclusive; not `value`)",
+            "zero_copy_ms": round(zms, 3), "zero_copy_GiBps": round(ALG_BYTES / (zms * 1e-3) / 2**30, 2),
+            "naive_h2d_reduce_d2h_ms": round(nms, 3),
+            "naive_GiBps": round(ALG_BYTES / (nms * 1e-3) / 2**30, 2), "matches_device_result": ok}
+
+
 def cpu_baseline(seconds: float = 1.5):
     """Oracle (C port of the reference semantics) on host cores, same workload
     shape, bounded sample: passes over the full config-B workload for about
@@ -440,6 +472,8 @@ def main():
         "cpu_baseline": None,
         "collective": None,
     }
+    if world == 1 and os.environ.get("NBX_BENCH_E2E", "1") != "0" and not args.no_cpu_baseline:
+        result["host_e2e"] = host_e2e_leg(torch, nbx, srcs, out, stream, op)
     if child is not None:
         del srcs, out
         torch.cuda.empty_cache()
