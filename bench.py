@@ -361,6 +361,12 @@ def rccl_leg(world: int):
         want = float(world * (world + 1) // 2)
         if not bool((y == want).all().item()):
             out["ok"] = False
+        # xGMI transport alone (reported separately from the reduce):
+        # the all-gather of the same 1 GiB moves what the reduce-scatter moves,
+        # with no reduction at all
+        t = timed(lambda: dist.all_gather_into_tensor(x, y), 5)
+        out["allgather_transport"] = {"ms": round(t * 1e3, 4), "algbw_GBs": round(S / t / 1e9, 2),
+                                      "busbw_GBs": round(S / t / 1e9 * (world - 1) / world, 2)}
         for name, cnt in (("allreduce_1MiB_us", 256 << 10), ("allreduce_4KiB_us", 1024)):
             z = torch.ones(cnt, device="cuda")
             out[name] = round(timed(lambda: dist.all_reduce(z), 100) * 1e6, 2)
