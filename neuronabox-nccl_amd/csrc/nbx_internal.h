@@ -6,6 +6,7 @@
 
 namespace nbx {
 struct LLArgs;
+struct RingArgs;
 // nbxReduceMulti with internal flags: kReduceAcquireSystem makes every
 // workgroup issue a system-scope acquire before its first load (sources in
 // peer GPU memory, written before the launch and ordered by a flag barrier).
@@ -21,6 +22,9 @@ ncclResult_t reduceMultiBatchEx(const nbxReduceTask* tasks, int nTasks, ncclData
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
 // The same for the LL128 kernel (args.nLines 64-byte lines).
 ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
+// Pipelined ring AllReduce (nbx_ring.h), `grid` workgroups = slices per chunk.
+ncclResult_t launchRingAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, RingArgs& args, unsigned grid,
+                                 hipStream_t stream);
 // LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
                                    hipStream_t stream);

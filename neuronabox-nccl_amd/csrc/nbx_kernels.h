@@ -261,6 +261,12 @@ __global__ __launch_bounds__(kBlock) void kReduceBatch(BatchArgs a) {
   }
 }
 
+}  // namespace nbx
+
+#include "nbx_ring.h"   // uses foldStore / ldPack above
+
+namespace nbx {
+
 // ---------------------------------------------------------------------------
 // Launch table for one functor.
 
@@ -293,6 +299,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;
+  ks.ring = (const void*)&kRingAllReduce<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.valid = 1;
   return ks;

@@ -52,4 +52,36 @@ struct LLArgs {
   int32_t root;            // kLLReduce
 };
 
+// Pipelined ring AllReduce (nbx_ring.h kRingAllReduce): device-resident
+// sequencing, as LLState.
+struct RingState {
+  uint64_t seq;      // completed ring calls
+  uint64_t arrive;   // workgroups of the running launch that have finished
+};
+
+constexpr int kRingMaxGrid = 256;   // slices per chunk = workgroups; one progress word each
+
+struct RingArgs {
+  const void* sendMe;     // this rank's input
+  const void* sendLeft;   // the left neighbour's input (peer mapping): step 0 reads it raw
+  void* recvMe;           // this rank's output: partials of steps 0..n-3 live here
+  const void* recvLeft;   // the left neighbour's output (peer mapping): its partials
+  void* outs[8];          // last step: rank (me + k) % n's output for k < nOuts (push-gather)
+  uint64_t* myProgress;   // [kRingMaxGrid] words the LEFT neighbour posts (uncached, this rank's memory)
+  uint64_t* rightProgress;// the right neighbour's words (peer mapping): this rank posts there
+  RingState* state;
+  uint64_t total;         // elements of the message
+  uint64_t blockElts;     // direct-schedule block (multiple of 16 B / element)
+  uint64_t slicePacks;    // 16-B packs per slice (one slice per workgroup per chunk)
+  uint64_t arg;
+  const void* argPtr;
+  const volatile int* abortWord;
+  volatile int* errWord;
+  uint64_t timeoutTicks;
+  int32_t rank;
+  int32_t nRanks;
+  int32_t nOuts;          // 1: own output only (gather follows), n: push to every rank
+  int32_t pad;
+};
+
 }  // namespace nbx

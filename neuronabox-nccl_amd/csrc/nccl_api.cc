@@ -692,6 +692,11 @@ struct MpState {
   uint64_t l128Bytes = 0;
   int protoMask = 0;                // NCCL_PROTO at init: kProtoLL | kProtoLL128 | kProtoSimple
   bool ring = false;                // NCCL_ALGO=Ring at init
+  bool ringPipeline = true;         // ring as the pipelined kernel (nbx_ring.h); NBX_RING_PIPELINE=0: per-step kernels
+  uint64_t* ringProg = nullptr;     // [kRingMaxGrid] progress words the left neighbour posts (uncached)
+  uint64_t* rightRingProg = nullptr;// the right neighbour's words (peer mapping)
+  nbx::RingState* ringState = nullptr;
+  unsigned ringMaxGrid = nbx::kRingMaxGrid;   // NBX_RING_MAX_GRID
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
 };
 
@@ -701,6 +706,7 @@ struct MpInitInfo {
   hipIpcMemHandle_t flagsHandle;
   hipIpcMemHandle_t llHandle;
   hipIpcMemHandle_t l128Handle;
+  hipIpcMemHandle_t ringHandle;
   uint64_t llMaxBytes;
   uint64_t l128MaxBytes;
   uint64_t l128OneShotMax;
@@ -894,6 +900,13 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   if (cm && std::atol(cm) > 0) mp->mapsMax = (size_t)std::atol(cm);
   mp->protoMask = protoFromEnv();
   mp->ring = algoRingFromEnv();
+  {
+    const char* v = std::getenv("NBX_RING_PIPELINE");
+    mp->ringPipeline = !(v && std::strcmp(v, "0") == 0);
+    const char* gcap = std::getenv("NBX_RING_MAX_GRID");
+    const long gv = (gcap && *gcap) ? std::atol(gcap) : nbx::kRingMaxGrid;
+    mp->ringMaxGrid = (unsigned)(gv < 1 ? 1 : gv > nbx::kRingMaxGrid ? nbx::kRingMaxGrid : gv);
+  }
   NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
   HIPCHECK(allocSyncMem((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
   HIPCHECK(hipMemset(mp->flags, 0, kNumSlots * sizeof(uint64_t)));
@@ -901,6 +914,10 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   HIPCHECK(hipMemset(mp->epochs, 0, kNumSlots * sizeof(uint64_t)));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
   HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
+  HIPCHECK(allocSyncMem((void**)&mp->ringProg, nbx::kRingMaxGrid * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->ringProg, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
+  HIPCHECK(hipMalloc((void**)&mp->ringState, sizeof(nbx::RingState)));
+  HIPCHECK(hipMemset(mp->ringState, 0, sizeof(nbx::RingState)));
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mp->hostWords, 0, 64);
   HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
@@ -943,6 +960,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
   if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
+  HIPCHECK(hipIpcGetMemHandle(&mine.ringHandle, mp->ringProg));
   std::vector<MpInitInfo> all(c->nRanks);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
   std::vector<uint64_t*> table(c->nRanks), llTable(c->nRanks), l128Table(c->nRanks, nullptr);
@@ -987,6 +1005,11 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
       mp->peerL128Maps.push_back(w);
       l128Table[j] = (uint64_t*)w;
     }
+    if (j == (c->rank + 1) % c->nRanks) {   // the ring's right neighbour: this rank posts its progress there
+      void* w = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].ringHandle, hipIpcMemLazyEnablePeerAccess));
+      mp->rightRingProg = (uint64_t*)w;
+    }
   }
   HIPCHECK(hipMalloc((void**)&mp->peerFlagsDev, c->nRanks * sizeof(uint64_t*)));
   HIPCHECK(hipMemcpy(mp->peerFlagsDev, table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
@@ -1015,6 +1038,9 @@ void mpFree(ncclComm* c) {
   for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerL128Maps) (void)hipIpcCloseMemHandle(p);
+  if (mp->rightRingProg) (void)hipIpcCloseMemHandle(mp->rightRingProg);
+  if (mp->ringProg) (void)hipFree(mp->ringProg);
+  if (mp->ringState) (void)hipFree(mp->ringState);
   if (mp->peerL128Dev) (void)hipFree(mp->peerL128Dev);
   if (mp->l128) (void)hipFree(mp->l128);
   if (mp->peerFlagsDev) (void)hipFree(mp->peerFlagsDev);
@@ -1239,6 +1265,42 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
     // Every rank works on a different chunk at each step, so all ring links
     // carry 1/n of the data concurrently.
     const int left = (me + n - 1) % n;
+    // pipelined: one kernel, slices flow through the ring on device progress
+    // words (nbx_ring.h). It needs 16-B aligned buffers, and every rank must
+    // choose it or none: decided from the exchanged offsets of all ranks
+    // (allocation bases are >= 256-B aligned, so an offset's alignment is the
+    // pointer's).
+    const int nOuts = push ? n : 1;
+    bool aligned = true;
+    for (const MpCallInfo& ai : all) aligned &= ((ai.sendOff | ai.recvOff) & 15u) == 0;
+    if (mp->ringPipeline && aligned) {
+      size_t o0, per;
+      blockRange(total, eb, n, 0, &o0, &per);
+      const uint64_t epp = (uint64_t)(16 / eb);
+      const uint64_t maxPacks = per / epp;
+      uint64_t grid = (maxPacks + 1023) / 1024;   // slices of >= 16 KiB
+      if (grid < 1) grid = 1;
+      if (grid > mp->ringMaxGrid) grid = mp->ringMaxGrid;
+      nbx::RingArgs ra{};
+      ra.sendMe = sendP[me];
+      ra.sendLeft = sendP[left];
+      ra.recvMe = recvP[me];
+      ra.recvLeft = recvP[left];
+      for (int k = 0; k < nOuts; k++) ra.outs[k] = recvP[(me + k) % n];
+      ra.myProgress = mp->ringProg;
+      ra.rightProgress = mp->rightRingProg;
+      ra.state = mp->ringState;
+      ra.total = total;
+      ra.blockElts = per;
+      ra.slicePacks = (maxPacks + grid - 1) / grid;
+      ra.abortWord = mp->hostWordsDev;
+      ra.errWord = mp->hostWordsDev + 1;
+      ra.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
+      ra.rank = me;
+      ra.nRanks = n;
+      ra.nOuts = nOuts;
+      NCCLCHECK(nbx::launchRingAllReduce(c.dt, c.op, ra, (unsigned)grid, stream));
+    } else {
     std::vector<void*> pushDsts;
     for (int st = 0; st < n - 1; st++) {
       const int ch = ((me - 2 - st) % n + n) % n;
@@ -1257,6 +1319,7 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
                                      nbx::kReduceAcquireSystem));
       }
       if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, 1ull << left, stream));
+    }
     }
   } else {
     // 2. direct reduce of this rank's block

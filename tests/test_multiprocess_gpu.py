@@ -100,6 +100,7 @@ def _blocks(count, eb, n):
 
 @pytest.mark.parametrize("n,algo,proto,cache", [(2, "direct", "LL,Simple", ""), (3, "direct", "LL,Simple", ""),
                                                 (3, "ring", "LL,Simple", ""), (4, "ring", "LL,Simple", ""),
+                                                (5, "ring", "LL,Simple", ""), (4, "ring-steps", "LL,Simple", ""),
                                                 (3, "direct", "", ""), (3, "direct", "LL,Simple", "2")])
 def test_multiprocess_collectives(nbx, oracle, n, algo, proto, cache, monkeypatch):
     """NCCL_ALGO=Ring: NCCL's ring order (chunk c from rank c+1 to c, Fn(local,
@@ -113,7 +114,9 @@ def test_multiprocess_collectives(nbx, oracle, n, algo, proto, cache, monkeypatc
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
     monkeypatch.setenv("NCCL_PROTO", proto)
-    monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
+    monkeypatch.setenv("NCCL_ALGO", "Ring" if algo.startswith("ring") else "")
+    # ring: the pipelined kernel (nbx_ring.h); ring-steps: one kernel + barrier per step
+    monkeypatch.setenv("NBX_RING_PIPELINE", "0" if algo == "ring-steps" else "1")
     monkeypatch.setenv("NBX_IPC_CACHE_MAX", cache)
     res = _run_ranks(nbx, n, _child)
     _check_cases(oracle, n, res)
@@ -236,12 +239,17 @@ def _child_big(uid_bytes, rank, n, q):
         q.put((rank, "error", traceback.format_exc()))
 
 
-def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch):
+@pytest.mark.parametrize("algo", ["direct", "ring"])
+def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch, algo):
     """8 ranks (SURVEY config D's rank count), 64 MiB fp32 per rank, AllReduce
-    sum; every rank's output hash equals the oracle's ring-order result."""
+    sum; every rank's output hash equals the oracle's ring-order result —
+    direct schedule, and the pipelined ring (64 slices per chunk, so the 8
+    ranks' persistent grids stay co-resident on the one GPU)."""
     import hashlib
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "120")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "120")
+    monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
+    monkeypatch.setenv("NBX_RING_MAX_GRID", "64")
     n = 8
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
