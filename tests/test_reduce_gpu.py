@@ -303,6 +303,59 @@ def test_batch_large_sets(nbx, oracle, torch_gpu, dtype, nsrc):
     run_batch(nbx, oracle, torch_gpu, dtype, 0, 0, buckets)
 
 
+@pytest.mark.parametrize("dtype", [7, 6, 9])
+def test_batch_device_scalar_and_graph_replay(nbx, oracle, torch_gpu, dtype):
+    """Batched PreMulSum with the scalar in device memory (dereferenced by the
+    batch kernel while it runs), captured into a HIP graph and replayed after
+    the scalar and the inputs change: the kernel-argument table is captured by
+    value, the scalar and data are read at replay time."""
+    torch = torch_gpu
+    st_np = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st_np).itemsize
+    counts = [5000, 40000, 123, 77777]
+    nsrc = 3
+    dev = Dev(torch)
+    srcs = [[torch.empty(c * eb, dtype=torch.uint8, device="cuda") for _ in range(nsrc)] for c in counts]
+    outs = [torch.empty(c * eb, dtype=torch.uint8, device="cuda") for c in counts]
+    scal = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    op = nbx.DevRedOpFull()
+    op.op, op.scalarArgIsPtr, op.scalarArg = 3, 1, scal.data_ptr()
+    buckets = [([o.data_ptr()], [t.data_ptr() for t in ss], c) for ss, o, c in zip(srcs, outs, counts)]
+    s = torch.cuda.Stream()
+
+    def fill(it):
+        host = []
+        for k, (ss, c) in enumerate(zip(srcs, counts)):
+            xs = oracle.random_inputs(dtype, nsrc, c, seed=100 * it + k)
+            for t, x in zip(ss, xs):
+                t.copy_(torch.from_numpy(x.view(np.uint8).copy()))
+            host.append(xs)
+        arg = oracle.host_to_dev_redop(4, dtype, 2 + it)[1]   # Avg scalar 1/(2+it)
+        scal.copy_(torch.from_numpy(np.array([arg], dtype=np.uint64).view(np.uint8)))
+        return host, arg
+
+    host, arg = fill(0)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        nbx.reduce_multi_batch(buckets, dtype, op, 1, False, s.cuda_stream)   # eager
+    s.synchronize()
+    for xs, o in zip(host, outs):
+        exp = oracle.reduce_multi(xs, dtype, 3, arg, 1, False)[0]
+        assert_same(o.cpu().numpy().view(st_np), exp, dtype)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        nbx.reduce_multi_batch(buckets, dtype, op, 1, False, s.cuda_stream)
+    for it in (1, 2):
+        host, arg = fill(it)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for xs, o in zip(host, outs):
+            exp = oracle.reduce_multi(xs, dtype, 3, arg, 1, False)[0]
+            assert_same(o.cpu().numpy().view(st_np), exp, dtype)
+    del dev
+
+
 def test_batch_mixed_bucket_sweep_fp16_bf16(nbx, oracle, torch_gpu):
     """Config C shape: 8-source fp16 and bf16 sums over 1..16 MiB buckets in one
     batch — by default the buckets that fill the GPU alone take the big-tile
