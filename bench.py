@@ -417,8 +417,18 @@ def main():
     sptr = [t.data_ptr() for t in srcs]
     f32 = int(nbx.ncclDataType.ncclFloat32)
 
+    # one step = one nbxReduceMulti launch through the C ABI; the pointer arrays
+    # are built once so the host enqueue (~µs) never leaves the GPU idle
+    import ctypes
+    lib = nbx.load_library()
+    d_arr = (ctypes.c_void_p * 1)(*dptr)
+    s_arr = (ctypes.c_void_p * N_SRCS)(*sptr)
+    sh_c = ctypes.c_void_p(sh)
+
     def step():
-        nbx.reduce_multi(dptr, sptr, COUNT, f32, op, 0, False, sh)
+        rc = lib.nbxReduceMulti(d_arr, 1, s_arr, N_SRCS, COUNT, f32, op, 0, 0, sh_c)
+        if rc != 0:
+            raise RuntimeError(f"nbxReduceMulti failed: {rc}")
 
     for _ in range(args.warmup):
         step()
