@@ -36,6 +36,12 @@ int nbxDebugProtoMask(const char* ncclProto);
 int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
                         uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax);
 
+/* The protocol set a communicator runs with (bits as nbxDebugProtoMask): its
+ * NCCL_PROTO at creation, minus LL128 if the creation-time LL128 self-test
+ * failed (multi-process communicators; -1 for others or a bad handle).
+ * NBX_LL128_SELFTEST_FAIL=1 makes that self-test report a failure (test hook). */
+int nbxDebugCommProtoMask(ncclComm_t comm);
+
 #ifdef __cplusplus
 }
 #endif

@@ -891,6 +891,8 @@ hipError_t allocSyncMem(void** p, size_t bytes) {
   return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
 }
 
+ncclResult_t mpLL128SelfTest(ncclComm* c);
+
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   MpState* mp = new MpState();
   c->mp = mp;
@@ -1024,6 +1026,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   std::vector<int> sink(c->nRanks);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), sink.data()));
   NCCLCHECK(mpSetupShmx(c, id));
+  NCCLCHECK(mpLL128SelfTest(c));
   info("comm %p rank %d nranks %d device %d: multi-process communicator ready", (void*)c, c->rank, c->nRanks,
        c->device);
   return ncclSuccess;
@@ -1354,6 +1357,81 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
   std::vector<MpCallInfo> all;
   NCCLCHECK(mpExchangeCall(comm, c, 0, &all));
   return mpRunSimple(comm, c, all);
+}
+
+// LL128 correctness probe at communicator creation. LL128 relies on a 64-byte
+// line written by one store instruction arriving whole (the flag in its last
+// 8 bytes vouches for the 56 payload bytes, nbx_ll.h). That holds for every
+// configuration measured here, but it is a property of the fabric between the
+// GPUs of this communicator, so each communicator checks it before use:
+// NBX_LL128_SELFTEST_ITERS (default 24; 0 = skip) AllReduces of integer data
+// that changes every call, at one-shot and at two-shot sizes, each result
+// compared exactly on the host. If any rank sees any wrong element, every rank
+// drops LL128 from its protocol set (decided from an allgather, so the choice
+// stays identical everywhere) and LL / Simple carry those sizes.
+ncclResult_t mpLL128SelfTest(ncclComm* c) {
+  MpState* mp = c->mp;
+  if (!(mp->protoMask & kProtoLL128) || mp->l128MaxBytes == 0) return ncclSuccess;
+  const char* v = std::getenv("NBX_LL128_SELFTEST_ITERS");
+  const long iters = (v && *v) ? std::atol(v) : 24;
+  if (iters <= 0) return ncclSuccess;
+  const int n = c->nRanks, me = c->rank;
+  // one-shot (just above the LL limit) and two-shot (n > 2, above the one-shot limit) sizes
+  std::vector<size_t> counts = {(size_t)(mp->llMaxBytes / 4 + 1024)};
+  const uint64_t twoShot = std::min<uint64_t>(mp->l128OneShotMax * 2, mp->l128MaxBytes);
+  if (n > 2 && twoShot > mp->l128OneShotMax) counts.push_back((size_t)(twoShot / 4 - 13));
+  size_t maxCount = 0;
+  for (size_t k : counts) maxCount = std::max(maxCount, k);
+  DevGuard g(c->device);
+  hipStream_t st = nullptr;
+  int32_t* dSend = nullptr;
+  int32_t* dRecv = nullptr;
+  HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIPCHECK(hipMalloc((void**)&dSend, maxCount * sizeof(int32_t)));
+  HIPCHECK(hipMalloc((void**)&dRecv, maxCount * sizeof(int32_t)));
+  std::vector<int32_t> hIn(maxCount), hOut(maxCount);
+  nbxDevRedOpFull sum{nbxDevSum, 0, 0};
+  int32_t bad = 0;
+  ncclResult_t r = ncclSuccess;
+  for (size_t count : counts) {
+    for (long it = 0; it < iters && r == ncclSuccess; it++) {
+      for (size_t i = 0; i < count; i++) hIn[i] = (int32_t)((i * 7 + (size_t)me * 13 + (size_t)it * 101) % 1000);
+      if (hipMemcpyAsync(dSend, hIn.data(), count * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+        r = ncclUnhandledCudaError;
+        break;
+      }
+      const MpCall call{kAllReduce, dSend, dRecv, count, ncclInt32, sum, 0, st};
+      r = runMpColl(c, call);
+      if (r != ncclSuccess) break;
+      if (hipMemcpyAsync(hOut.data(), dRecv, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        r = ncclUnhandledCudaError;
+        break;
+      }
+      for (size_t i = 0; i < count && !bad; i++) {
+        int64_t want = 0;
+        for (int q = 0; q < n; q++) want += (int64_t)((i * 7 + (size_t)q * 13 + (size_t)it * 101) % 1000);
+        if (hOut[i] != (int32_t)want) bad = 1;
+      }
+    }
+  }
+  const char* fail = std::getenv("NBX_LL128_SELFTEST_FAIL");   // test hook: simulate a torn line
+  if (fail && std::strcmp(fail, "1") == 0) bad = 1;
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(dSend);
+  (void)hipFree(dRecv);
+  (void)hipStreamDestroy(st);
+  if (r != ncclSuccess) return r;
+  std::vector<int32_t> all(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &bad, sizeof(bad), all.data()));
+  bool anyBad = false;
+  for (int32_t b : all) anyBad |= b != 0;
+  if (anyBad) {
+    warn("comm %p rank %d: LL128 self-test found torn lines on this fabric; LL128 disabled for this communicator",
+         (void*)c, me);
+    mp->protoMask &= ~kProtoLL128;
+  }
+  return ncclSuccess;
 }
 
 // ---------------------------------------------------------------------------
@@ -1869,6 +1947,11 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
 }
 
 NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
+
+NBX_EXPORT int nbxDebugCommProtoMask(ncclComm_t comm) {
+  if (comm == nullptr || comm->magic != kCommMagic || comm->mp == nullptr) return -1;
+  return comm->mp->protoMask;
+}
 
 NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
                                    uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax) {

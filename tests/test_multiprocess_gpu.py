@@ -250,6 +250,7 @@ def test_multiprocess_8_ranks_config_d_shape(nbx, oracle, monkeypatch, algo):
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "120")
     monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
     monkeypatch.setenv("NBX_RING_MAX_GRID", "64")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")   # the creation-time LL128 self-test
     n = 8
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
@@ -584,6 +585,59 @@ def _child_failure(uid_bytes, rank, q, evq):
     except Exception:
         import traceback
         q.put((rank, "error", traceback.format_exc()))
+
+
+def _child_selftest(uid_bytes, rank, n, q):
+    try:
+        import ctypes
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        lib.nbxDebugCommProtoMask.argtypes = [ctypes.c_void_p]
+        lib.nbxDebugCommProtoMask.restype = ctypes.c_int
+        mask = lib.nbxDebugCommProtoMask(comm.handle)
+        st = torch.cuda.current_stream().cuda_stream
+        bad = 0
+        for cnt in (30000, 300001):   # LL128 one-shot / two-shot sizes (Simple without LL128)
+            idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+            x = torch.remainder(idx * 3 + 11 * rank, 257)
+            y = torch.empty_like(x)
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, st)
+            torch.cuda.synchronize()
+            want = sum(torch.remainder(idx * 3 + 11 * r, 257) for r in range(n))
+            bad += int((y != want).sum())
+        comm.destroy()
+        q.put((rank, "ok", (mask, bad)))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("fail", [False, True])
+def test_multiprocess_ll128_selftest(nbx, monkeypatch, fail):
+    """ncclCommInitRank probes LL128 (AllReduces checked exactly) before using
+    it; a failed probe on any rank drops LL128 on every rank (simulated with
+    NBX_LL128_SELFTEST_FAIL=1) and the LL128-sized calls still come out right
+    on the Simple path."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
+    monkeypatch.delenv("NCCL_PROTO", raising=False)
+    monkeypatch.delenv("NCCL_ALGO", raising=False)
+    if fail:
+        monkeypatch.setenv("NBX_LL128_SELFTEST_FAIL", "1")
+    else:
+        monkeypatch.delenv("NBX_LL128_SELFTEST_FAIL", raising=False)
+    n = 3
+    res = _run_ranks(nbx, n, _child_selftest)
+    for r in range(n):
+        mask, bad = res[r]
+        assert bad == 0, (r, bad)
+        assert mask == (5 if fail else 7), (r, mask)   # LL|Simple after a failed probe, else all three
 
 
 def _child_abort(uid_bytes, rank, q, evq):
