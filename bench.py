@@ -298,6 +298,9 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
         rows = [r.get("sweep_" + name + "_us") for r in allres]
         sw[name] = None if any(v is None for v in rows) else [max(col) for col in zip(*rows)]
     out["protocol_sweep"] = sw
+    # LL128 kept by every rank's creation-time probe (else LL / Simple carried those sizes)
+    act = [r.get("ll128_active") for r in allres]
+    out["ll128_active"] = None if any(a is None for a in act) else all(act)
     return out
 
 

@@ -165,6 +165,13 @@ def run(ids, rank, world, dev):
             res["errors"].append(f"{name}: {bad} elements differ")
 
     _progress("communicators ready")
+    # LL128 survives the creation-time probe on this fabric (bit 1 of the comm's protocol set)
+    import ctypes
+    lib = nbx.load_library()
+    lib.nbxDebugCommProtoMask.argtypes = [ctypes.c_void_p]
+    lib.nbxDebugCommProtoMask.restype = ctypes.c_int
+    res["proto_mask"] = int(lib.nbxDebugCommProtoMask(comm.handle))
+    res["ll128_active"] = bool(res["proto_mask"] & 2)
     for name, c in (("allreduce_direct", comm), ("allreduce_ring", comm_ring)):
         y.zero_()
         c.all_reduce(x.data_ptr(), y.data_ptr(), COUNT, F32, SUM, st)
