@@ -692,6 +692,7 @@ struct MpState {
   uint64_t l128Bytes = 0;
   int protoMask = 0;                // NCCL_PROTO at init: kProtoLL | kProtoLL128 | kProtoSimple
   bool ring = false;                // NCCL_ALGO=Ring at init
+  bool multiGpu = false;            // the ranks span more than one physical GPU (PCI key)
   bool ringPipeline = true;         // ring as the pipelined kernel (nbx_ring.h); NBX_RING_PIPELINE=0: per-step kernels
   uint64_t* ringProg = nullptr;     // [kRingMaxGrid] progress words the left neighbour posts (uncached)
   uint64_t* rightRingProg = nullptr;// the right neighbour's words (peer mapping)
@@ -707,6 +708,7 @@ struct MpInitInfo {
   hipIpcMemHandle_t llHandle;
   hipIpcMemHandle_t l128Handle;
   hipIpcMemHandle_t ringHandle;
+  uint64_t pciKey;   // (domain, bus, device) of this rank's GPU: identifies it across processes
   uint64_t llMaxBytes;
   uint64_t l128MaxBytes;
   uint64_t l128OneShotMax;
@@ -963,8 +965,16 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
   if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
   HIPCHECK(hipIpcGetMemHandle(&mine.ringHandle, mp->ringProg));
+  {
+    int dom = 0, bus = 0, dv = 0;
+    (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device);
+    (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device);
+    (void)hipDeviceGetAttribute(&dv, hipDeviceAttributePciDeviceId, c->device);
+    mine.pciKey = ((uint64_t)(uint32_t)dom << 32) | ((uint64_t)(uint32_t)bus << 8) | (uint64_t)(uint32_t)dv;
+  }
   std::vector<MpInitInfo> all(c->nRanks);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
+  for (int j = 0; j < c->nRanks; j++) mp->multiGpu |= all[j].pciKey != mine.pciKey;
   std::vector<uint64_t*> table(c->nRanks), llTable(c->nRanks), l128Table(c->nRanks, nullptr);
   for (int j = 0; j < c->nRanks; j++) {
     // every rank must pick the same protocol for the same call
@@ -1372,8 +1382,11 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
 ncclResult_t mpLL128SelfTest(ncclComm* c) {
   MpState* mp = c->mp;
   if (!(mp->protoMask & kProtoLL128) || mp->l128MaxBytes == 0) return ncclSuccess;
+  // only across GPUs (within one GPU the 64-byte line was stress-tested, DESIGN
+  // §6), unless NBX_LL128_SELFTEST_ITERS asks for it explicitly; multiGpu is
+  // the same on every rank (derived from every rank's PCI key)
   const char* v = std::getenv("NBX_LL128_SELFTEST_ITERS");
-  const long iters = (v && *v) ? std::atol(v) : 24;
+  const long iters = (v && *v) ? std::atol(v) : (mp->multiGpu ? 24 : 0);
   if (iters <= 0) return ncclSuccess;
   const int n = c->nRanks, me = c->rank;
   // one-shot (just above the LL limit) and two-shot (n > 2, above the one-shot limit) sizes

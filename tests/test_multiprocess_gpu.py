@@ -628,6 +628,7 @@ def test_multiprocess_ll128_selftest(nbx, monkeypatch, fail):
     monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
     monkeypatch.delenv("NCCL_PROTO", raising=False)
     monkeypatch.delenv("NCCL_ALGO", raising=False)
+    monkeypatch.setenv("NBX_LL128_SELFTEST_ITERS", "8")   # forced: the ranks share one GPU here
     if fail:
         monkeypatch.setenv("NBX_LL128_SELFTEST_FAIL", "1")
     else:
