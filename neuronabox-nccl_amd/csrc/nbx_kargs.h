@@ -58,6 +58,7 @@ struct BatchArgs {
 struct KernelSet {
   const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
+  const void* shifted;              // sources realigned against 16-B aligned destinations (kReduceShifted)
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)

@@ -176,6 +176,102 @@ __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Sources misaligned against the destinations (common_kernel.h:229-238 falls
+// back to sizeof(T) packs there). Here the destinations (which share one
+// alignment) stay 16-B packs, and each source is read as 16-B aligned packs
+// and realigned in registers: lane p loads packs p and p+1 of the source's
+// aligned-down base and funnel-shifts the 32 bytes by the source's byte
+// offset (v_alignbyte_b32; the offset is per source, so the shift case is
+// uniform). The second load mostly hits L2/L1 (it is the next lane's first),
+// so HBM traffic stays the algorithmic bytes. Memory safety: a 16-B aligned
+// pack never crosses a page, and every pack loaded holds at least one byte
+// of the source range, so no load can touch an unmapped page.
+__device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t m) {
+  const uint32_t b = m & 3u;   // byte shift inside a dword (0: plain dword select)
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u32x4 r;
+  switch (m >> 2) {   // uniform across the wave
+    case 0:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], b), __builtin_amdgcn_alignbyte(w[2], w[1], b),
+                __builtin_amdgcn_alignbyte(w[3], w[2], b), __builtin_amdgcn_alignbyte(w[4], w[3], b)};
+      break;
+    case 1:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[2], w[1], b), __builtin_amdgcn_alignbyte(w[3], w[2], b),
+                __builtin_amdgcn_alignbyte(w[4], w[3], b), __builtin_amdgcn_alignbyte(w[5], w[4], b)};
+      break;
+    case 2:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[3], w[2], b), __builtin_amdgcn_alignbyte(w[4], w[3], b),
+                __builtin_amdgcn_alignbyte(w[5], w[4], b), __builtin_amdgcn_alignbyte(w[6], w[5], b)};
+      break;
+    default:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[4], w[3], b), __builtin_amdgcn_alignbyte(w[5], w[4], b),
+                __builtin_amdgcn_alignbyte(w[6], w[5], b), __builtin_amdgcn_alignbyte(w[7], w[6], b)};
+      break;
+  }
+  return r;
+}
+
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kReduceShifted(KArgs a) {
+  using E = typename Fn::Elt;
+  constexpr int EPP = 16 / (int)sizeof(E);
+  acquirePeerData(a);
+  const Fn fn(loadArg<Fn>(a));
+  const uint64_t headBytes = (uint64_t)a.headElts * sizeof(E);
+  const int nSrcs = a.nSrcs, nDsts = a.nDsts;
+  const u32x4* base[kMaxKSrcs];
+  uint32_t sh[kMaxKSrcs];
+#pragma unroll
+  for (int s = 0; s < kMaxKSrcs; s++) {
+    const uintptr_t q = (uintptr_t)a.src[s < nSrcs ? s : 0] + headBytes;
+    sh[s] = (uint32_t)(q & 15u);
+    base[s] = (const u32x4*)(q - sh[s]);
+  }
+  u32x4* dst[kMaxKDsts];
+#pragma unroll
+  for (int d = 0; d < kMaxKDsts; d++) dst[d] = (u32x4*)((char*)a.dst[d] + headBytes);
+  const bool doPost = Fn::kHasPost && a.postOp;
+  const uint32_t preMask = a.preMask;
+  const uint64_t n = a.nPacks;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += stride) {
+    u32x4 lo[kMaxKSrcs], hi[kMaxKSrcs];
+#pragma unroll
+    for (int s = 0; s < kMaxKSrcs; s++) {
+      if (s < nSrcs) {   // plain (temporal) loads: the second one must find the line in L2
+        lo[s] = base[s][p];
+        hi[s] = sh[s] ? base[s][p + 1] : lo[s];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 acc = funnel16(lo[0], hi[0], sh[0]);
+    if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
+#pragma unroll
+    for (int s = 1; s < kMaxKSrcs; s++) {
+      if (s < nSrcs) {
+        u32x4 t = funnel16(lo[s], hi[s], sh[s]);
+        if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
+        acc = fn.redPack(acc, t);
+      }
+    }
+    if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
+    stPack(dst[0] + p, acc);
+#pragma unroll
+    for (int d = 1; d < kMaxKDsts; d++)
+      if (d < nDsts) stPack(dst[d] + p, acc);
+  }
+  // head (before the destinations' 16-B boundary) and tail elements
+  if (blockIdx.x == gridDim.x - 1) {
+    const int head = a.headElts;
+    const uint64_t tailStart = (uint64_t)head + n * EPP;
+    const int tail = (int)(a.nElts - tailStart);
+    const int t = (int)threadIdx.x;
+    if (t < head) reduceElt(fn, a, nSrcs, (uint64_t)t);
+    else if (t < head + tail) reduceElt(fn, a, nSrcs, tailStart + (uint64_t)(t - head));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Batched buckets (nbxReduceMultiBatch). The tiles of every bucket form one
 // index space (bucket k owns the tiles between the previous record's tileEnd
 // and its own); workgroups grid-stride over it, so a batch of small buckets
@@ -296,6 +392,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
     ks.unroll[i] = un[i];
   }
   ks.elts = (const void*)&kReduceElts<Fn>;
+  ks.shifted = (const void*)&kReduceShifted<Fn>;
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;

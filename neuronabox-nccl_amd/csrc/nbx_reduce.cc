@@ -170,10 +170,28 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     err = hipLaunchKernel((const void*)ks.packs[big ? 1 : 0][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args,
                           0, stream);
   } else {
-    size_t blocks = (count + kBlock - 1) / kBlock;
-    size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs, /*classic=*/true);
-    size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
-    err = hipLaunchKernel((const void*)ks.elts, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
+    const unsigned dmis = (unsigned)((uintptr_t)dsts[0] & 15u);
+    bool dstShared = true;
+    for (int d = 1; d < nDsts; d++) dstShared &= (((uintptr_t)dsts[d] & 15u) == dmis);
+    if (dstShared && ks.shifted != nullptr) {
+      // destinations share one alignment: 16-B packs on their side, the
+      // sources realigned in registers (kReduceShifted)
+      size_t head = dmis ? (size_t)((16u - dmis) / (unsigned)eb) : 0;
+      if (head > count) head = count;
+      const size_t nPacks = (count - head) / (size_t)epp;
+      a.headElts = (int)head;
+      a.nPacks = nPacks;
+      size_t blocks = (nPacks + kBlock - 1) / kBlock;
+      if (blocks == 0) blocks = 1;
+      const size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs, /*classic=*/true);
+      const size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
+      err = hipLaunchKernel((const void*)ks.shifted, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
+    } else {
+      size_t blocks = (count + kBlock - 1) / kBlock;
+      size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs, /*classic=*/true);
+      size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
+      err = hipLaunchKernel((const void*)ks.elts, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
+    }
   }
   if (err != hipSuccess) {
     std::fprintf(stderr, "nbx: kernel launch failed: %s\n", hipGetErrorString(err));

@@ -7,6 +7,7 @@ GPU box. Not the bench: feeds DESIGN.md and the launch-default choice.
   e2e     host-staged path: pinned host -> hipMemcpy H2D -> reduce -> D2H (BASELINE asks for it)
   small   latency of small buckets (4 KiB .. 1 MiB), nSrcs 2
   tiles   single-bucket tile choice: auto / small (U=1, 8 per CU) / big per nSrcs, dtype, size
+  mixed   mixed pointer alignment (element kernel) vs shared alignment, 2 / 8 sources
   batch   config C bucket sets through nbxReduceMultiBatch vs one nbxReduceMulti per bucket
 
 Prints one JSON object per line.
@@ -191,6 +192,24 @@ def main():
                         row[f"bpc{x[0]}_v{x[1]}_GBps"] = round(gbps(alg, v[len(v) // 2]), 1)
                     print(json.dumps(row), flush=True)
                     del srcs, out
+
+    if "mixed" in what:
+        for dt, name, tdt in ((7, "fp32", torch.float32), (6, "fp16", torch.float16)):
+            for nsrc in (2, 8):
+                esz = torch.tensor([], dtype=tdt).element_size()
+                n = (64 << 20) // esz
+                raw = [torch.rand(n + 16, device="cuda").to(tdt) for _ in range(nsrc)]
+                out = torch.empty(n + 16, dtype=tdt, device="cuda")
+                op = op_for(dt)
+                row = {"what": "mixed", "dtype": name, "nsrc": nsrc, "MiB_per_input": 64}
+                for label, doff in (("aligned", 0), ("dst_off_1elt", 1)):
+                    sp = [t.data_ptr() for t in raw]
+                    dp = out.data_ptr() + doff * esz
+                    ts = sorted(timed(torch, lambda: nbx.reduce_multi([dp], sp, n, dt, op, 0, False, st), 10)
+                                for _ in range(args.rounds))
+                    row[label + "_GBps"] = round(gbps((nsrc + 1) * n * esz, ts[len(ts) // 2]), 1)
+                print(json.dumps(row), flush=True)
+                del raw, out
 
     if "batch" in what:
         # bucket sets (MiB per input): 16 x 1 MiB, 64 x 256 KiB, the mixed 1..64 MiB sweep

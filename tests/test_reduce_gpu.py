@@ -162,11 +162,34 @@ def test_shared_misalignment(nbx, oracle, torch_gpu, dtype):
 
 @pytest.mark.parametrize("dtype", [1, 6, 7, 8])
 def test_mixed_misalignment(nbx, oracle, torch_gpu, dtype):
-    """Different alignments modulo 16 -> element kernel (common_kernel.h:229-238)."""
+    """Different alignments modulo 16: sources realigned against one destination
+    alignment (kReduceShifted), or destinations of different alignments (element
+    kernel, common_kernel.h:229-238)."""
     eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
     srcs = oracle.random_inputs(dtype, 4, 12345, seed=3)
     run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, src_off=[0, eb, 0, 2 * eb % 16], dst_off=[eb % 16])
     run_case(nbx, oracle, torch_gpu, srcs, dtype, 2, 0, ndst=2, src_off=[eb % 16, 0, 0, 0], dst_off=[0, eb % 16])
+
+
+@pytest.mark.parametrize("dtype", [0, 6, 7, 4, 10, 9])
+@pytest.mark.parametrize("count", [1, 7, 100, 4097, 70001])
+def test_realigned_sources(nbx, oracle, torch_gpu, dtype, count):
+    """Sources at alignments that differ from the destinations' (kReduceShifted:
+    16-B packs on the destination side, every source realigned in registers by
+    its own byte offset): every offset an element size allows, 1-8 sources,
+    1-3 destinations sharing one alignment, heads and tails, every op."""
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    offs = list(range(0, 16, eb))
+    rng = np.random.default_rng(count * 16 + dtype)
+    for devop in devops_for(dtype):
+        nsrc = 1 + (devop * 3 + count) % 8
+        srcs = oracle.random_inputs(dtype, nsrc, count, seed=int(rng.integers(1 << 20)))
+        src_off = [offs[(k * 5 + devop + 1) % len(offs)] for k in range(nsrc)]
+        dst_o = offs[(devop + 2) % len(offs)]
+        ndst = 1 + devop % 3
+        arg = op_arg(oracle, dtype, devop, rng)
+        run_case(nbx, oracle, torch_gpu, srcs, dtype, devop, arg, npre=min(2, nsrc) if devop == 3 else 0,
+                 post=devop == 4, ndst=ndst, src_off=src_off, dst_off=[dst_o] * ndst)
 
 
 @pytest.mark.parametrize("dtype", [2, 7, 9])
