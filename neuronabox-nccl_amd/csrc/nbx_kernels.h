@@ -179,13 +179,23 @@ __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
 // Sources misaligned against the destinations (common_kernel.h:229-238 falls
 // back to sizeof(T) packs there). Here the destinations (which share one
 // alignment) stay 16-B packs, and each source is read as 16-B aligned packs
-// and realigned in registers: lane p loads packs p and p+1 of the source's
-// aligned-down base and funnel-shifts the 32 bytes by the source's byte
-// offset (v_alignbyte_b32; the offset is per source, so the shift case is
-// uniform). The second load mostly hits L2/L1 (it is the next lane's first),
-// so HBM traffic stays the algorithmic bytes. Memory safety: a 16-B aligned
-// pack never crosses a page, and every pack loaded holds at least one byte
-// of the source range, so no load can touch an unmapped page.
+// and realigned in registers: output pack q needs packs q and q+1 of the
+// source's aligned-down base, funnel-shifted by the source's byte offset
+// (v_alignbyte_b32; the offset is per source, so the shift case is uniform).
+// Lanes of a wave own consecutive packs, so pack q+1 is the next lane's q.
+// Two shapes (scripts/sweep_shift.hip, profiles/r1/sweep_shift.txt):
+//  * kReduceShifted (1-3 sources; 1 pack per lane, 8 workgroups per CU): each
+//    lane loads q and q+1 itself with plain (temporal) loads; the second
+//    mostly hits L2 (it is the next lane's first);
+//  * kReduceShiftedDpp (4+ sources; 2 packs per lane, 4 workgroups per CU): each
+//    lane loads q only (nontemporal) and takes
+//    q+1 from the next lane by a DPP wave shift (wave_shl:1, VALU, no LDS);
+//    lane 63 and the lane holding the last pack load q+1 themselves, issued
+//    with the main loads so the shift waits on no second round trip.
+// HBM traffic stays the algorithmic bytes either way. Memory safety: a 16-B
+// aligned pack never crosses a page, and every pack loaded holds at least one
+// byte of the source range (pack indices are clamped to the last one), so no
+// load can touch an unmapped page.
 __device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t m) {
   const uint32_t b = m & 3u;   // byte shift inside a dword (0: plain dword select)
   const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -209,6 +219,14 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint
       break;
   }
   return r;
+}
+
+// lane i receives lane i+1's value (DPP wave_shl:1); lane 63 gets 0
+__device__ __forceinline__ u32x4 fromNextLane(const u32x4& v) {
+  return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x130, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x130, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x130, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x130, 0xf, 0xf, false)};
 }
 
 template <class Fn>
@@ -259,6 +277,98 @@ __global__ __launch_bounds__(kBlock) void kReduceShifted(KArgs a) {
 #pragma unroll
     for (int d = 1; d < kMaxKDsts; d++)
       if (d < nDsts) stPack(dst[d] + p, acc);
+  }
+  // head (before the destinations' 16-B boundary) and tail elements
+  if (blockIdx.x == gridDim.x - 1) {
+    const int head = a.headElts;
+    const uint64_t tailStart = (uint64_t)head + n * EPP;
+    const int tail = (int)(a.nElts - tailStart);
+    const int t = (int)threadIdx.x;
+    if (t < head) reduceElt(fn, a, nSrcs, (uint64_t)t);
+    else if (t < head + tail) reduceElt(fn, a, nSrcs, tailStart + (uint64_t)(t - head));
+  }
+}
+
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
+  using E = typename Fn::Elt;
+  constexpr int EPP = 16 / (int)sizeof(E);
+  constexpr int U = kShiftUDpp;
+  acquirePeerData(a);
+  const Fn fn(loadArg<Fn>(a));
+  const uint64_t headBytes = (uint64_t)a.headElts * sizeof(E);
+  const int nSrcs = a.nSrcs, nDsts = a.nDsts;
+  const u32x4* base[kMaxKSrcs];
+  uint32_t sh[kMaxKSrcs];
+#pragma unroll
+  for (int s = 0; s < kMaxKSrcs; s++) {
+    const uintptr_t q = (uintptr_t)a.src[s < nSrcs ? s : 0] + headBytes;
+    sh[s] = (uint32_t)(q & 15u);
+    base[s] = (const u32x4*)(q - sh[s]);
+  }
+  u32x4* dst[kMaxKDsts];
+#pragma unroll
+  for (int d = 0; d < kMaxKDsts; d++) dst[d] = (u32x4*)((char*)a.dst[d] + headBytes);
+  const bool doPost = Fn::kHasPost && a.postOp;
+  const uint32_t preMask = a.preMask;
+  const uint64_t n = a.nPacks;
+  const uint32_t lane = threadIdx.x & 63u;
+  constexpr uint64_t tile = (uint64_t)U * kBlock;
+  const uint64_t stride = (uint64_t)gridDim.x * tile;
+  // the whole workgroup iterates while its tile starts inside the range, so
+  // every lane of a wave is active at the shift (indices past n are clamped
+  // for the loads and masked for the stores)
+  for (uint64_t p0 = (uint64_t)blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
+    u32x4 lo[kMaxKSrcs][U], hi[kMaxKSrcs][U];
+#pragma unroll
+    for (int s = 0; s < kMaxKSrcs; s++) {
+      if (s < nSrcs) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          uint64_t q = p0 + (uint64_t)u * kBlock;
+          if (q >= n) q = n - 1;
+          lo[s][u] = ldPack(base[s] + q);
+          if (sh[s] && (lane == 63u || q + 1 >= n)) hi[s][u] = base[s][q + 1];
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = p0 + (uint64_t)u * kBlock;
+      const bool own = lane == 63u || (q >= n ? n - 1 : q) + 1 >= n;
+      // the shift runs on every lane (a lane reading a disabled lane would get 0),
+      // then lanes that loaded pack q+1 themselves keep their own
+      u32x4 acc = lo[0][u];
+      if (sh[0]) {
+        u32x4 h = hi[0][u];
+        const u32x4 x = fromNextLane(lo[0][u]);
+        if (!own) h = x;
+        acc = funnel16(lo[0][u], h, sh[0]);
+      }
+      if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
+#pragma unroll
+      for (int s = 1; s < kMaxKSrcs; s++) {
+        if (s < nSrcs) {
+          u32x4 t = lo[s][u];
+          if (sh[s]) {
+            u32x4 h = hi[s][u];
+            const u32x4 x = fromNextLane(lo[s][u]);
+            if (!own) h = x;
+            t = funnel16(lo[s][u], h, sh[s]);
+          }
+          if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
+          acc = fn.redPack(acc, t);
+        }
+      }
+      if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
+      if (q < n) {
+        stPack(dst[0] + q, acc);
+#pragma unroll
+        for (int d = 1; d < kMaxKDsts; d++)
+          if (d < nDsts) stPack(dst[d] + q, acc);
+      }
+    }
   }
   // head (before the destinations' 16-B boundary) and tail elements
   if (blockIdx.x == gridDim.x - 1) {
@@ -393,6 +503,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   }
   ks.elts = (const void*)&kReduceElts<Fn>;
   ks.shifted = (const void*)&kReduceShifted<Fn>;
+  ks.shiftedDpp = (const void*)&kReduceShiftedDpp<Fn>;
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;

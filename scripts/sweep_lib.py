@@ -195,7 +195,7 @@ def main():
 
     if "mixed" in what:
         for dt, name, tdt in ((7, "fp32", torch.float32), (6, "fp16", torch.float16)):
-            for nsrc in (2, 8):
+            for nsrc in [int(x) for x in os.environ.get("NBX_SWEEP_NSRCS", "2,3,4,8").split(",")]:
                 esz = torch.tensor([], dtype=tdt).element_size()
                 n = (64 << 20) // esz
                 raw = [torch.rand(n + 16, device="cuda").to(tdt) for _ in range(nsrc)]

@@ -1,0 +1,306 @@
+// sweep_shift.hip — experiment for the realigning kernel (kReduceShifted),
+// not part of the product: sources whose alignment mod 16 differs from the
+// destination's. fp32 sum, NSRC x 64 MiB -> 64 MiB, destination one element
+// past a 16-B boundary (so every source is read 12 B off its packs).
+//
+// Variants:
+//   temporal Ux  : lane loads packs q and q+1 of each source (plain loads;
+//                  q+1 is the next lane's q, served by L2) — the production
+//                  shape at U = 1, here also unrolled to U packs per lane;
+//   dpp Ux       : lane loads pack q only (nontemporal) and takes q+1 from
+//                  the next lane with a DPP wave shift (VALU, no LDS); lane 63
+//                  and the lane holding the last pack load q+1 themselves.
+// Outputs are checked bit-exact against the first variant.
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off scripts/sweep_shift.hip -o scripts/sweep_shift
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(2); } } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+  const u32x4* base[8];   // 16-B aligned-down source bases
+  uint32_t sh[8];         // byte offset of each source inside its first pack
+  u32x4* dst;
+  uint64_t nPacks;
+};
+
+__device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t m) {
+  const uint32_t b = m & 3u;
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  u32x4 r;
+  switch (m >> 2) {
+    case 0:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], b), __builtin_amdgcn_alignbyte(w[2], w[1], b),
+                __builtin_amdgcn_alignbyte(w[3], w[2], b), __builtin_amdgcn_alignbyte(w[4], w[3], b)};
+      break;
+    case 1:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[2], w[1], b), __builtin_amdgcn_alignbyte(w[3], w[2], b),
+                __builtin_amdgcn_alignbyte(w[4], w[3], b), __builtin_amdgcn_alignbyte(w[5], w[4], b)};
+      break;
+    case 2:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[3], w[2], b), __builtin_amdgcn_alignbyte(w[4], w[3], b),
+                __builtin_amdgcn_alignbyte(w[5], w[4], b), __builtin_amdgcn_alignbyte(w[6], w[5], b)};
+      break;
+    default:
+      r = u32x4{__builtin_amdgcn_alignbyte(w[4], w[3], b), __builtin_amdgcn_alignbyte(w[5], w[4], b),
+                __builtin_amdgcn_alignbyte(w[6], w[5], b), __builtin_amdgcn_alignbyte(w[7], w[6], b)};
+      break;
+  }
+  return r;
+}
+
+__device__ __forceinline__ u32x4 add4(u32x4 a, u32x4 b) {
+  f32x4 x = __builtin_bit_cast(f32x4, a), y = __builtin_bit_cast(f32x4, b);
+  return __builtin_bit_cast(u32x4, x + y);
+}
+
+// wave_shl:1 (DPP control 0x130): lane i receives lane i+1's value
+__device__ __forceinline__ u32x4 fromNextLane(const u32x4& v) {
+  return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x130, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x130, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x130, 0xf, 0xf, false),
+               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x130, 0xf, 0xf, false)};
+}
+
+template <int NSRC, int U, bool DPP>
+__global__ __launch_bounds__(256) void kshift(Args a) {
+  const uint64_t n = a.nPacks, tile = (uint64_t)U * 256, stride = (uint64_t)gridDim.x * tile;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t p0 = blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
+    u32x4 lo[NSRC][U], hi[NSRC][U];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t q = p0 + (uint64_t)u * 256;
+        if (q >= n) q = n - 1;   // clamp: every lane stays active for the shift
+        if constexpr (DPP) {
+          lo[s][u] = __builtin_nontemporal_load(a.base[s] + q);
+        } else {
+          lo[s][u] = a.base[s][q];
+          hi[s][u] = a.base[s][q + 1];
+        }
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DPP) {
+#pragma unroll
+      for (int s = 0; s < NSRC; s++)
+#pragma unroll
+        for (int u = 0; u < U; u++) hi[s][u] = fromNextLane(lo[s][u]);
+#pragma unroll
+      for (int s = 0; s < NSRC; s++)
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          uint64_t q = p0 + (uint64_t)u * 256;
+          if (q >= n) q = n - 1;
+          if (lane == 63u || q + 1 >= n) hi[s][u] = a.base[s][q + 1];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = p0 + (uint64_t)u * 256;
+      u32x4 acc = funnel16(lo[0][u], hi[0][u], a.sh[0]);
+#pragma unroll
+      for (int s = 1; s < NSRC; s++) acc = add4(acc, funnel16(lo[s][u], hi[s][u], a.sh[s]));
+      if (q < n) a.dst[q] = acc;
+    }
+  }
+}
+
+// dpp, with the own loads of lane 63 / the last pack issued in the load
+// phase (no extra memory round trip after the shift)
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kshiftPre(Args a) {
+  const uint64_t n = a.nPacks, tile = (uint64_t)U * 256, stride = (uint64_t)gridDim.x * tile;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t p0 = blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
+    u32x4 lo[NSRC][U], own[NSRC][U];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t q = p0 + (uint64_t)u * 256;
+        if (q >= n) q = n - 1;
+        lo[s][u] = __builtin_nontemporal_load(a.base[s] + q);
+        if (lane == 63u || q + 1 >= n) own[s][u] = a.base[s][q + 1];
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t q = p0 + (uint64_t)u * 256;
+      const bool mine = lane == 63u || (q >= n ? n - 1 : q) + 1 >= n;
+      u32x4 h = fromNextLane(lo[0][u]);
+      u32x4 acc = funnel16(lo[0][u], mine ? own[0][u] : h, a.sh[0]);
+#pragma unroll
+      for (int s = 1; s < NSRC; s++) {
+        h = fromNextLane(lo[s][u]);
+        acc = add4(acc, funnel16(lo[s][u], mine ? own[s][u] : h, a.sh[s]));
+      }
+      if (q < n) a.dst[q] = acc;
+    }
+  }
+}
+
+// 63 output packs per wave: lane 63 only loads (the pack lane 62 needs), so
+// every lane's q+1 comes from the next lane by DPP and nothing is loaded
+// twice inside a wave; loads clamp at the last pack the source range touches
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kshift63(Args a) {
+  const uint64_t n = a.nPacks, span = (uint64_t)U * 63;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t waves = (uint64_t)gridDim.x * 4, wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint64_t lim[NSRC];
+#pragma unroll
+  for (int s = 0; s < NSRC; s++) lim[s] = a.sh[s] ? n : n - 1;
+  for (uint64_t w0 = wave * span; w0 < n; w0 += waves * span) {
+    u32x4 lo[NSRC][U];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t q = w0 + (uint64_t)u * 63 + lane;
+        lo[s][u] = __builtin_nontemporal_load(a.base[s] + (q < lim[s] ? q : lim[s]));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = w0 + (uint64_t)u * 63 + lane;
+      u32x4 acc = funnel16(lo[0][u], fromNextLane(lo[0][u]), a.sh[0]);
+#pragma unroll
+      for (int s = 1; s < NSRC; s++) acc = add4(acc, funnel16(lo[s][u], fromNextLane(lo[s][u]), a.sh[s]));
+      if (lane < 63u && q < n) a.dst[q] = acc;
+    }
+  }
+}
+
+struct Variant {
+  std::string name;
+  const void* fn;
+  int unroll, blocksPerCU;
+};
+
+template <int NSRC>
+int run(int cus, int rounds, int iters) {
+  const size_t count = (64ull << 20) / 4;   // fp32 elements per input
+  std::vector<void*> src(NSRC);
+  std::vector<float> h(count + 64);
+  for (int s = 0; s < NSRC; s++) {
+    CK(hipMalloc(&src[s], (count + 64) * 4));
+    for (size_t i = 0; i < h.size(); i++) h[i] = (float)((i * 2654435761u + s * 97u) % 100003u) / 1000.0f;
+    CK(hipMemcpy(src[s], h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  }
+  // destination one element past a 16-B boundary: 3 head elements, then
+  // packs; source element k of the body sits 12 B into pack (k*4+12)/16
+  float *dstRaw, *refRaw;
+  CK(hipMalloc(&dstRaw, (count + 64) * 4));
+  CK(hipMalloc(&refRaw, (count + 64) * 4));
+  const size_t head = 3;
+  const uint64_t nPacks = (count - head) / 4;
+  Args a;
+  for (int s = 0; s < NSRC; s++) {
+    uintptr_t qa = (uintptr_t)src[s] + head * 4;
+    a.sh[s] = (uint32_t)(qa & 15u);
+    a.base[s] = (const u32x4*)(qa - a.sh[s]);
+  }
+  a.nPacks = nPacks;
+  std::vector<Variant> vs = {
+      {"temporal u1 bpc8 (production)", (const void*)&kshift<NSRC, 1, false>, 1, 8},
+      {"temporal u2 bpc4", (const void*)&kshift<NSRC, 2, false>, 2, 4},
+      {"temporal u2 bpc2", (const void*)&kshift<NSRC, 2, false>, 2, 2},
+      {"dpp u1 bpc8", (const void*)&kshift<NSRC, 1, true>, 1, 8},
+      {"dpp-pre u1 bpc8", (const void*)&kshiftPre<NSRC, 1>, 1, 8},
+      {"dpp-pre u2 bpc4", (const void*)&kshiftPre<NSRC, 2>, 2, 4},
+      {"dpp-pre u4 bpc1", (const void*)&kshiftPre<NSRC, 4>, 4, 1},
+      {"63-lane u1 bpc8", (const void*)&kshift63<NSRC, 1>, -1, 8},
+      {"63-lane u2 bpc4", (const void*)&kshift63<NSRC, 2>, -2, 4},
+      {"63-lane u4 bpc1", (const void*)&kshift63<NSRC, 4>, -4, 1},
+      {"63-lane u4 bpc2", (const void*)&kshift63<NSRC, 4>, -4, 2},
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto launch = [&](const Variant& v, float* outRaw) {
+    Args b = a;
+    b.dst = (u32x4*)(outRaw + 1 + head);   // dst + 1 element is 4 B off; its body starts 3 elements later
+    // unroll < 0: 63-lane variant, a workgroup covers 4 x 63 x |unroll| packs
+    uint64_t tile = v.unroll > 0 ? (uint64_t)v.unroll * 256 : (uint64_t)(-v.unroll) * 252;
+    uint64_t grid = std::min<uint64_t>((nPacks + tile - 1) / tile, (uint64_t)cus * v.blocksPerCU);
+    void* args[] = {&b};
+    CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(256), args, 0, 0));
+  };
+  CK(hipMemset(refRaw, 0, (count + 64) * 4));
+  launch(vs[0], refRaw);
+  CK(hipDeviceSynchronize());
+  // host check of the reference variant: ordered left fold of the sources
+  std::vector<float> r(count + 64), o(count + 64);
+  CK(hipMemcpy(r.data(), refRaw, r.size() * 4, hipMemcpyDeviceToHost));
+  int bad = 0;
+  {
+    std::vector<std::vector<float>> hs(NSRC, std::vector<float>(count + 64));
+    for (int s = 0; s < NSRC; s++) CK(hipMemcpy(hs[s].data(), src[s], hs[s].size() * 4, hipMemcpyDeviceToHost));
+    for (uint64_t k = 0; k < nPacks * 4; k++) {
+      float acc = hs[0][head + k];
+      for (int s = 1; s < NSRC; s++) acc = acc + hs[s][head + k];
+      if (memcmp(&acc, &r[1 + head + k], 4) != 0) {
+        if (bad < 4) printf("host mismatch at %llu\n", (unsigned long long)k);
+        bad++;
+      }
+    }
+  }
+  for (auto& v : vs) {
+    CK(hipMemset(dstRaw, 0, (count + 64) * 4));
+    launch(v, dstRaw);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(o.data(), dstRaw, o.size() * 4, hipMemcpyDeviceToHost));
+    if (memcmp(o.data(), r.data(), o.size() * 4) != 0) {
+      printf("MISMATCH in %s\n", v.name.c_str());
+      bad++;
+    }
+  }
+  std::vector<std::vector<float>> t(vs.size());
+  for (int rd = 0; rd < rounds; rd++)
+    for (size_t i = 0; i < vs.size(); i++) {
+      launch(vs[i], dstRaw);
+      CK(hipEventRecord(e0, 0));
+      for (int it = 0; it < iters; it++) launch(vs[i], dstRaw);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[i].push_back(ms / iters);
+    }
+  printf("%d x 64 MiB fp32 -> 64 MiB, sources 12 B off their packs\n", NSRC);
+  printf("%-34s %10s %10s %9s\n", "variant", "med_ms", "min_ms", "GB/s(med)");
+  for (size_t i = 0; i < vs.size(); i++) {
+    auto x = t[i];
+    std::sort(x.begin(), x.end());
+    double med = x[x.size() / 2];
+    printf("%-34s %10.4f %10.4f %9.1f\n", vs[i].name.c_str(), med, x[0],
+           (double)(NSRC + 1) * nPacks * 16 / (med * 1e-3) / 1e9);
+  }
+  printf("mismatches: %d\n", bad);
+  for (auto p : src) CK(hipFree(p));
+  CK(hipFree(dstRaw));
+  CK(hipFree(refRaw));
+  return bad;
+}
+
+int main(int argc, char** argv) {
+  int rounds = argc > 1 ? atoi(argv[1]) : 7, iters = argc > 2 ? atoi(argv[2]) : 10;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  int bad = run<8>(cus, rounds, iters);
+  bad += run<2>(cus, rounds, iters);
+  printf("total mismatches: %d\n", bad);
+  return bad ? 1 : 0;
+}

@@ -48,6 +48,8 @@ def test_all_kernels_present(kernels):
     elts = [n for n in names if "kReduceElts" in n]
     assert len(elts) == 42                 # one element kernel per distinct functor
     assert len(packs) == 42 * 16           # 8 source counts x {small, big} tiles
+    shifted = [n for n in names if "kReduceShifted" in n]
+    assert len(shifted) == 42 * 2          # realigning kernel: two-load and DPP shapes
     assert any("kPeerBarrier" in n for n in names)
 
 

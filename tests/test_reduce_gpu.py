@@ -192,6 +192,18 @@ def test_realigned_sources(nbx, oracle, torch_gpu, dtype, count):
                  post=devop == 4, ndst=ndst, src_off=src_off, dst_off=[dst_o] * ndst)
 
 
+@pytest.mark.parametrize("dtype,nsrc,count", [(7, 8, 3_000_001), (7, 4, 2_097_155), (6, 5, 4_194_309),
+                                              (9, 3, 1_048_583), (10, 8, 8_388_617)])
+def test_realigned_sources_grid_stride(nbx, oracle, torch_gpu, dtype, nsrc, count):
+    """Realigned sources at sizes where the workgroups stride past the grid
+    (more packs than 4 workgroups/CU x 2 x 256 cover in one pass): the DPP
+    next-lane shape at 4+ sources, the two-load shape below; ragged last tile."""
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    srcs = oracle.random_inputs(dtype, nsrc, count, seed=nsrc * 7 + dtype)
+    src_off = [(k * 3 * eb) % 16 for k in range(nsrc)]
+    run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, src_off=src_off, dst_off=[eb % 16])
+
+
 @pytest.mark.parametrize("dtype", [2, 7, 9])
 def test_two_destinations(nbx, oracle, torch_gpu, dtype):
     srcs = oracle.random_inputs(dtype, 4, 70001, seed=21)
