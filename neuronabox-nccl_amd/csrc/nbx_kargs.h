@@ -8,7 +8,8 @@ namespace nbx {
 
 constexpr int kBlock = 256;      // workgroup = 4 wave64
 constexpr int kMaxKSrcs = 8;     // sources per kernel pass
-constexpr int kShiftUDpp = 2;    // packs per lane in the DPP realigning kernel (kReduceShifted<Fn, true>)
+constexpr int kShiftUDpp = 2;    // packs per lane in the DPP realigning kernel (kReduceShiftedDpp)
+constexpr int kShiftDppMinSrcs = 4;  // fewest sources with a DPP realigning kernel
 constexpr int kMaxKDsts = 8;     // destinations: NCCL_MAX_DIRECT_ARITY + 1 (device.h:147, all_reduce.h:343-360)
 
 struct KArgs {
@@ -60,7 +61,7 @@ struct KernelSet {
   const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
   const void* shifted;              // sources realigned against 16-B aligned destinations (kReduceShifted, 1-3 sources)
-  const void* shiftedDpp;           // the same, next-lane pack by DPP (4+ sources)
+  const void* shiftedDpp[kMaxKSrcs]; // the same, next-lane pack by DPP, [nSrcs-1] (4+ sources; else null)
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)

@@ -289,20 +289,24 @@ __global__ __launch_bounds__(kBlock) void kReduceShifted(KArgs a) {
   }
 }
 
-template <class Fn>
+template <class Fn, int NSRC>
 __global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
-  constexpr int U = kShiftUDpp;
+  // 64-bit SumPostDiv (integer Avg) keeps 1 pack per lane: its division code
+  // on top of the 2-pack arrays spilled (tests/test_code_object.py); the tile
+  // is the kernel's own, so the host's grid only sets the workgroup count
+  constexpr int U = (Fn::kHasPost && sizeof(E) == 8) ? 1 : kShiftUDpp;
   acquirePeerData(a);
   const Fn fn(loadArg<Fn>(a));
   const uint64_t headBytes = (uint64_t)a.headElts * sizeof(E);
-  const int nSrcs = a.nSrcs, nDsts = a.nDsts;
-  const u32x4* base[kMaxKSrcs];
-  uint32_t sh[kMaxKSrcs];
+  constexpr int nSrcs = NSRC;   // a compile-time count sizes the arrays (occupancy)
+  const int nDsts = a.nDsts;
+  const u32x4* base[NSRC];
+  uint32_t sh[NSRC];
 #pragma unroll
-  for (int s = 0; s < kMaxKSrcs; s++) {
-    const uintptr_t q = (uintptr_t)a.src[s < nSrcs ? s : 0] + headBytes;
+  for (int s = 0; s < NSRC; s++) {
+    const uintptr_t q = (uintptr_t)a.src[s] + headBytes;
     sh[s] = (uint32_t)(q & 15u);
     base[s] = (const u32x4*)(q - sh[s]);
   }
@@ -319,10 +323,10 @@ __global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
   // every lane of a wave is active at the shift (indices past n are clamped
   // for the loads and masked for the stores)
   for (uint64_t p0 = (uint64_t)blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
-    u32x4 lo[kMaxKSrcs][U], hi[kMaxKSrcs][U];
+    u32x4 lo[NSRC][U], hi[NSRC][U];
 #pragma unroll
-    for (int s = 0; s < kMaxKSrcs; s++) {
-      if (s < nSrcs) {
+    for (int s = 0; s < NSRC; s++) {
+      {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           uint64_t q = p0 + (uint64_t)u * kBlock;
@@ -348,8 +352,8 @@ __global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
       }
       if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
 #pragma unroll
-      for (int s = 1; s < kMaxKSrcs; s++) {
-        if (s < nSrcs) {
+      for (int s = 1; s < NSRC; s++) {
+        {
           u32x4 t = lo[s][u];
           if (sh[s]) {
             u32x4 h = hi[s][u];
@@ -488,6 +492,13 @@ constexpr int bigUnroll() {
   return u < CAP ? u : CAP;
 }
 
+// DPP realigning kernels exist for kShiftDppMinSrcs..8 sources only
+template <class Fn, int NSRC>
+inline const void* shiftedDppFor() {
+  if constexpr (NSRC >= kShiftDppMinSrcs) return (const void*)&kReduceShiftedDpp<Fn, NSRC>;
+  else return nullptr;
+}
+
 template <class Fn, int... I>
 KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   KernelSet ks{};
@@ -503,7 +514,8 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   }
   ks.elts = (const void*)&kReduceElts<Fn>;
   ks.shifted = (const void*)&kReduceShifted<Fn>;
-  ks.shiftedDpp = (const void*)&kReduceShiftedDpp<Fn>;
+  const void* sdpp[] = {shiftedDppFor<Fn, I + 1>()...};
+  for (int i = 0; i < kMaxKSrcs; i++) ks.shiftedDpp[i] = sdpp[i];
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;

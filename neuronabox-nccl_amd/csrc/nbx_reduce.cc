@@ -97,12 +97,12 @@ int maxBlocksPerCU(bool big, int loadsPerLane, bool classic = false) {
 }
 
 // Realigning kernel (kReduceShifted): 8 workgroups per CU for the 1-pack
-// two-load shape, 4 for the 2-pack DPP shape (profiles/r1/sweep_shift.txt).
+// two-load shape, 2 for the 2-pack DPP shape (profiles/r1/sweep_shift.txt).
 int shiftedBlocksPerCU(bool dpp) {
   int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
   if (v > 0) return v;
   static const int env = envInt("NBX_BLOCKS_PER_CU", 0);
-  return env > 0 ? env : (dpp ? 4 : 8);
+  return env > 0 ? env : (dpp ? 2 : 8);
 }
 
 bool isFloatType(int dt) {
@@ -192,14 +192,14 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
       a.nPacks = nPacks;
       // 4+ sources: next-lane packs by DPP, 2 packs per lane; 1-3: two loads
       // per lane, 1 pack (profiles/r1/mixed_alignment_dpp_r1w.jsonl)
-      static const int dppMin = envInt("NBX_SHIFT_DPP_MIN_SRCS", 4);
-      const bool dpp = nSrcs >= dppMin && ks.shiftedDpp != nullptr;
+      static const int dppMin = envInt("NBX_SHIFT_DPP_MIN_SRCS", kShiftDppMinSrcs);
+      const bool dpp = nSrcs >= dppMin && ks.shiftedDpp[nSrcs - 1] != nullptr;
       const size_t tile = (size_t)(dpp ? kShiftUDpp : 1) * kBlock;
       size_t blocks = (nPacks + tile - 1) / tile;
       if (blocks == 0) blocks = 1;
       const size_t maxBlocks = (size_t)cus * (size_t)shiftedBlocksPerCU(dpp);
       const size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
-      const void* fn = dpp ? ks.shiftedDpp : ks.shifted;
+      const void* fn = dpp ? ks.shiftedDpp[nSrcs - 1] : ks.shifted;
       err = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
     } else {
       size_t blocks = (count + kBlock - 1) / kBlock;

@@ -150,6 +150,43 @@ __global__ __launch_bounds__(256) void kshiftPre(Args a) {
   }
 }
 
+// dpp-pre with the source count a run-time value and arrays sized for 8
+// sources (the library's kReduceShiftedDpp shape)
+template <int U>
+__global__ __launch_bounds__(256) void kshiftPreRt(Args a, int nSrcs) {
+  const uint64_t n = a.nPacks, tile = (uint64_t)U * 256, stride = (uint64_t)gridDim.x * tile;
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint64_t p0 = blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
+    u32x4 lo[8][U], own[8][U];
+#pragma unroll
+    for (int s = 0; s < 8; s++)
+      if (s < nSrcs) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          uint64_t q = p0 + (uint64_t)u * 256;
+          if (q >= n) q = n - 1;
+          lo[s][u] = __builtin_nontemporal_load(a.base[s] + q);
+          if (lane == 63u || q + 1 >= n) own[s][u] = a.base[s][q + 1];
+        }
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t q = p0 + (uint64_t)u * 256;
+      const bool mine = lane == 63u || (q >= n ? n - 1 : q) + 1 >= n;
+      u32x4 h = fromNextLane(lo[0][u]);
+      u32x4 acc = funnel16(lo[0][u], mine ? own[0][u] : h, a.sh[0]);
+#pragma unroll
+      for (int s = 1; s < 8; s++)
+        if (s < nSrcs) {
+          h = fromNextLane(lo[s][u]);
+          acc = add4(acc, funnel16(lo[s][u], mine ? own[s][u] : h, a.sh[s]));
+        }
+      if (q < n) a.dst[q] = acc;
+    }
+  }
+}
+
 // 63 output packs per wave: lane 63 only loads (the pack lane 62 needs), so
 // every lane's q+1 comes from the next lane by DPP and nothing is loaded
 // twice inside a wave; loads clamp at the last pack the source range touches
@@ -214,6 +251,9 @@ int run(int cus, int rounds, int iters) {
   a.nPacks = nPacks;
   std::vector<Variant> vs = {
       {"temporal u1 bpc8 (production)", (const void*)&kshift<NSRC, 1, false>, 1, 8},
+      {"dpp-pre runtime-nsrc u2 bpc4 (library)", (const void*)&kshiftPreRt<2>, 2, 4},
+      {"dpp-pre runtime-nsrc u2 bpc2", (const void*)&kshiftPreRt<2>, 2, 2},
+      {"dpp-pre u2 bpc2", (const void*)&kshiftPre<NSRC, 2>, 2, 2},
       {"temporal u2 bpc4", (const void*)&kshift<NSRC, 2, false>, 2, 4},
       {"temporal u2 bpc2", (const void*)&kshift<NSRC, 2, false>, 2, 2},
       {"dpp u1 bpc8", (const void*)&kshift<NSRC, 1, true>, 1, 8},
@@ -234,7 +274,8 @@ int run(int cus, int rounds, int iters) {
     // unroll < 0: 63-lane variant, a workgroup covers 4 x 63 x |unroll| packs
     uint64_t tile = v.unroll > 0 ? (uint64_t)v.unroll * 256 : (uint64_t)(-v.unroll) * 252;
     uint64_t grid = std::min<uint64_t>((nPacks + tile - 1) / tile, (uint64_t)cus * v.blocksPerCU);
-    void* args[] = {&b};
+    int ns = NSRC;
+    void* args[] = {&b, &ns};
     CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(256), args, 0, 0));
   };
   CK(hipMemset(refRaw, 0, (count + 64) * 4));
@@ -279,12 +320,12 @@ int run(int cus, int rounds, int iters) {
       t[i].push_back(ms / iters);
     }
   printf("%d x 64 MiB fp32 -> 64 MiB, sources 12 B off their packs\n", NSRC);
-  printf("%-34s %10s %10s %9s\n", "variant", "med_ms", "min_ms", "GB/s(med)");
+  printf("%-40s %10s %10s %9s\n", "variant", "med_ms", "min_ms", "GB/s(med)");
   for (size_t i = 0; i < vs.size(); i++) {
     auto x = t[i];
     std::sort(x.begin(), x.end());
     double med = x[x.size() / 2];
-    printf("%-34s %10.4f %10.4f %9.1f\n", vs[i].name.c_str(), med, x[0],
+    printf("%-40s %10.4f %10.4f %9.1f\n", vs[i].name.c_str(), med, x[0],
            (double)(NSRC + 1) * nPacks * 16 / (med * 1e-3) / 1e9);
   }
   printf("mismatches: %d\n", bad);
@@ -300,7 +341,8 @@ int main(int argc, char** argv) {
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   int bad = run<8>(cus, rounds, iters);
-  bad += run<2>(cus, rounds, iters);
+  bad += run<5>(cus, rounds, iters);
+  bad += run<4>(cus, rounds, iters);
   printf("total mismatches: %d\n", bad);
   return bad ? 1 : 0;
 }
