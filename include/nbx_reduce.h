@@ -119,7 +119,9 @@ ncclResult_t nbxReduceMultiHost(void* const* hostDsts, int nDsts,
 /* Launch knobs (NCCL_NTHREADS / NCCL_MAX_NCHANNELS analogues, tuning.cc:12,
  * connect.cc:314): blocksPerCU caps the grid at CUs x blocksPerCU workgroups
  * (0 = default: 1 for big tiles, 3-5 for small; env NBX_BLOCKS_PER_CU);
- * variant 0 = auto tile choice, 1 = force small tiles, 2 = force big tiles. */
+ * variant 0 = auto tile choice, 1 = force small tiles (and, for sources
+ * misaligned against the destinations, the 1-pack run-time-source-count
+ * realigning kernel), 2 = force big tiles. */
 ncclResult_t nbxSetLaunchConfig(int blocksPerCU, int variant);
 ncclResult_t nbxGetLaunchConfig(int* blocksPerCU, int* variant);
 

@@ -8,8 +8,8 @@ namespace nbx {
 
 constexpr int kBlock = 256;      // workgroup = 4 wave64
 constexpr int kMaxKSrcs = 8;     // sources per kernel pass
-constexpr int kShiftUDpp = 2;    // packs per lane in the DPP realigning kernel (kReduceShiftedDpp)
-constexpr int kShiftDppMinSrcs = 4;  // fewest sources with a DPP realigning kernel
+constexpr int kShiftUDpp = 2;    // packs per lane in the per-source-count realigning kernels (kReduceShiftedN)
+constexpr int kShiftDppMinSrcs = 4;  // fewest sources for the DPP realigning shape
 constexpr int kMaxKDsts = 8;     // destinations: NCCL_MAX_DIRECT_ARITY + 1 (device.h:147, all_reduce.h:343-360)
 
 struct KArgs {
@@ -60,8 +60,8 @@ struct BatchArgs {
 struct KernelSet {
   const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
-  const void* shifted;              // sources realigned against 16-B aligned destinations (kReduceShifted, 1-3 sources)
-  const void* shiftedDpp[kMaxKSrcs]; // the same, next-lane pack by DPP, [nSrcs-1] (4+ sources; else null)
+  const void* shifted;              // sources realigned against 16-B aligned destinations (kReduceShifted, run-time source count; fallback)
+  const void* shiftedN[kMaxKSrcs];   // the same per source count, [nSrcs-1] (kReduceShiftedN: DPP shape from 4)
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)

@@ -184,15 +184,17 @@ __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
 // (v_alignbyte_b32; the offset is per source, so the shift case is uniform).
 // Lanes of a wave own consecutive packs, so pack q+1 is the next lane's q.
 // Two shapes (scripts/sweep_shift.hip, profiles/r1/sweep_shift.txt):
-//  * kReduceShifted (1-3 sources; 1 pack per lane, 8 workgroups per CU): each
-//    lane loads q and q+1 itself with plain (temporal) loads; the second
-//    mostly hits L2 (it is the next lane's first);
-//  * kReduceShiftedDpp (4+ sources; 2 packs per lane, 4 workgroups per CU): each
-//    lane loads q only (nontemporal) and takes
+//  * two loads (1-3 sources): each lane loads q and q+1 itself with plain
+//    (temporal) loads; the second mostly hits L2 (it is the next lane's
+//    first). kReduceShifted is this shape with a run-time source count
+//    (1 pack per lane, 8 workgroups per CU; the fallback);
+//  * DPP (4-8 sources): each lane loads q only (nontemporal) and takes
 //    q+1 from the next lane by a DPP wave shift (wave_shl:1, VALU, no LDS);
 //    lane 63 and the lane holding the last pack load q+1 themselves, issued
 //    with the main loads so the shift waits on no second round trip.
-// HBM traffic stays the algorithmic bytes either way. Memory safety: a 16-B
+// kReduceShiftedN<Fn, NSRC, kDpp> is one kernel per source count, 2 packs per
+// lane (4 workgroups per CU for two loads, 2 for DPP). HBM traffic stays the
+// algorithmic bytes either way. Memory safety: a 16-B
 // aligned pack never crosses a page, and every pack loaded holds at least one
 // byte of the source range (pack indices are clamped to the last one), so no
 // load can touch an unmapped page.
@@ -289,8 +291,11 @@ __global__ __launch_bounds__(kBlock) void kReduceShifted(KArgs a) {
   }
 }
 
-template <class Fn, int NSRC>
-__global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
+// Per-source-count realigning kernel, 2 packs per lane: kDpp = true is the
+// DPP next-lane shape (4-8 sources), kDpp = false the two-load shape (1-3
+// sources; +4 % over kReduceShifted at 2 sources in scripts/sweep_shift.hip).
+template <class Fn, int NSRC, bool kDpp>
+__global__ __launch_bounds__(kBlock) void kReduceShiftedN(KArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
   // 64-bit SumPostDiv (integer Avg) keeps 1 pack per lane: its division code
@@ -331,8 +336,13 @@ __global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
         for (int u = 0; u < U; u++) {
           uint64_t q = p0 + (uint64_t)u * kBlock;
           if (q >= n) q = n - 1;
-          lo[s][u] = ldPack(base[s] + q);
-          if (sh[s] && (lane == 63u || q + 1 >= n)) hi[s][u] = base[s][q + 1];
+          if constexpr (kDpp) {
+            lo[s][u] = ldPack(base[s] + q);
+            if (sh[s] && (lane == 63u || q + 1 >= n)) hi[s][u] = base[s][q + 1];
+          } else {   // plain (temporal) loads: the second one must find the line in L2
+            lo[s][u] = base[s][q];
+            hi[s][u] = sh[s] ? base[s][q + 1] : lo[s][u];
+          }
         }
       }
     }
@@ -346,8 +356,10 @@ __global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
       u32x4 acc = lo[0][u];
       if (sh[0]) {
         u32x4 h = hi[0][u];
-        const u32x4 x = fromNextLane(lo[0][u]);
-        if (!own) h = x;
+        if constexpr (kDpp) {
+          const u32x4 x = fromNextLane(lo[0][u]);
+          if (!own) h = x;
+        }
         acc = funnel16(lo[0][u], h, sh[0]);
       }
       if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
@@ -357,8 +369,10 @@ __global__ __launch_bounds__(kBlock) void kReduceShiftedDpp(KArgs a) {
           u32x4 t = lo[s][u];
           if (sh[s]) {
             u32x4 h = hi[s][u];
-            const u32x4 x = fromNextLane(lo[s][u]);
-            if (!own) h = x;
+            if constexpr (kDpp) {
+              const u32x4 x = fromNextLane(lo[s][u]);
+              if (!own) h = x;
+            }
             t = funnel16(lo[s][u], h, sh[s]);
           }
           if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
@@ -492,11 +506,10 @@ constexpr int bigUnroll() {
   return u < CAP ? u : CAP;
 }
 
-// DPP realigning kernels exist for kShiftDppMinSrcs..8 sources only
+// per-source-count realigning kernels: DPP shape from kShiftDppMinSrcs sources
 template <class Fn, int NSRC>
-inline const void* shiftedDppFor() {
-  if constexpr (NSRC >= kShiftDppMinSrcs) return (const void*)&kReduceShiftedDpp<Fn, NSRC>;
-  else return nullptr;
+inline const void* shiftedNFor() {
+  return (const void*)&kReduceShiftedN<Fn, NSRC, (NSRC >= kShiftDppMinSrcs)>;
 }
 
 template <class Fn, int... I>
@@ -514,8 +527,8 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   }
   ks.elts = (const void*)&kReduceElts<Fn>;
   ks.shifted = (const void*)&kReduceShifted<Fn>;
-  const void* sdpp[] = {shiftedDppFor<Fn, I + 1>()...};
-  for (int i = 0; i < kMaxKSrcs; i++) ks.shiftedDpp[i] = sdpp[i];
+  const void* sn[] = {shiftedNFor<Fn, I + 1>()...};
+  for (int i = 0; i < kMaxKSrcs; i++) ks.shiftedN[i] = sn[i];
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;

@@ -96,13 +96,16 @@ int maxBlocksPerCU(bool big, int loadsPerLane, bool classic = false) {
   return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
 
-// Realigning kernel (kReduceShifted): 8 workgroups per CU for the 1-pack
-// two-load shape, 2 for the 2-pack DPP shape (profiles/r1/sweep_shift.txt).
-int shiftedBlocksPerCU(bool dpp) {
+// Realigning kernels (profiles/r1/sweep_shift.txt): 8 workgroups per CU for
+// the run-time-count kernel; per source count, 2 for the DPP shape and 4 for
+// the two-load shape.
+int shiftedBlocksPerCU(bool perCount, int nSrcs) {
   int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
   if (v > 0) return v;
   static const int env = envInt("NBX_BLOCKS_PER_CU", 0);
-  return env > 0 ? env : (dpp ? 2 : 8);
+  if (env > 0) return env;
+  if (!perCount) return 8;
+  return nSrcs >= kShiftDppMinSrcs ? 2 : 4;
 }
 
 bool isFloatType(int dt) {
@@ -190,16 +193,20 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
       const size_t nPacks = (count - head) / (size_t)epp;
       a.headElts = (int)head;
       a.nPacks = nPacks;
-      // 4+ sources: next-lane packs by DPP, 2 packs per lane; 1-3: two loads
-      // per lane, 1 pack (profiles/r1/mixed_alignment_dpp_r1w.jsonl)
-      static const int dppMin = envInt("NBX_SHIFT_DPP_MIN_SRCS", kShiftDppMinSrcs);
-      const bool dpp = nSrcs >= dppMin && ks.shiftedDpp[nSrcs - 1] != nullptr;
-      const size_t tile = (size_t)(dpp ? kShiftUDpp : 1) * kBlock;
+      // one kernel per source count, 2 packs per lane: 4+ sources take the
+      // next-lane pack by DPP, 1-3 load it (DESIGN §4,
+      // profiles/r1/mixed_alignment_dpp_r1w.jsonl). NBX_SHIFT_N=0 or launch
+      // variant 1 (small tiles) selects the run-time-count kernel (1 pack per
+      // lane, 8 workgroups/CU).
+      static const int useN = envInt("NBX_SHIFT_N", 1);
+      const bool small = g_variant.load(std::memory_order_relaxed) == 1;
+      const void* fn = (useN && !small) ? ks.shiftedN[nSrcs - 1] : nullptr;
+      const size_t tile = (size_t)(fn ? kShiftUDpp : 1) * kBlock;
       size_t blocks = (nPacks + tile - 1) / tile;
       if (blocks == 0) blocks = 1;
-      const size_t maxBlocks = (size_t)cus * (size_t)shiftedBlocksPerCU(dpp);
+      const size_t maxBlocks = (size_t)cus * (size_t)shiftedBlocksPerCU(fn != nullptr, nSrcs);
       const size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
-      const void* fn = dpp ? ks.shiftedDpp[nSrcs - 1] : ks.shifted;
+      if (!fn) fn = ks.shifted;
       err = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
     } else {
       size_t blocks = (count + kBlock - 1) / kBlock;

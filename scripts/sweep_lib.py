@@ -197,11 +197,12 @@ def main():
         for dt, name, tdt in ((7, "fp32", torch.float32), (6, "fp16", torch.float16)):
             for nsrc in [int(x) for x in os.environ.get("NBX_SWEEP_NSRCS", "2,3,4,8").split(",")]:
                 esz = torch.tensor([], dtype=tdt).element_size()
-                n = (64 << 20) // esz
+                mib = int(os.environ.get("NBX_SWEEP_MIB", "64"))
+                n = (mib << 20) // esz
                 raw = [torch.rand(n + 16, device="cuda").to(tdt) for _ in range(nsrc)]
                 out = torch.empty(n + 16, dtype=tdt, device="cuda")
                 op = op_for(dt)
-                row = {"what": "mixed", "dtype": name, "nsrc": nsrc, "MiB_per_input": 64}
+                row = {"what": "mixed", "dtype": name, "nsrc": nsrc, "MiB_per_input": mib}
                 for label, doff in (("aligned", 0), ("dst_off_1elt", 1)):
                     sp = [t.data_ptr() for t in raw]
                     dp = out.data_ptr() + doff * esz

@@ -49,7 +49,7 @@ def test_all_kernels_present(kernels):
     assert len(elts) == 42                 # one element kernel per distinct functor
     assert len(packs) == 42 * 16           # 8 source counts x {small, big} tiles
     shifted = [n for n in names if "kReduceShifted" in n]
-    assert len(shifted) == 42 * (1 + 5)    # realigning kernels: two-load, and DPP per source count 4..8
+    assert len(shifted) == 42 * (1 + 8)    # realigning kernels: run-time count, and one per source count 1..8
     assert any("kPeerBarrier" in n for n in names)
 
 

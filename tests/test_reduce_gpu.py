@@ -204,6 +204,29 @@ def test_realigned_sources_grid_stride(nbx, oracle, torch_gpu, dtype, nsrc, coun
     run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, src_off=src_off, dst_off=[eb % 16])
 
 
+@pytest.mark.parametrize("dtype", [7, 6, 4])
+def test_realigned_sources_runtime_count_kernel(nbx, oracle, torch_gpu, dtype):
+    """Launch variant 1 sends misaligned sources to the run-time-source-count
+    realigning kernel (kReduceShifted, the fallback of the per-count kernels):
+    1-8 sources, every op, several destinations."""
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    offs = list(range(0, 16, eb))
+    rng = np.random.default_rng(dtype + 99)
+    try:
+        nbx.set_launch_config(0, 1)
+        for nsrc in range(1, 9):
+            for devop in devops_for(dtype):
+                count = int(rng.integers(1, 40000))
+                srcs = oracle.random_inputs(dtype, nsrc, count, seed=nsrc * 31 + devop)
+                src_off = [offs[(k * 3 + devop + 1) % len(offs)] for k in range(nsrc)]
+                ndst = 1 + (nsrc + devop) % 3
+                arg = op_arg(oracle, dtype, devop, rng)
+                run_case(nbx, oracle, torch_gpu, srcs, dtype, devop, arg, npre=min(2, nsrc) if devop == 3 else 0,
+                         post=devop == 4, ndst=ndst, src_off=src_off, dst_off=[offs[devop % len(offs)]] * ndst)
+    finally:
+        nbx.set_launch_config(0, 0)
+
+
 @pytest.mark.parametrize("dtype", [2, 7, 9])
 def test_two_destinations(nbx, oracle, torch_gpu, dtype):
     srcs = oracle.random_inputs(dtype, 4, 70001, seed=21)
