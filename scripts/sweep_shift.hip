@@ -116,6 +116,34 @@ __global__ __launch_bounds__(256) void kshift(Args a) {
   }
 }
 
+// two loads per lane, q nontemporal and q+1 temporal (the next lane's q is
+// then read nontemporally by that lane while this lane's copy hits L2)
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kshiftMix(Args a) {
+  const uint64_t n = a.nPacks, tile = (uint64_t)U * 256, stride = (uint64_t)gridDim.x * tile;
+  for (uint64_t p0 = blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
+    u32x4 lo[NSRC][U], hi[NSRC][U];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t q = p0 + (uint64_t)u * 256;
+        if (q >= n) q = n - 1;
+        lo[s][u] = __builtin_nontemporal_load(a.base[s] + q);
+        hi[s][u] = a.base[s][q + 1];
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = p0 + (uint64_t)u * 256;
+      u32x4 acc = funnel16(lo[0][u], hi[0][u], a.sh[0]);
+#pragma unroll
+      for (int s = 1; s < NSRC; s++) acc = add4(acc, funnel16(lo[s][u], hi[s][u], a.sh[s]));
+      if (q < n) a.dst[q] = acc;
+    }
+  }
+}
+
 // dpp, with the own loads of lane 63 / the last pack issued in the load
 // phase (no extra memory round trip after the shift)
 template <int NSRC, int U>
@@ -226,8 +254,8 @@ struct Variant {
 };
 
 template <int NSRC>
-int run(int cus, int rounds, int iters) {
-  const size_t count = (64ull << 20) / 4;   // fp32 elements per input
+int run(int cus, int rounds, int iters, int mib) {
+  const size_t count = ((size_t)mib << 20) / 4;   // fp32 elements per input
   std::vector<void*> src(NSRC);
   std::vector<float> h(count + 64);
   for (int s = 0; s < NSRC; s++) {
@@ -250,21 +278,18 @@ int run(int cus, int rounds, int iters) {
   }
   a.nPacks = nPacks;
   std::vector<Variant> vs = {
-      {"temporal u1 bpc8 (production)", (const void*)&kshift<NSRC, 1, false>, 1, 8},
-      {"dpp-pre runtime-nsrc u2 bpc4 (library)", (const void*)&kshiftPreRt<2>, 2, 4},
-      {"dpp-pre runtime-nsrc u2 bpc2", (const void*)&kshiftPreRt<2>, 2, 2},
-      {"dpp-pre u2 bpc2", (const void*)&kshiftPre<NSRC, 2>, 2, 2},
-      {"temporal u2 bpc4", (const void*)&kshift<NSRC, 2, false>, 2, 4},
+      {"temporal u2 bpc4 (library, 1-3 src)", (const void*)&kshift<NSRC, 2, false>, 2, 4},
+      {"dpp-pre u2 bpc2 (library, 4-8 src)", (const void*)&kshiftPre<NSRC, 2>, 2, 2},
+      {"temporal u1 bpc8", (const void*)&kshift<NSRC, 1, false>, 1, 8},
       {"temporal u2 bpc2", (const void*)&kshift<NSRC, 2, false>, 2, 2},
-      {"dpp u1 bpc8", (const void*)&kshift<NSRC, 1, true>, 1, 8},
-      {"dpp-pre u1 bpc8", (const void*)&kshiftPre<NSRC, 1>, 1, 8},
+      {"lo-nt/hi-temporal u2 bpc4", (const void*)&kshiftMix<NSRC, 2>, 2, 4},
+      {"lo-nt/hi-temporal u2 bpc2", (const void*)&kshiftMix<NSRC, 2>, 2, 2},
+      {"lo-nt/hi-temporal u1 bpc8", (const void*)&kshiftMix<NSRC, 1>, 1, 8},
       {"dpp-pre u2 bpc4", (const void*)&kshiftPre<NSRC, 2>, 2, 4},
-      {"dpp-pre u4 bpc1", (const void*)&kshiftPre<NSRC, 4>, 4, 1},
-      {"63-lane u1 bpc8", (const void*)&kshift63<NSRC, 1>, -1, 8},
-      {"63-lane u2 bpc4", (const void*)&kshift63<NSRC, 2>, -2, 4},
-      {"63-lane u4 bpc1", (const void*)&kshift63<NSRC, 4>, -4, 1},
+      {"dpp-pre u1 bpc8", (const void*)&kshiftPre<NSRC, 1>, 1, 8},
       {"63-lane u4 bpc2", (const void*)&kshift63<NSRC, 4>, -4, 2},
   };
+
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -319,7 +344,7 @@ int run(int cus, int rounds, int iters) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       t[i].push_back(ms / iters);
     }
-  printf("%d x 64 MiB fp32 -> 64 MiB, sources 12 B off their packs\n", NSRC);
+  printf("%d x %d MiB fp32 -> %d MiB, sources 12 B off their packs\n", NSRC, mib, mib);
   printf("%-40s %10s %10s %9s\n", "variant", "med_ms", "min_ms", "GB/s(med)");
   for (size_t i = 0; i < vs.size(); i++) {
     auto x = t[i];
@@ -340,9 +365,10 @@ int main(int argc, char** argv) {
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
-  int bad = run<8>(cus, rounds, iters);
-  bad += run<5>(cus, rounds, iters);
-  bad += run<4>(cus, rounds, iters);
+  const int mib = argc > 3 ? atoi(argv[3]) : 64;
+  int bad = run<8>(cus, rounds, iters, mib);
+  bad += run<4>(cus, rounds, iters, mib);
+  bad += run<2>(cus, rounds, iters, mib);
   printf("total mismatches: %d\n", bad);
   return bad ? 1 : 0;
 }
