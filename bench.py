@@ -143,6 +143,70 @@ def host_e2e_leg(torch, nbx, srcs, out, stream, op, reps: int = 2):
             "naive_GiBps": round(ALG_BYTES / (nms * 1e-3) / 2**30, 2), "matches_device_result": ok}
 
 
+def host_cpu_share():
+    """(threads this process may run in parallel, CPUs on the box): the
+    affinity mask, capped by the cgroup CPU quota when there is one (the GPU
+    box grants each GPU's jobs a share of the host's CPUs)."""
+    on_box = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = on_box
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), on_box, quota
+
+
+def stream_ceilings(torch, nbx, srcs, out, stream, reps: int = 10):
+    """HBM stream ceilings on THIS box, same process, right after the timed
+    region: read-only over the config-B inputs with the hot
+    kernel's loads and tile, write-only with its stores, and a 1:1 copy
+    (the production kernel at one source) of the config-B byte count."""
+    import ctypes
+    lib = nbx.load_library()
+    lib.nbxDebugStream.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t,
+                                   ctypes.c_int, ctypes.c_void_p]
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    half = ALG_BYTES // 2   # copy: read + write = the config-B byte count
+    a = torch.empty(half // 4, dtype=torch.float32, device=out.device).uniform_(-1, 1)
+    b = torch.empty_like(a)
+    s_arr = (ctypes.c_void_p * N_SRCS)(*[t.data_ptr() for t in srcs])
+    f32 = int(nbx.ncclDataType.ncclFloat32)
+    op = nbx.host_to_dev_redop(nbx.ncclRedOp.ncclSum, nbx.ncclDataType.ncclFloat32, 1)
+    a_arr = (ctypes.c_void_p * 1)(a.data_ptr())
+    b_arr = (ctypes.c_void_p * 1)(b.data_ptr())
+
+    def timed(fn, nbytes):
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return round(nbytes / (e0.elapsed_time(e1) / reps * 1e-3) / 1e9, 1)
+
+    def chk(rc):
+        if rc != 0:
+            raise RuntimeError(f"stream ceiling launch failed: {rc}")
+    rd = timed(lambda: chk(lib.nbxDebugStream(0, out.data_ptr(), s_arr, N_SRCS, COUNT * ELT, 0, sh)),
+               N_SRCS * COUNT * ELT)
+    wr = timed(lambda: chk(lib.nbxDebugStream(1, b.data_ptr(), None, 0, half, 0, sh)), half)
+    cp = timed(lambda: chk(lib.nbxReduceMulti(b_arr, 1, a_arr, 1, half // 4, f32, op, 0, 0, sh)), 2 * half)
+    del a, b
+    return {"read_GBs": rd, "write_GBs": wr, "copy_GBs": cp,
+            "what": "same process, this box: read-only 8 x 256 MiB (hot kernel's nt loads, 8x4 packs/lane, "
+                    "1 WG/CU, nothing stored); write-only 1.125 GiB (plain 16-B stores); 1:1 copy 1.125 GiB -> "
+                    "1.125 GiB (nbxReduceMulti, 1 source)"}
+
+
 def cpu_baseline(seconds: float = 1.5):
     """Oracle (C port of the reference semantics) on host cores, same workload
     shape, bounded sample: passes over the full config-B workload for about
@@ -153,7 +217,8 @@ def cpu_baseline(seconds: float = 1.5):
     import numpy as np
     from oracle import oracle   # checker / baseline only
     oracle.build()
-    threads = int(os.environ.get("NBX_CPU_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    share, on_box, quota = host_cpu_share()
+    threads = int(os.environ.get("NBX_CPU_THREADS", "0")) or share
     rng = np.random.default_rng(1234)
     srcs = [rng.uniform(-1, 1, COUNT).astype(np.float32) for _ in range(N_SRCS)]
     out = [np.empty(COUNT, np.float32)]
@@ -178,6 +243,7 @@ def cpu_baseline(seconds: float = 1.5):
         ta.append(time.perf_counter() - t1)
     ta = min(ta[1:])
     return {"value": round(ALG_BYTES / best / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "cores_used": threads, "cores_on_box": on_box, "cpu_quota": quota,
             "sample": f"{len(passes)} passes of the full config-B workload (8 x 256 MiB fp32 -> 256 MiB), "
                       f"{el:.2f} s wall x {threads} threads, oracle/reduce_oracle.c (gcc -O3); value = best pass, "
                       f"mean {ALG_BYTES / mean / 2**30:.1f} GiB/s",
@@ -466,6 +532,9 @@ def main():
 
     achieved = ALG_BYTES / (kern_avg_ms * 1e-3) / 1e9
     traffic = _pmc_traffic()
+    ceil = None
+    if os.environ.get("NBX_BENCH_CEILING", "1") != "0":
+        ceil = stream_ceilings(torch, nbx, srcs, out, stream)
     result = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -491,6 +560,11 @@ def main():
         "cpu_baseline": None,
         "collective": None,
     }
+    if ceil:
+        rf = result["roofline"]
+        rf["ceiling_read"], rf["ceiling_write"], rf["ceiling_copy"] = ceil["read_GBs"], ceil["write_GBs"], ceil["copy_GBs"]
+        rf["frac_of_ceiling"] = round(achieved / max(ceil["read_GBs"], ceil["copy_GBs"]), 4)
+        rf["ceiling_what"] = ceil["what"] + "; frac_of_ceiling = achieved / max(read, copy)"
     if world == 1 and os.environ.get("NBX_BENCH_E2E", "1") != "0" and not args.no_cpu_baseline:
         result["host_e2e"] = host_e2e_leg(torch, nbx, srcs, out, stream, op)
     if child is not None:

@@ -42,6 +42,16 @@ int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint
  * NBX_LL128_SELFTEST_FAIL=1 makes that self-test report a failure (test hook). */
 int nbxDebugCommProtoMask(ncclComm_t comm);
 
+/* Stream ceilings in the caller's process (SURVEY §8(d) "a measured stream
+ * ceiling"): kind 0 reads nSrcs == 8 buffers of `bytes` each with the hot
+ * kernel's loads and tile (16-B nontemporal, 8 x 4 packs per lane, one
+ * workgroup per CU) and stores nothing; kind 1 writes `bytes` to dst with its
+ * stores (plain 16-B). Buffers 16-B aligned, bytes a multiple of 16;
+ * blocksPerCU 0 = the production shape. Asynchronous on `stream` (a
+ * hipStream_t). The 1:1 copy ceiling is nbxReduceMulti with one source. */
+ncclResult_t nbxDebugStream(int kind, void* dst, const void* const* srcs, int nSrcs, size_t bytes, int blocksPerCU,
+                            ncclStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

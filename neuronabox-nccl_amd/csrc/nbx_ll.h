@@ -32,6 +32,7 @@
 //   3. stores the result; the last block to finish publishes this rank's
 //      done word (= seq) into every peer's buffer and advances the state.
 #pragma once
+#include "nbx_diag.h"
 #include "nbx_functors.h"
 #include "nbx_ll_args.h"
 
@@ -61,17 +62,27 @@ __device__ __forceinline__ void llStoreBytes(unsigned char* p, uint64_t off, uin
     if (off + b < limit) p[off + b] = (unsigned char)(v >> (8 * b));
 }
 
-// Bounded spin until *w >= target; false on timeout/abort.
-__device__ __forceinline__ bool llWait(const uint64_t* w, uint64_t target, const LLArgs& a, uint64_t t0) {
+// A bounded spin gives up: error word (1 timeout, 2 abort) + what it waited for.
+__device__ __forceinline__ void llGiveUp(const LLArgs& a, uint64_t site, int peer, uint64_t target, uint64_t seen,
+                                         uint64_t t0, bool record = true) {
+  const bool aborted = *a.abortWord != 0;
+  if (!aborted && record) diagTimeout(a.errWord, site, peer, target, seen, wall_clock64() - t0);
+  *a.errWord = aborted ? 2 : 1;
+}
+
+__device__ __forceinline__ bool llExpired(const LLArgs& a, uint64_t t0) {
+  return *a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks;
+}
+
+// Bounded spin until *w >= target (peer `peer`'s word); false on timeout/abort.
+__device__ __forceinline__ bool llWait(const uint64_t* w, uint64_t target, const LLArgs& a, uint64_t t0, int peer) {
   uint32_t spins = 0;
   for (;;) {
     const uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (v >= target) return true;
-    if ((++spins & 1023u) == 0u) {
-      if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
-        *a.errWord = *a.abortWord != 0 ? 2 : 1;
-        return false;
-      }
+    if ((++spins & 1023u) == 0u && llExpired(a, t0)) {
+      llGiveUp(a, kDiagCredit, peer, target, v, t0);
+      return false;
     }
   }
 }
@@ -130,7 +141,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
 
   // 0. credits: each target has finished reading this parity's previous use
   if (call.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
-    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0)) sFailed = 1;
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0, (int)threadIdx.x)) sFailed = 1;
   }
   __syncthreads();
   bool failed = sFailed != 0;
@@ -183,11 +194,9 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
           l0 = __hip_atomic_load(line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           l1 = __hip_atomic_load(line + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((uint32_t)(l0 >> 32) == call.flag && (uint32_t)(l1 >> 32) == call.flag) break;
-          if ((++spins & 1023u) == 0u) {
-            if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
-              *a.errWord = *a.abortWord != 0 ? 2 : 1;
-              failed = true;
-            }
+          if ((++spins & 1023u) == 0u && llExpired(a, t0)) {
+            llGiveUp(a, kDiagLLLine, j, call.flag, (uint32_t)(l0 >> 32), t0);
+            failed = true;
           }
         }
         x.u = (l0 & 0xffffffffull) | (l1 << 32);
@@ -264,6 +273,11 @@ __device__ __forceinline__ uint64_t l128Pick(const u32x4 (&v)[kL128MaxRanks], in
   return ((uint64_t)hi << 32) | lo;
 }
 
+// the flag word of v[q] (meaningful in the line's last lane)
+__device__ __forceinline__ uint64_t l128Flag(const u32x4 (&v)[kL128MaxRanks], int q) {
+  return l128Pick(v, q, 1);
+}
+
 template <class Fn>
 __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   using E = typename Fn::Elt;
@@ -282,7 +296,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
 
   // 0. credits (as kLLColl)
   if (call.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
-    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0)) sFailed = 1;
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0, (int)threadIdx.x)) sFailed = 1;
   }
   __syncthreads();
   bool failed = sFailed != 0;
@@ -338,11 +352,10 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
           if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
         }
       }
-      if (need != 0 && (++spins & 1023u) == 0u) {
-        if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
-          *a.errWord = *a.abortWord != 0 ? 2 : 1;
-          failed = true;
-        }
+      if (need != 0 && (++spins & 1023u) == 0u && llExpired(a, t0)) {
+        const int q = __builtin_ctz(need);
+        llGiveUp(a, kDiagLL128Line, q, call.seq, l128Flag(v, q), t0, t == kL128Lanes - 1);
+        failed = true;
       }
     }
     const uint64_t off = i * kL128DataBytes + (uint64_t)t * 16;
@@ -435,7 +448,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
   if (call.needDone != 0 && (int)threadIdx.x < n && (int)threadIdx.x != me) {
-    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0)) sFailed = 1;
+    if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0, (int)threadIdx.x)) sFailed = 1;
   }
   __syncthreads();
   bool failed = sFailed != 0;
@@ -487,11 +500,10 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
             if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
           }
         }
-        if (need != 0 && (++spins & 1023u) == 0u) {
-          if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
-            *a.errWord = *a.abortWord != 0 ? 2 : 1;
-            failed = true;
-          }
+        if (need != 0 && (++spins & 1023u) == 0u && llExpired(a, t0)) {
+          const int q = __builtin_ctz(need);
+          llGiveUp(a, kDiagLL128RS, q, call.seq, l128Flag(v, q), t0, t == kL128Lanes - 1);
+          failed = true;
         }
       }
       union Pk {
@@ -546,11 +558,9 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
                                           kL128LoadAux));
         const uint64_t fw = ((uint64_t)v.w << 32) | v.z;
         if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) break;
-        if ((++spins & 1023u) == 0u) {
-          if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
-            *a.errWord = *a.abortWord != 0 ? 2 : 1;
-            failed = true;
-          }
+        if ((++spins & 1023u) == 0u && llExpired(a, t0)) {
+          llGiveUp(a, kDiagLL128AG, j, call.seq, fw, t0, t == kL128Lanes - 1);
+          failed = true;
         }
       }
       const uint64_t o = i * kL128DataBytes + (uint64_t)t * 16;

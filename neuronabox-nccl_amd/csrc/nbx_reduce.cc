@@ -438,22 +438,31 @@ ncclResult_t reduceMultiImpl(void* const* dsts, int nDsts, const void* const* sr
     return launchPass(ks, dsts, nDsts, srcs, nSrcs, count, op, mask, post, acq, st);
   }
 
-  // > 8 sources: ordered multi-pass left fold through dsts[0]:
-  //   pass 0: dsts[0] = fold(srcs[0..8)); pass k: dsts[0] = fold(dsts[0], next <= 7 srcs).
-  // dsts[0] must not alias a source consumed in a later pass.
+  // > 8 sources: ordered multi-pass left fold through a partial buffer:
+  //   pass 0: part = fold(srcs[0..8)); pass k: part = fold(part, next <= 7 srcs);
+  //   the last pass writes every destination.
+  // The partial lives in dsts[0] unless dsts[0] overlaps a source read by a
+  // later pass — in-place collectives past 8 ranks put the rank's own send
+  // block (= its output) last in fold order — then in stream-ordered scratch
+  // memory, so the fold order (and the result) is unchanged.
   const size_t bytes = count * (size_t)eb;
-  for (int s = kMaxKSrcs; s < nSrcs; s++)
-    if (overlaps(dsts[0], srcs[s], bytes)) return ncclInvalidArgument;
+  bool alias = false;
+  for (int s = kMaxKSrcs; s < nSrcs; s++) alias |= overlaps(dsts[0], srcs[s], bytes);
+  void* part = dsts[0];
+  if (alias) {
+    // graph-capturable (a stream-ordered allocation node); freed after the last pass
+    if (hipMallocAsync(&part, bytes, st) != hipSuccess) return ncclUnhandledCudaError;
+  }
+  void* partDst[1] = {part};
   uint32_t mask = 0;
   if (pre)
     for (int s = 0; s < kMaxKSrcs; s++)
       if (s < nPreOpSrcs) mask |= 1u << s;
-  ncclResult_t r = launchPass(ks, dsts, 1, srcs, kMaxKSrcs, count, op, mask, 0, acq, st);
-  if (r != ncclSuccess) return r;
+  ncclResult_t r = launchPass(ks, partDst, 1, srcs, kMaxKSrcs, count, op, mask, 0, acq, st);
   int next = kMaxKSrcs;
-  while (next < nSrcs) {
+  while (r == ncclSuccess && next < nSrcs) {
     const void* ps[kMaxKSrcs];
-    ps[0] = dsts[0];
+    ps[0] = part;
     int n = 1;
     uint32_t m = 0;
     while (n < kMaxKSrcs && next < nSrcs) {
@@ -461,10 +470,10 @@ ncclResult_t reduceMultiImpl(void* const* dsts, int nDsts, const void* const* sr
       ps[n++] = srcs[next++];
     }
     const bool last = next >= nSrcs;
-    r = launchPass(ks, dsts, last ? nDsts : 1, ps, n, count, op, m, last ? post : 0, acq, st);
-    if (r != ncclSuccess) return r;
+    r = launchPass(ks, last ? dsts : partDst, last ? nDsts : 1, ps, n, count, op, m, last ? post : 0, acq, st);
   }
-  return ncclSuccess;
+  if (alias && hipFreeAsync(part, st) != hipSuccess && r == ncclSuccess) r = ncclUnhandledCudaError;
+  return r;
 }
 
 // Shared misalignment modulo 16 of every pointer of a bucket (-1: mixed).

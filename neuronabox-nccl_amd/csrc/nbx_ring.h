@@ -26,6 +26,7 @@
 // device (graph replays advance it), so they only grow across calls.
 // Included by nbx_kernels.h after foldStore.
 #pragma once
+#include "nbx_diag.h"
 #include "nbx_functors.h"
 #include "nbx_kargs.h"
 #include "nbx_ll_args.h"
@@ -40,7 +41,9 @@ __device__ __forceinline__ bool ringWait(const uint64_t* w, uint64_t target, con
     __builtin_amdgcn_s_sleep(1);
     if ((++spins & 255u) == 0u) {
       if (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks) {
-        *a.errWord = *a.abortWord != 0 ? 2 : 1;
+        const bool aborted = *a.abortWord != 0;
+        if (!aborted) diagTimeout(a.errWord, kDiagRing, (a.rank + a.nRanks - 1) % a.nRanks, target, v, wall_clock64() - t0);
+        *a.errWord = aborted ? 2 : 1;
         return false;
       }
     }

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "nbx_diag.h"
+
 namespace nbx {
 
 // Advances this rank's epoch of flag `slot` (plain device memory, one counter
@@ -39,7 +41,8 @@ __global__ __launch_bounds__(64) void kPeerBarrier(uint64_t* myFlags, uint64_t* 
     const uint64_t* f = peerFlags[lane] + slot;
     const uint64_t t0 = wall_clock64();
     uint32_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+    uint64_t v;
+    while ((v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < seq) {
       __builtin_amdgcn_s_sleep(2);
       if ((++spins & 255u) == 0u) {
         if (*abortWord != 0) {
@@ -47,6 +50,7 @@ __global__ __launch_bounds__(64) void kPeerBarrier(uint64_t* myFlags, uint64_t* 
           break;
         }
         if (wall_clock64() - t0 > timeoutTicks) {
+          diagTimeout(errWord, kDiagBarrier, lane, seq, v, wall_clock64() - t0);
           *errWord = 1;
           break;
         }

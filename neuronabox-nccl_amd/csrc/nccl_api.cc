@@ -46,6 +46,7 @@
 #include "nbx_sync.h"
 #include "nbx_internal.h"
 #include "nbx_ll_args.h"
+#include "nbx_diag.h"
 
 #define NBX_EXPORT extern "C" __attribute__((visibility("default")))
 // NCCL_API (src/include/core.h:17-32): every entry point plus a p-prefixed alias.
@@ -694,6 +695,7 @@ struct MpState {
   bool ring = false;                // NCCL_ALGO=Ring at init
   bool multiGpu = false;            // the ranks span more than one physical GPU (PCI key)
   bool ringPipeline = true;         // ring as the pipelined kernel (nbx_ring.h); NBX_RING_PIPELINE=0: per-step kernels
+  bool groupBatch = true;           // NBX_GROUP_BATCH at init: groups run as batched exchanges
   uint64_t* ringProg = nullptr;     // [kRingMaxGrid] progress words the left neighbour posts (uncached)
   uint64_t* rightRingProg = nullptr;// the right neighbour's words (peer mapping)
   nbx::RingState* ringState = nullptr;
@@ -713,6 +715,14 @@ struct MpInitInfo {
   uint64_t l128MaxBytes;
   uint64_t l128OneShotMax;
   int32_t protoMask;
+  // schedule settings every rank must share: a workgroup of the pipelined ring
+  // waits on its left neighbour's progress word of the same slice, so a
+  // different grid (NBX_RING_MAX_GRID) or schedule would fold unfinished
+  // partials or drift the barrier epochs apart
+  int32_t ring;           // NCCL_ALGO=Ring
+  int32_t ringPipeline;   // NBX_RING_PIPELINE
+  int32_t ringMaxGrid;    // NBX_RING_MAX_GRID
+  int32_t groupBatch;     // NBX_GROUP_BATCH
 };
 
 // NCCL_PROTO (tuning.cc:254-259, parseList): a comma-separated list of the
@@ -894,6 +904,28 @@ hipError_t allocSyncMem(void** p, size_t bytes) {
 }
 
 ncclResult_t mpLL128SelfTest(ncclComm* c);
+bool groupBatchEnabled();
+
+// A device spin gave up (host error word set): name the wait, the peer, the
+// value it waited for and the last one it saw (nbx_diag.h), once per record.
+void mpReportDeviceError(ncclComm* c) {
+  MpState* mp = c->mp;
+  if (!mp || !mp->hostWords || mp->hostWords[1] == 0) return;
+  const volatile uint64_t* d = (const volatile uint64_t*)((const volatile char*)mp->hostWords + nbx::kDiagByteOffset);
+  static thread_local uint64_t lastReported[nbx::kDiagWords] = {};
+  uint64_t rec[nbx::kDiagWords];
+  for (int i = 0; i < nbx::kDiagWords; i++) rec[i] = d[i];
+  if (std::memcmp(rec, lastReported, sizeof(rec)) == 0) return;
+  std::memcpy(lastReported, rec, sizeof(rec));
+  if (mp->hostWords[1] == 2) {
+    warn("comm %p rank %d: a device wait was aborted (ncclCommAbort)", (void*)c, c->rank);
+    return;
+  }
+  warn("comm %p rank %d: device wait timed out after %.3f s: %s of peer %lld, waited for %llu, last saw %llu "
+       "(workgroup %llu)", (void*)c, c->rank, (double)rec[5] * 1e-8, nbx::diagSiteName(rec[0]),
+       (long long)(int64_t)rec[1], (unsigned long long)rec[2], (unsigned long long)rec[3],
+       (unsigned long long)rec[4]);
+}
 
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   MpState* mp = new MpState();
@@ -961,6 +993,11 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.l128MaxBytes = mp->l128MaxBytes;
   mine.l128OneShotMax = mp->l128OneShotMax;
   mine.protoMask = mp->protoMask;
+  mp->groupBatch = groupBatchEnabled();
+  mine.ring = mp->ring;
+  mine.ringPipeline = mp->ringPipeline;
+  mine.ringMaxGrid = (int32_t)mp->ringMaxGrid;
+  mine.groupBatch = mp->groupBatch;
   HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
   if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
@@ -982,6 +1019,11 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
         all[j].l128OneShotMax != mp->l128OneShotMax || all[j].protoMask != mp->protoMask) {
       warn("ncclCommInitRank : NCCL_PROTO / NBX_LL_MAX_BYTES / NBX_LL128_MAX_BYTES / NBX_LL128_ONESHOT_MAX differ "
            "across ranks");
+      return ncclInvalidUsage;
+    }
+    if (all[j].ring != mine.ring || all[j].ringPipeline != mine.ringPipeline ||
+        all[j].ringMaxGrid != mine.ringMaxGrid || all[j].groupBatch != mine.groupBatch) {
+      warn("ncclCommInitRank : NCCL_ALGO / NBX_RING_PIPELINE / NBX_RING_MAX_GRID / NBX_GROUP_BATCH differ across ranks");
       return ncclInvalidUsage;
     }
     if (j == c->rank) {
@@ -1421,6 +1463,12 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
         r = ncclUnhandledCudaError;
         break;
       }
+      if (mp->hostWords[1] != 0) {   // a device wait gave up: an error, not a torn line
+        mpReportDeviceError(c);
+        warn("comm %p rank %d: LL128 self-test call %ld (%zu elements) did not complete", (void*)c, me, it, count);
+        r = ncclRemoteError;
+        break;
+      }
       for (size_t i = 0; i < count && !bad; i++) {
         int64_t want = 0;
         for (int q = 0; q < n; q++) want += (int64_t)((i * 7 + (size_t)q * 13 + (size_t)it * 101) % 1000);
@@ -1617,7 +1665,7 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
   }
   if (comm->mp) {
     const MpCall call{kind, sendbuff, recvbuff, count, dt, opFull, root, stream};
-    if (t_groupDepth > 0 && groupBatchEnabled()) {   // run at the outermost ncclGroupEnd
+    if (t_groupDepth > 0 && comm->mp->groupBatch) {   // run at the outermost ncclGroupEnd
       if (comm->mp->group.empty()) t_groupMpComms.push_back(comm);
       comm->mp->group.push_back(call);
       return ncclSuccess;
@@ -1840,8 +1888,10 @@ NBX_API(ncclResult_t, ncclCommGetAsyncError, ncclComm_t comm, ncclResult_t* asyn
   NCCLCHECK(commCheck(comm, "ncclGetAsyncError"));
   if (asyncError == nullptr) return ncclInvalidArgument;
   *asyncError = (ncclResult_t)comm->asyncError.load();
-  if (*asyncError == ncclSuccess && comm->mp && comm->mp->hostWords && comm->mp->hostWords[1] != 0)
+  if (*asyncError == ncclSuccess && comm->mp && comm->mp->hostWords && comm->mp->hostWords[1] != 0) {
     *asyncError = ncclRemoteError;   // a peer barrier timed out or was aborted
+    mpReportDeviceError(comm);
+  }
   return ncclSuccess;
 }
 

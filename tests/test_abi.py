@@ -96,7 +96,7 @@ def test_reduce_multi_argument_checks_before_device(nbx):
     E = 4
     fake = 0x10000
     assert nbx.reduce_multi_raw([fake], [], 16, 7, op) == E
-    assert nbx.reduce_multi_raw([fake], [fake] * 33, 16, 7, op) == E
+    assert nbx.reduce_multi_raw([fake], [fake] * 65, 16, 7, op) == E   # > NBX_MAX_SRCS
     assert nbx.reduce_multi_raw([], [fake], 16, 7, op) == E
     assert nbx.reduce_multi_raw([fake], [fake], 16, -1, op) == E
     op.op = 9

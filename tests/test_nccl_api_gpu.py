@@ -212,6 +212,55 @@ def test_clique_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, nranks):
             c.destroy()
 
 
+@pytest.mark.parametrize("nranks", [9, 12])
+def test_clique_in_place_past_8_ranks(nbx, oracle, torch_gpu, nranks):
+    """In-place AllReduce (recv == send), ReduceScatter (recv == send +
+    rank * recvcount) and Reduce (root's recv == send) with more than 8 ranks:
+    the fold takes several passes and the rank's own block — its output — is
+    read last, so the partial goes through scratch memory. Checked
+    against the oracle in the schedule's fold order."""
+    torch = torch_gpu
+    comms = nbx.Communicator.init_all([0] * nranks)
+    try:
+        count = 20011
+        xs = oracle.random_inputs(F32, nranks, count, seed=900 + nranks)
+        txs = [t_of(torch, x) for x in xs]
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].all_reduce(txs[r].data_ptr(), txs[r].data_ptr(), count, F32, 0, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        exp = _ring_order_reduce(oracle, xs, F32, 0, 0, False, nranks, _blocks(count, 4, nranks))
+        for r in range(nranks):
+            assert np.array_equal(np_of(txs[r], np.float32), exp), f"allreduce rank {r}"
+        rc = 3001
+        ys = oracle.random_inputs(I32, nranks, rc * nranks, seed=910 + nranks)
+        tys = [t_of(torch, y) for y in ys]
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].reduce_scatter(tys[r].data_ptr(), tys[r].data_ptr() + r * rc * 4, rc, I32, 4, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        devop, arg = oracle.host_to_dev_redop(4, I32, nranks)
+        exp = _ring_order_reduce(oracle, ys, I32, devop, arg, True, nranks, lambda b: (b * rc, (b + 1) * rc))
+        for r in range(nranks):
+            got = np_of(tys[r], np.int32)[r * rc:(r + 1) * rc]
+            assert np.array_equal(got, exp[r * rc:(r + 1) * rc]), f"reduce_scatter rank {r}"
+        zs = oracle.random_inputs(F32, nranks, count, seed=920 + nranks)
+        tzs = [t_of(torch, z) for z in zs]
+        root = nranks - 1
+        nbx.group_start()
+        for r in range(nranks):
+            comms[r].reduce(tzs[r].data_ptr(), tzs[r].data_ptr() if r == root else 0, count, F32, 0, root, 0)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        exp = _ring_order_reduce(oracle, zs, F32, 0, 0, False, nranks, _blocks(count, 4, nranks), root=root)
+        assert np.array_equal(np_of(tzs[root], np.float32), exp)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 @pytest.mark.parametrize("nranks", [2, 3, 9])
 def test_clique_grouped_collectives_batched(nbx, oracle, torch_gpu, nranks):
     """A group of independent collectives runs as one batched exchange (one

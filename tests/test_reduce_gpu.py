@@ -444,8 +444,25 @@ def test_invalid_arguments(nbx, torch_gpu):
     op.op = 0
     assert nbx.reduce_multi_raw([p], [p + 2], 16, 7, op) == E                  # not element-aligned
     assert nbx.reduce_multi_raw([0], [p], 16, 7, op) == E                      # NULL dst
-    srcs = [p + 4 * 16 * k for k in range(9)]
-    assert nbx.reduce_multi_raw([srcs[8]], srcs, 16, 7, op) == E               # dst aliases a later-pass src
+
+
+@pytest.mark.parametrize("nsrc,alias", [(9, 8), (9, 0), (16, 15), (20, 9), (20, 19), (64, 63)])
+def test_multipass_destination_aliases_a_source(nbx, oracle, torch_gpu, nsrc, alias):
+    """More than 8 sources fold in passes; when the destination IS a source a
+    later pass reads (in-place collectives past 8 ranks: the rank's own block
+    is last in fold order), the partial goes through scratch memory and the
+    result is still the oracle's left fold (this used to be
+    ncclInvalidArgument)."""
+    torch = torch_gpu
+    count = 100003
+    srcs = oracle.random_inputs(7, nsrc, count, seed=300 + nsrc + alias)
+    ts = [torch.from_numpy(x.copy()).cuda() for x in srcs]
+    op = nbx.DevRedOpFull()
+    nbx.reduce_multi([ts[alias].data_ptr(), ], [t.data_ptr() for t in ts], count, 7, op, 0, False,
+                     torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    exp = oracle.reduce_multi(srcs, 7, 0, threads=8)[0]
+    assert_same(ts[alias].cpu().numpy(), exp, 7)
 
 
 def test_config_b_full_size_bit_exact(nbx, oracle, torch_gpu):
