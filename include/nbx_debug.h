@@ -52,6 +52,16 @@ int nbxDebugCommProtoMask(ncclComm_t comm);
 ncclResult_t nbxDebugStream(int kind, void* dst, const void* const* srcs, int nSrcs, size_t bytes, int blocksPerCU,
                             ncclStream_t stream);
 
+/* A deliberately torn LL128 line against the collectives' own line reader
+ * (nbx_ll.h l128Poll + l128FoldLine), one GPU: a writer kernel stores the
+ * line's last 32 bytes, waits delayUs, then its first 32 bytes (tear = 1; 0
+ * stores it whole); a reader kernel on another stream polls it. Returns 0 if
+ * the reader folded exactly the new payload and (tear = 1) accepted the line
+ * only after its second half was issued; 1 stale payload folded; 2 accepted
+ * early; 3 the reader timed out; < 0 HIP error. *acceptAfterTornTicks =
+ * acceptance time minus second-half issue time (100 MHz ticks). */
+int nbxDebugLL128TearTest(int delayUs, int tear, long long* acceptAfterTornTicks);
+
 #ifdef __cplusplus
 }
 #endif

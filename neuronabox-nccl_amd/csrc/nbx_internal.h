@@ -7,6 +7,7 @@
 namespace nbx {
 struct LLArgs;
 struct RingArgs;
+struct RingFifoArgs;
 // nbxReduceMulti with internal flags: kReduceAcquireSystem makes every
 // workgroup issue a system-scope acquire before its first load (sources in
 // peer GPU memory, written before the launch and ordered by a flag barrier).
@@ -25,6 +26,9 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
 // Pipelined ring AllReduce (nbx_ring.h), `grid` workgroups = slices per chunk.
 ncclResult_t launchRingAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, RingArgs& args, unsigned grid,
                                  hipStream_t stream);
+// Step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h kRingFifo).
+ncclResult_t launchRingFifo(ncclDataType_t dt, const nbxDevRedOpFull& op, RingFifoArgs& args, unsigned grid,
+                            hipStream_t stream);
 // LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
                                    hipStream_t stream);

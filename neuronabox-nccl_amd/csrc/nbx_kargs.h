@@ -66,6 +66,7 @@ struct KernelSet {
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)
   const void* ring;                 // pipelined ring AllReduce (nbx_ring.h)
+  const void* ringFifo;             // step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h)
   const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;

@@ -533,6 +533,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;
   ks.ring = (const void*)&kRingAllReduce<Fn>;
+  ks.ringFifo = (const void*)&kRingFifo<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.valid = 1;
   return ks;

@@ -225,24 +225,33 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
 
 // ---------------------------------------------------------------------------
 // LL128 protocol for medium messages (NCCL's LL128 idea, prims_ll128.h:185-291:
-// lines of several 16-byte lane chunks, one flag word per line, the whole line
-// moved by ONE wave store instruction and polled by ONE wave load
-// instruction, so a reader whose flag lane sees the flag trusts the rest of
-// the line). NCCL uses 128-byte lines (120 payload bytes + 8-byte flag) and
-// relies on NVLink delivering a 128-byte store whole. gfx950 does not: a
-// 128-byte line torn at its 64-byte halves was observed (flag half new,
-// first half stale; scripts/ll128_stress.py, profiles/r1/ll128_stress_128B.jsonl),
-// so lines here are 64 bytes — 56 payload bytes in words 0..6 and the flag
-// (= seq) in word 7, four consecutive lanes per line, 16 bytes each:
-// global_store_dwordx4 sc0 sc1 (system scope) on the writer,
-// buffer_load_dwordx4 sc0 sc1 (volatile) on the reader, flag checked by lane 3
-// and broadcast with a width-4 __shfl. Payload efficiency 87.5 % (LL: 50 %).
-// Buffers, parities, done words and credits are the LL protocol's (above).
-// Restricted to n <= 8 ranks (one node): a lane keeps the line of every source
-// in registers and folds each 8-byte word in its own direct-schedule order.
+// lines of several 16-byte lane chunks moved by ONE wave store instruction and
+// polled by ONE wave load instruction, most of each line payload).
+// NCCL's 128-byte line carries ONE flag and relies on NVLink delivering a
+// 128-byte store whole. gfx950 does not: a 128-byte line tore at its 64-byte
+// halves (scripts/ll128_stress.py, profiles/r1/ll128_stress_128B.jsonl), and
+// nothing guarantees that a 64-byte line crossing xGMI arrives whole either.
+// So here EVERY 16-byte lane chunk carries its own 32-bit flag (= seq) in
+// dword 3 — the LL idea ({data, flag} per store, prims_ll.h:226-294) at
+// 16-byte granularity: a reader accepts a line only when all four chunks show
+// the flag, so a line torn at any 16-byte boundary is waited on, never folded
+// (tests/test_multiprocess_gpu.py::test_ll128_torn_line_is_waited_on). The
+// remaining assumption is that one 16-byte aligned global_store_dwordx4 lands
+// whole.
+// Line: 64 bytes = 4 lanes x {12 payload bytes, flag}; 48 payload bytes as two
+// pairs of lanes, each pair 24 bytes = 8-byte words W0, W1, W2:
+//   lane A (even) {W0.lo, W0.hi, W1.lo, flag}   lane B (odd) {W2.lo, W2.hi, W1.hi, flag}
+// so every 8-byte word is folded whole by one lane (A: W0 and W1, taking
+// W1.hi from B by a lane shuffle; B: W2) in its own direct-schedule order.
+// Writer: global_store_dwordx4 sc0 sc1 (system scope); reader:
+// buffer_load_dwordx4 sc0 sc1 (volatile) and a wave ballot per 4-lane line.
+// Payload efficiency 75 % (LL: 50 %). Buffers, parities, done words and
+// credits are the LL protocol's (above). Restricted to n <= 8 ranks (one
+// node): a lane keeps the chunk of every source in registers.
 constexpr int kL128Lanes = 4;                 // lanes per line
 constexpr int kL128LineBytes = 64;
-constexpr int kL128DataBytes = 56;
+constexpr int kL128DataBytes = 48;
+constexpr int kL128PairBytes = 24;            // payload of a lane pair: words W0, W1, W2
 constexpr int kL128MaxRanks = kL128MaxRanksHost;
 constexpr int kL128LoadAux = 1 | 16 | (int)(1u << 31);   // sc0 sc1 (system scope), volatile
 static_assert(kL128LineBytes == kL128LineBytesHost && kL128DataBytes == kL128DataBytesHost &&
@@ -252,36 +261,128 @@ __device__ __forceinline__ void l128StoreLine16(uint64_t* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-// lane t's 16 bytes of payload line i (the last lane: 8 payload bytes + the flag word)
-__device__ __forceinline__ u32x4 l128Payload(const unsigned char* src, uint64_t bytes, uint64_t i, int t,
-                                             uint64_t flagWord) {
-  const uint64_t off = i * kL128DataBytes + (uint64_t)t * 16;
-  const uint64_t w0 = llLoadBytes(src, off, bytes);
-  const uint64_t w1 = t == kL128Lanes - 1 ? flagWord : llLoadBytes(src, off + 8, bytes);
-  return (u32x4){(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+// byte offset (in the message) of lane t's pair in line i, and of its first whole word
+__device__ __forceinline__ uint64_t l128PairOff(uint64_t i, int t) {
+  return i * kL128DataBytes + (uint64_t)(t >> 1) * kL128PairBytes;
+}
+__device__ __forceinline__ uint64_t l128WordOff(uint64_t i, int t) { return l128PairOff(i, t) + ((t & 1) ? 16u : 0u); }
+
+// lane t's chunk of line i of `src` (bytes long) from its words, flag in dword 3
+__device__ __forceinline__ u32x4 l128Chunk(const unsigned char* src, uint64_t bytes, uint64_t i, int t,
+                                           uint32_t flag) {
+  const uint64_t w = llLoadBytes(src, l128WordOff(i, t), bytes);
+  const uint64_t w1 = llLoadBytes(src, l128PairOff(i, t) + 8, bytes);
+  return (u32x4){(uint32_t)w, (uint32_t)(w >> 32), (t & 1) ? (uint32_t)(w1 >> 32) : (uint32_t)w1, flag};
 }
 
-// word k (0/1) of v[j] for a runtime j < 8, as a select chain (no scratch)
-__device__ __forceinline__ uint64_t l128Pick(const u32x4 (&v)[kL128MaxRanks], int j, int k) {
+// every lane of this lane's 4-lane line group sees `ok` (lanes of a group are
+// always active together, so their ballot bits are current)
+__device__ __forceinline__ bool l128LineReady(bool ok) {
+  const uint64_t b = __ballot((int)ok);
+  const uint64_t gm = 0xFull << ((threadIdx.x & 63u) & ~3u);
+  return (b & gm) == gm;
+}
+
+// the other lane of the pair's dword (every lane of the group participates)
+__device__ __forceinline__ uint32_t l128Partner(uint32_t x) { return (uint32_t)__shfl_xor((int)x, 1, kL128Lanes); }
+
+// word k of source j's chunk for a runtime j < 8 (select chain, no scratch):
+// k = 0 the lane's whole word (x, y); k = 1 (lane A only) W1 = (z, pz = B's z)
+__device__ __forceinline__ uint64_t l128Pick(const u32x4 (&v)[kL128MaxRanks], const uint32_t (&pz)[kL128MaxRanks],
+                                             int j, int k) {
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int q = 0; q < kL128MaxRanks; q++) {
     const bool m = q == j;
     lo = m ? (k ? v[q].z : v[q].x) : lo;
-    hi = m ? (k ? v[q].w : v[q].y) : hi;
+    hi = m ? (k ? pz[q] : v[q].y) : hi;
   }
   return ((uint64_t)hi << 32) | lo;
 }
 
-// the flag word of v[q] (meaningful in the line's last lane)
-__device__ __forceinline__ uint64_t l128Flag(const u32x4 (&v)[kL128MaxRanks], int q) {
-  return l128Pick(v, q, 1);
+__device__ __forceinline__ uint32_t l128FlagOf(const u32x4 (&v)[kL128MaxRanks], int j) {
+  uint32_t f = 0;
+#pragma unroll
+  for (int q = 0; q < kL128MaxRanks; q++) f = q == j ? v[q].w : f;
+  return f;
+}
+
+// Poll the chunks of the sources in `need` (slot byte offset slotOff(q)) until
+// every chunk of the line shows `flag`; false if the wait gave up.
+template <class SlotOff>
+__device__ __forceinline__ bool l128Poll(const LLArgs& a, __amdgpu_buffer_rsrc_t rs, u32x4 (&v)[kL128MaxRanks],
+                                         uint32_t need, uint32_t flag, uint64_t site, uint64_t t0, int t,
+                                         SlotOff slotOff) {
+  uint32_t spins = 0;
+  while (need != 0) {
+#pragma unroll
+    for (int q = 0; q < kL128MaxRanks; q++)
+      if ((need >> q) & 1u)
+        v[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, slotOff(q) + (uint32_t)t * 16u, 0,
+                                                                               kL128LoadAux));
+#pragma unroll
+    for (int q = 0; q < kL128MaxRanks; q++)
+      if (((need >> q) & 1u) && l128LineReady(v[q].w == flag)) need &= ~(1u << q);
+    if (need != 0 && (++spins & 1023u) == 0u && llExpired(a, t0)) {
+      const int q = __builtin_ctz(need);
+      llGiveUp(a, site, q, flag, l128FlagOf(v, q), t0, t == 0);
+      return false;
+    }
+  }
+  return true;
+}
+
+// Fold lane t's words of line i over the n sources in v (own contribution
+// included) in the direct schedule's order, apply postOp, and hand each word
+// to `sink(k, byteOffset, word)`: lane A words k = 0 (W0), 1 (W1); lane B k = 0 (W2).
+template <class Fn, class Sink>
+__device__ __forceinline__ void l128FoldLine(const Fn& fn, const LLArgs& a, const u32x4 (&v)[kL128MaxRanks], uint64_t i,
+                                             int t, int fixedFirst, Sink sink) {
+  using E = typename Fn::Elt;
+  constexpr int EPK = 8 / (int)sizeof(E);
+  const int n = a.nRanks;
+  uint32_t pz[kL128MaxRanks];
+#pragma unroll
+  for (int q = 0; q < kL128MaxRanks; q++) pz[q] = l128Partner(v[q].z);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if (k == 1 && (t & 1)) break;   // lane B owns one word
+    const uint64_t off = k ? l128PairOff(i, t) + 8 : l128WordOff(i, t);
+    int first = fixedFirst;
+    if (first < 0) {   // AllReduce: the word's block c folds c+1, ..., c (8-byte words never straddle blocks)
+      const int c = (int)((off / sizeof(E)) / a.blockElts);
+      first = (c + 1) % n;
+    }
+    union Pk {
+      uint64_t u;
+      E e[EPK];
+    };
+    Pk acc;
+    acc.u = 0;
+    for (int q = 0; q < n; q++) {
+      const int j = first + q < n ? first + q : first + q - n;
+      Pk x;
+      x.u = l128Pick(v, pz, j, k);
+#pragma unroll
+      for (int e = 0; e < EPK; e++) {
+        E y = x.e[e];
+        if constexpr (Fn::kHasPre) y = fn.pre(y);   // PreMulSum: every contribution pre-multiplied once
+        acc.e[e] = q == 0 ? y : fn.red(acc.e[e], y);
+      }
+    }
+    if constexpr (Fn::kHasPost) {
+      if (a.postOp) {
+#pragma unroll
+        for (int e = 0; e < EPK; e++) acc.e[e] = fn.post(acc.e[e]);
+      }
+    }
+    sink(k, off, acc.u);
+  }
 }
 
 template <class Fn>
 __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   using E = typename Fn::Elt;
-  constexpr int EPK = 8 / (int)sizeof(E);
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
   const int t = (int)(threadIdx.x % kL128Lanes);   // lane within the line's group
@@ -305,11 +406,11 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   if (!failed) {
     for (uint64_t i = g0; i < a.nLines; i += groups) {
       u32x4 whole = {0, 0, 0, 0};
-      if (a.mode != kLLReduceScatter) whole = l128Payload((const unsigned char*)a.send, bytes, i, t, call.seq);
+      if (a.mode != kLLReduceScatter) whole = l128Chunk((const unsigned char*)a.send, bytes, i, t, call.flag);
       for (int j = 0; j < n; j++) {
         if (!llIsTarget(a, j)) continue;
         const u32x4 v = a.mode == kLLReduceScatter
-                            ? l128Payload((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, call.seq)
+                            ? l128Chunk((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, call.flag)
                             : whole;
         uint64_t* line = a.peerL128[j] + ((uint64_t)(call.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) +
                          2 * t;
@@ -318,82 +419,29 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
     }
   }
 
-  // 2.+3. poll own slots (all sources' line i in registers), fold, store
+  // 2.+3. poll own slots (every source's chunk of line i in registers), fold, store
   const bool receives = a.mode != kLLReduce || me == a.root;
   const unsigned char* own = (const unsigned char*)a.send + (a.mode == kLLReduceScatter ? (uint64_t)me * bytes : 0);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.myL128, (short)0, (int)a.l128Bytes,
                                                                       0x00020000);
-  for (uint64_t i = g0; receives && i < a.nLines; i += groups) {
+  const int fixedFirst = a.mode == kLLAllReduce ? -1 : ((a.mode == kLLReduce ? a.root : me) + 1) % n;
+  for (uint64_t i = g0; receives && !failed && i < a.nLines; i += groups) {
     u32x4 v[kL128MaxRanks];
     uint32_t need = 0;
 #pragma unroll
     for (int q = 0; q < kL128MaxRanks; q++) {
       v[q] = (u32x4){0, 0, 0, 0};
       if (q < n) {
-        if (q == me) v[q] = l128Payload(own, bytes, i, t, 0);
+        if (q == me) v[q] = l128Chunk(own, bytes, i, t, 0);
         else need |= 1u << q;
       }
     }
-    uint32_t spins = 0;
-    while (need != 0 && !failed) {
-#pragma unroll
-      for (int q = 0; q < kL128MaxRanks; q++) {
-        if ((need >> q) & 1u) {
-          const uint32_t off = (uint32_t)((((uint64_t)(call.parity * n + q)) * a.l128SlotLines + i) *
-                                          kL128LineBytes) + (uint32_t)t * 16u;
-          v[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kL128LoadAux));
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < kL128MaxRanks; q++) {
-        if ((need >> q) & 1u) {
-          const uint64_t fw = ((uint64_t)v[q].w << 32) | v[q].z;
-          // the group's last lane holds the flag
-          if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
-        }
-      }
-      if (need != 0 && (++spins & 1023u) == 0u && llExpired(a, t0)) {
-        const int q = __builtin_ctz(need);
-        llGiveUp(a, kDiagLL128Line, q, call.seq, l128Flag(v, q), t0, t == kL128Lanes - 1);
-        failed = true;
-      }
-    }
-    const uint64_t off = i * kL128DataBytes + (uint64_t)t * 16;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      if (k == 1 && t == kL128Lanes - 1) break;   // the line's last word is the flag
-      int first;
-      if (a.mode == kLLAllReduce) {
-        const int c = (int)(((off + 8 * k) / sizeof(E)) / a.blockElts);   // 8-byte words never straddle blocks
-        first = (c + 1) % n;
-      } else {
-        first = ((a.mode == kLLReduce ? a.root : me) + 1) % n;
-      }
-      union Pk {
-        uint64_t u;
-        E e[EPK];
-      };
-      Pk acc;
-      acc.u = 0;
-      for (int q = 0; q < n; q++) {
-        const int j = first + q < n ? first + q : first + q - n;
-        Pk x;
-        x.u = l128Pick(v, j, k);
-#pragma unroll
-        for (int e = 0; e < EPK; e++) {
-          E y = x.e[e];
-          if constexpr (Fn::kHasPre) y = fn.pre(y);
-          acc.e[e] = q == 0 ? y : fn.red(acc.e[e], y);
-        }
-      }
-      if constexpr (Fn::kHasPost) {
-        if (a.postOp) {
-#pragma unroll
-          for (int e = 0; e < EPK; e++) acc.e[e] = fn.post(acc.e[e]);
-        }
-      }
-      llStoreBytes((unsigned char*)a.recv, off + 8 * k, bytes, acc.u);
-    }
+    failed = !l128Poll(a, rs, v, need, call.flag, kDiagLL128Line, t0, t, [&](int q) {
+      return (uint32_t)((((uint64_t)(call.parity * n + q)) * a.l128SlotLines + i) * kL128LineBytes);
+    });
+    l128FoldLine(fn, a, v, i, t, fixedFirst, [&](int, uint64_t off, uint64_t w) {
+      llStoreBytes((unsigned char*)a.recv, off, bytes, w);
+    });
   }
 
   // done word (as kLLColl)
@@ -433,7 +481,6 @@ __device__ __forceinline__ void l128BlockRange(const LLArgs& a, int j, int eb, u
 template <class Fn>
 __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
   using E = typename Fn::Elt;
-  constexpr int EPK = 8 / (int)sizeof(E);
   constexpr int eb = (int)sizeof(E);
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
@@ -463,7 +510,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
     l128BlockRange(a, j, eb, &off, &len);
     const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
     for (uint64_t i = g0; i < lines; i += groups) {
-      const u32x4 v = l128Payload(send + off, len, i, t, call.seq);
+      const u32x4 v = l128Chunk(send + off, len, i, t, call.flag);
       l128StoreLine16(a.peerL128[j] + (subSlot(0, me) + i) * (kL128LineBytes / 8) + 2 * t, v);
     }
   }
@@ -474,69 +521,27 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
     const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
     const bool reduce = a.mode == kLLReduce;
     const int first = ((reduce ? a.root : me) + 1) % n;
-    for (uint64_t i = g0; i < lines; i += groups) {
+    for (uint64_t i = g0; i < lines && !failed; i += groups) {
       u32x4 v[kL128MaxRanks];
       uint32_t need = 0;
 #pragma unroll
       for (int q = 0; q < kL128MaxRanks; q++) {
         v[q] = (u32x4){0, 0, 0, 0};
         if (q < n) {
-          if (q == me) v[q] = l128Payload(send + off, len, i, t, 0);
+          if (q == me) v[q] = l128Chunk(send + off, len, i, t, 0);
           else need |= 1u << q;
         }
       }
-      uint32_t spins = 0;
-      while (need != 0 && !failed) {
-#pragma unroll
-        for (int q = 0; q < kL128MaxRanks; q++)
-          if ((need >> q) & 1u)
-            v[q] = __builtin_bit_cast(
-                u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                           rs, (uint32_t)((subSlot(0, q) + i) * kL128LineBytes) + (uint32_t)t * 16u, 0, kL128LoadAux));
-#pragma unroll
-        for (int q = 0; q < kL128MaxRanks; q++) {
-          if ((need >> q) & 1u) {
-            const uint64_t fw = ((uint64_t)v[q].w << 32) | v[q].z;
-            if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) need &= ~(1u << q);
-          }
-        }
-        if (need != 0 && (++spins & 1023u) == 0u && llExpired(a, t0)) {
-          const int q = __builtin_ctz(need);
-          llGiveUp(a, kDiagLL128RS, q, call.seq, l128Flag(v, q), t0, t == kL128Lanes - 1);
-          failed = true;
-        }
-      }
-      union Pk {
-        uint64_t u;
-        E e[EPK];
-      };
-      uint64_t w[2] = {0, call.seq};
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        if (k == 1 && t == kL128Lanes - 1) break;   // the flag word
-        Pk acc;
-        acc.u = 0;
-        for (int q = 0; q < n; q++) {
-          const int j = first + q < n ? first + q : first + q - n;
-          Pk x;
-          x.u = l128Pick(v, j, k);
-#pragma unroll
-          for (int e = 0; e < EPK; e++) {
-            E y = x.e[e];
-            if constexpr (Fn::kHasPre) y = fn.pre(y);
-            acc.e[e] = q == 0 ? y : fn.red(acc.e[e], y);
-          }
-        }
-        if constexpr (Fn::kHasPost) {
-          if (a.postOp) {
-#pragma unroll
-            for (int e = 0; e < EPK; e++) acc.e[e] = fn.post(acc.e[e]);
-          }
-        }
-        w[k] = acc.u;
-        if (!reduce || me == a.root) llStoreBytes(recv + off, i * kL128DataBytes + (uint64_t)t * 16 + 8 * k, len, acc.u);
-      }
-      const u32x4 line = {(uint32_t)w[0], (uint32_t)(w[0] >> 32), (uint32_t)w[1], (uint32_t)(w[1] >> 32)};
+      failed = !l128Poll(a, rs, v, need, call.flag, kDiagLL128RS, t0, t,
+                         [&](int q) { return (uint32_t)((subSlot(0, q) + i) * kL128LineBytes); });
+      uint64_t w[2] = {0, 0};
+      l128FoldLine(fn, a, v, i, t, first, [&](int k, uint64_t o, uint64_t r) {
+        w[k] = r;
+        if (!reduce || me == a.root) llStoreBytes(recv + off, o, len, r);
+      });
+      // the folded line in the chunk layout: lane B takes W1.hi from lane A
+      const uint32_t w1hi = l128Partner((uint32_t)(w[1] >> 32));
+      const u32x4 line = {(uint32_t)w[0], (uint32_t)(w[0] >> 32), (t & 1) ? w1hi : (uint32_t)w[1], call.flag};
       for (int j = 0; j < n; j++) {
         if (j == me || failed || (reduce && j != a.root)) continue;
         l128StoreLine16(a.peerL128[j] + (subSlot(1, me) + i) * (kL128LineBytes / 8) + 2 * t, line);
@@ -544,28 +549,20 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
     }
   }
   // C. the other blocks arrive folded: copy them into recv
-  for (int j = 0; j < n && (a.mode != kLLReduce || me == a.root); j++) {
+  for (int j = 0; j < n && !failed && (a.mode != kLLReduce || me == a.root); j++) {
     if (j == me) continue;
     uint64_t off, len;
     l128BlockRange(a, j, eb, &off, &len);
     const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
-    for (uint64_t i = g0; i < lines; i += groups) {
-      u32x4 v = {0, 0, 0, 0};
-      uint32_t spins = 0;
-      while (!failed) {
-        v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          rs, (uint32_t)((subSlot(1, j) + i) * kL128LineBytes) + (uint32_t)t * 16u, 0,
-                                          kL128LoadAux));
-        const uint64_t fw = ((uint64_t)v.w << 32) | v.z;
-        if (__shfl((int)(fw == call.seq), kL128Lanes - 1, kL128Lanes)) break;
-        if ((++spins & 1023u) == 0u && llExpired(a, t0)) {
-          llGiveUp(a, kDiagLL128AG, j, call.seq, fw, t0, t == kL128Lanes - 1);
-          failed = true;
-        }
-      }
-      const uint64_t o = i * kL128DataBytes + (uint64_t)t * 16;
-      llStoreBytes(recv + off, o, len, ((uint64_t)v.y << 32) | v.x);
-      if (t != kL128Lanes - 1) llStoreBytes(recv + off, o + 8, len, ((uint64_t)v.w << 32) | v.z);
+    for (uint64_t i = g0; i < lines && !failed; i += groups) {
+      u32x4 v[kL128MaxRanks];
+#pragma unroll
+      for (int q = 0; q < kL128MaxRanks; q++) v[q] = (u32x4){0, 0, 0, 0};
+      failed = !l128Poll(a, rs, v, 1u, call.flag, kDiagLL128AG, t0, t,
+                         [&](int) { return (uint32_t)((subSlot(1, j) + i) * kL128LineBytes); });
+      const uint32_t pz = l128Partner(v[0].z);
+      llStoreBytes(recv + off, l128WordOff(i, t), len, ((uint64_t)v[0].y << 32) | v[0].x);
+      if (!(t & 1)) llStoreBytes(recv + off, l128PairOff(i, t) + 8, len, ((uint64_t)pz << 32) | v[0].z);
     }
   }
   __syncthreads();

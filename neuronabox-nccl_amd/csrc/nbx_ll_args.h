@@ -7,8 +7,8 @@ namespace nbx {
 
 enum LLMode : int32_t { kLLAllReduce = 0, kLLReduceScatter = 1, kLLReduce = 2 };
 constexpr int kL128MaxRanksHost = 8;   // LL128 kernel keeps one line per rank in registers
-constexpr int kL128LineBytesHost = 64;  // LL128 line: 56 payload bytes + 8-byte flag (nbx_ll.h)
-constexpr int kL128DataBytesHost = 56;
+constexpr int kL128LineBytesHost = 64;  // LL128 line: 4 x {12 payload bytes + 4-byte flag} (nbx_ll.h)
+constexpr int kL128DataBytesHost = 48;
 constexpr int kL128LanesHost = 4;       // lanes (16 bytes each) per LL128 line
 
 // Device-resident sequencing of the LL-family calls of one communicator
@@ -52,14 +52,52 @@ struct LLArgs {
   int32_t root;            // kLLReduce
 };
 
+constexpr int kRingMaxGrid = 256;   // slices per chunk = workgroups; one progress word each
+
 // Pipelined ring AllReduce (nbx_ring.h kRingAllReduce): device-resident
-// sequencing, as LLState.
+// sequencing, as LLState. The step-FIFO kernels (kRingFifo) keep, per
+// workgroup, how many FIFO entries this rank has produced and consumed over
+// all calls — every rank counts the same calls, so producer and consumer
+// agree without the host passing values (graph replays included).
 struct RingState {
   uint64_t seq;      // completed ring calls
   uint64_t arrive;   // workgroups of the running launch that have finished
+  uint64_t produced[kRingMaxGrid];   // kRingFifo: entries written into this rank's FIFO, per workgroup
+  uint64_t consumed[kRingMaxGrid];   // kRingFifo: entries of the left neighbour's FIFO read, per workgroup
 };
 
-constexpr int kRingMaxGrid = 256;   // slices per chunk = workgroups; one progress word each
+// Step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h kRingFifo): NCCL's
+// Simple-protocol FIFO (prims_simple.h:129-185: the receiver waits on the
+// sender's tail, the sender on the receiver's head credit) with the FIFO in
+// the producer's HBM, read in place by the right neighbour over xGMI.
+enum RingFifoMode : int32_t { kRingFifoReduceScatter = 0, kRingFifoReduce = 1 };
+constexpr int kRingFifoSlots = 4;          // entries in flight per workgroup (NCCL_STEPS analogue)
+constexpr int kRingFifoEntryPacks = 2048;  // 16-B packs per entry: 32 KiB per workgroup per step
+constexpr uint64_t kRingFifoBytes = (uint64_t)kRingMaxGrid * kRingFifoSlots * kRingFifoEntryPacks * 16;
+
+struct RingFifoArgs {
+  const void* sendMe;     // this rank's input
+  const void* sendLeft;   // the left neighbour's input (peer mapping): the chain's first hop reads it raw
+  void* recv;             // RS: this rank's block; Reduce: the root's output (root only)
+  void* fifoMe;           // this rank's FIFO [kRingMaxGrid][kRingFifoSlots][kRingFifoEntryPacks] packs
+  const void* fifoLeft;   // the left neighbour's FIFO (peer mapping)
+  uint64_t* myTail;       // [kRingMaxGrid] entries the left neighbour has produced (it posts here; uncached)
+  uint64_t* rightTail;    // the right neighbour's tail words (peer mapping): this rank posts there
+  uint64_t* myHead;       // [kRingMaxGrid] entries of this rank's FIFO the right neighbour has consumed
+  uint64_t* leftHead;     // the left neighbour's head words (peer mapping): this rank posts there
+  RingState* state;
+  uint64_t blockElts;     // RS: recvcount (a whole number of 16-B packs); Reduce: count
+  uint64_t slicePacks;    // 16-B packs per workgroup slice of a block (Reduce: of the message)
+  uint64_t arg;
+  const void* argPtr;
+  const volatile int* abortWord;
+  volatile int* errWord;
+  uint64_t timeoutTicks;
+  int32_t rank;
+  int32_t nRanks;
+  int32_t root;           // Reduce
+  int32_t mode;           // RingFifoMode
+};
 
 struct RingArgs {
   const void* sendMe;     // this rank's input

@@ -285,6 +285,19 @@ ncclResult_t launchRingAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, R
   return ncclSuccess;
 }
 
+ncclResult_t launchRingFifo(ncclDataType_t dt, const nbxDevRedOpFull& op, RingFifoArgs& a, unsigned grid,
+                            hipStream_t stream) {
+  if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
+  const KernelSet& ks = table()[(int)dt][op.op];
+  if (!ks.valid || ks.ringFifo == nullptr || grid < 1 || grid > (unsigned)kRingMaxGrid) return ncclInvalidArgument;
+  a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+  a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+  void* args[] = {&a};
+  hipError_t e = hipLaunchKernel(ks.ringFifo, dim3(grid), dim3(kBlock), args, 0, stream);
+  if (e != hipSuccess) return ncclUnhandledCudaError;
+  return ncclSuccess;
+}
+
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, uint64_t blockLines,
                                    hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;

@@ -700,6 +700,13 @@ struct MpState {
   uint64_t* rightRingProg = nullptr;// the right neighbour's words (peer mapping)
   nbx::RingState* ringState = nullptr;
   unsigned ringMaxGrid = nbx::kRingMaxGrid;   // NBX_RING_MAX_GRID
+  // step FIFO of the ring ReduceScatter / chain Reduce (NCCL_ALGO=Ring only)
+  void* fifo = nullptr;             // own FIFO (device memory, IPC-exported)
+  uint64_t* fifoTail = nullptr;     // [kRingMaxGrid] entries the left neighbour produced (uncached)
+  uint64_t* fifoHead = nullptr;     // [kRingMaxGrid] entries of `fifo` the right neighbour consumed (uncached)
+  void* leftFifo = nullptr;         // peer mappings
+  uint64_t* rightFifoTail = nullptr;
+  uint64_t* leftFifoHead = nullptr;
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
 };
 
@@ -710,6 +717,7 @@ struct MpInitInfo {
   hipIpcMemHandle_t llHandle;
   hipIpcMemHandle_t l128Handle;
   hipIpcMemHandle_t ringHandle;
+  hipIpcMemHandle_t fifoHandle, fifoTailHandle, fifoHeadHandle;   // NCCL_ALGO=Ring only
   uint64_t pciKey;   // (domain, bus, device) of this rank's GPU: identifies it across processes
   uint64_t llMaxBytes;
   uint64_t l128MaxBytes;
@@ -954,6 +962,13 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   HIPCHECK(hipMemset(mp->ringProg, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
   HIPCHECK(hipMalloc((void**)&mp->ringState, sizeof(nbx::RingState)));
   HIPCHECK(hipMemset(mp->ringState, 0, sizeof(nbx::RingState)));
+  if (mp->ring) {
+    HIPCHECK(hipMalloc(&mp->fifo, nbx::kRingFifoBytes));
+    HIPCHECK(allocSyncMem((void**)&mp->fifoTail, nbx::kRingMaxGrid * sizeof(uint64_t)));
+    HIPCHECK(hipMemset(mp->fifoTail, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
+    HIPCHECK(allocSyncMem((void**)&mp->fifoHead, nbx::kRingMaxGrid * sizeof(uint64_t)));
+    HIPCHECK(hipMemset(mp->fifoHead, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
+  }
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mp->hostWords, 0, 64);
   HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
@@ -1002,6 +1017,11 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
   if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
   HIPCHECK(hipIpcGetMemHandle(&mine.ringHandle, mp->ringProg));
+  if (mp->ring) {
+    HIPCHECK(hipIpcGetMemHandle(&mine.fifoHandle, mp->fifo));
+    HIPCHECK(hipIpcGetMemHandle(&mine.fifoTailHandle, mp->fifoTail));
+    HIPCHECK(hipIpcGetMemHandle(&mine.fifoHeadHandle, mp->fifoHead));
+  }
   {
     int dom = 0, bus = 0, dv = 0;
     (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device);
@@ -1063,6 +1083,17 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
       void* w = nullptr;
       HIPCHECK(hipIpcOpenMemHandle(&w, all[j].ringHandle, hipIpcMemLazyEnablePeerAccess));
       mp->rightRingProg = (uint64_t*)w;
+      if (mp->ring) {   // ... and its FIFO tail words
+        HIPCHECK(hipIpcOpenMemHandle(&w, all[j].fifoTailHandle, hipIpcMemLazyEnablePeerAccess));
+        mp->rightFifoTail = (uint64_t*)w;
+      }
+    }
+    if (mp->ring && j == (c->rank + c->nRanks - 1) % c->nRanks) {   // the left neighbour: its FIFO and head words
+      void* w = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].fifoHandle, hipIpcMemLazyEnablePeerAccess));
+      mp->leftFifo = w;
+      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].fifoHeadHandle, hipIpcMemLazyEnablePeerAccess));
+      mp->leftFifoHead = (uint64_t*)w;
     }
   }
   HIPCHECK(hipMalloc((void**)&mp->peerFlagsDev, c->nRanks * sizeof(uint64_t*)));
@@ -1094,6 +1125,12 @@ void mpFree(ncclComm* c) {
   for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerL128Maps) (void)hipIpcCloseMemHandle(p);
   if (mp->rightRingProg) (void)hipIpcCloseMemHandle(mp->rightRingProg);
+  if (mp->rightFifoTail) (void)hipIpcCloseMemHandle(mp->rightFifoTail);
+  if (mp->leftFifo) (void)hipIpcCloseMemHandle(mp->leftFifo);
+  if (mp->leftFifoHead) (void)hipIpcCloseMemHandle(mp->leftFifoHead);
+  if (mp->fifo) (void)hipFree(mp->fifo);
+  if (mp->fifoTail) (void)hipFree(mp->fifoTail);
+  if (mp->fifoHead) (void)hipFree(mp->fifoHead);
   if (mp->ringProg) (void)hipFree(mp->ringProg);
   if (mp->ringState) (void)hipFree(mp->ringState);
   if (mp->peerL128Dev) (void)hipFree(mp->peerL128Dev);
@@ -1290,6 +1327,22 @@ RankBlock mpDirectBlock(const MpCall& c, int n, int me, const std::vector<const 
   return b;
 }
 
+// NCCL_ALGO=Ring ReduceScatter / Reduce through the step FIFO (kRingFifo):
+// every rank's buffers 16-B aligned (decided from the exchanged offsets, so
+// every rank decides alike) and, for ReduceScatter, blocks of whole 16-B packs
+// (block c starts at c * recvcount elements). Otherwise the direct schedule.
+bool mpRingFifoEligible(const MpCall& c, int n, const std::vector<MpCallInfo>& all) {
+  if (c.kind != kReduceScatter && c.kind != kReduce) return false;
+  const int eb = typeSize(c.dt);
+  if (c.kind == kReduceScatter && ((uint64_t)c.count * (uint64_t)eb) % 16 != 0) return false;
+  for (int j = 0; j < n; j++) {
+    const MpCallInfo& ai = all[j];
+    if ((ai.sendOff & 15u) != 0) return false;
+    if (ai.hasRecv && (ai.recvOff & 15u) != 0) return false;
+  }
+  return true;
+}
+
 // Simple path, after the exchange: map, barriers, reduce (direct or ring), gather.
 ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCallInfo>& all) {
   MpState* mp = comm->mp;
@@ -1376,6 +1429,36 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
       if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, 1ull << left, stream));
     }
     }
+  } else if (mp->ring && mp->ringPipeline && n > 1 && mpRingFifoEligible(c, n, all)) {
+    // 2''. ring ReduceScatter / chain Reduce through the step FIFO (nbx_ring.h
+    // kRingFifo; reduce_scatter.h:13-66, reduce.h:12-68)
+    const int left = (me + n - 1) % n;
+    const uint64_t epp = (uint64_t)(16 / eb);
+    const uint64_t blockPacks = ((uint64_t)c.count + epp - 1) / epp;   // RS: recvcount, Reduce: count
+    uint64_t grid = (blockPacks + 1023) / 1024;   // slices of >= 16 KiB
+    if (grid < 1) grid = 1;
+    if (grid > mp->ringMaxGrid) grid = mp->ringMaxGrid;
+    nbx::RingFifoArgs fa{};
+    fa.sendMe = sendP[me];
+    fa.sendLeft = sendP[left];
+    fa.recv = recvP[me];
+    fa.fifoMe = mp->fifo;
+    fa.fifoLeft = mp->leftFifo;
+    fa.myTail = mp->fifoTail;
+    fa.rightTail = mp->rightFifoTail;
+    fa.myHead = mp->fifoHead;
+    fa.leftHead = mp->leftFifoHead;
+    fa.state = mp->ringState;
+    fa.blockElts = c.count;
+    fa.slicePacks = (blockPacks + grid - 1) / grid;
+    fa.abortWord = mp->hostWordsDev;
+    fa.errWord = mp->hostWordsDev + 1;
+    fa.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
+    fa.rank = me;
+    fa.nRanks = n;
+    fa.root = c.root;
+    fa.mode = c.kind == kReduceScatter ? nbx::kRingFifoReduceScatter : nbx::kRingFifoReduce;
+    NCCLCHECK(nbx::launchRingFifo(c.dt, c.op, fa, (unsigned)grid, stream));
   } else {
     // 2. direct reduce of this rank's block
     const RankBlock b = mpDirectBlock(c, n, me, sendP, recvP);
@@ -1587,7 +1670,8 @@ ncclResult_t runMpGroupImpl(ncclComm* comm) {
   auto directSimple = [&](size_t k) {
     const MpCall& c = calls[k];
     return protos[k] == kMpSimple && c.count > 0 && !(c.kind == kAllReduce && n > NBX_MAX_DSTS) &&
-           !(c.kind == kAllReduce && n > 2 && mp->ring);
+           !(c.kind == kAllReduce && n > 2 && mp->ring) &&
+           !(mp->ring && mp->ringPipeline && mpRingFifoEligible(c, n, alls[k]));   // ring RS / Reduce: alone
   };
   auto contigEverywhere = [&](size_t k) {
     for (const MpCallInfo& a : alls[k])

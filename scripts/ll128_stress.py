@@ -4,7 +4,7 @@ test of the suite): N processes (all on GPU 0, or one per GPU with
 --per-gpu) run ITERS back-to-back LL128 collectives with inputs that change
 every call (small integers, so any fold order gives the exact result) and
 check every output. Mismatching elements are binned by the 8-byte word of the
-payload line they travel in (--line-payload: 56 for the current 64-byte line,
+payload line they travel in (--line-payload: 48 for the current 64-byte line,
 the default; the original 128-byte-line run binned by 120): a torn
 line — the flag visible before part of the payload — shows up as mismatches
 concentrated in one part of the line (with 128-byte lines: words 0..7, the
@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--kind", default="ar")
     ap.add_argument("--dtype", type=int, default=2)
     ap.add_argument("--per-gpu", action="store_true")
-    ap.add_argument("--line-payload", type=int, default=56)
+    ap.add_argument("--line-payload", type=int, default=48)
     args = ap.parse_args()
     os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
     os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "60")

@@ -203,6 +203,105 @@ def _check_cases(oracle, n, res):
                 assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, kind, dtype, op, r)
 
 
+# NCCL_ALGO=Ring ReduceScatter / Reduce through the step FIFO (nbx_ring.h
+# kRingFifo): (kind, dtype, op, count, root). RS counts whose blocks are whole
+# 16-B packs take the FIFO kernel; the bf16 RS of 777 does not (direct
+# fallback, still checked). Reduce counts with a partial last pack exercise the
+# element tail.
+RING_FIFO_CASES = [
+    ("rs", 7, 0, 4096, 0), ("rs", 6, 4, 1 << 20, 0), ("rs", 2, 2, 300000, 0), ("rs", 9, 0, 777, 0),
+    ("rs", 8, 1, 65536, 0), ("red", 7, 0, 1000003, 0), ("red", 7, 0, 250000, -1), ("red", 8, 1, 200001, 1),
+    ("red", 0, 0, 123457, 1), ("red", 6, 4, 99999, -1),
+]
+
+
+def _ring_fifo_input(kind, dtype, count, n, r):
+    from oracle import oracle
+    total = count * n if kind == "rs" else count
+    return oracle.random_inputs(dtype, 8, total, seed=500 + dtype + count % 1000)[r]
+
+
+def _child_ring_fifo(uid_bytes, rank, n, q):
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        for it in range(2):   # twice: cumulative FIFO counts carry across calls
+            for i, (kind, dtype, op, count, root) in enumerate(RING_FIFO_CASES):
+                root = root % n
+                x = _ring_fifo_input(kind, dtype, count, n, rank)
+                tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+                nb = (count * x.itemsize) if kind == "rs" else x.nbytes
+                ty = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+                if kind == "rs":
+                    comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
+                else:
+                    comm.reduce(tx.data_ptr(), ty.data_ptr() if rank == root else 0, count, dtype, op, root, st)
+                torch.cuda.synchronize()
+                out[(it, i)] = ty.cpu().numpy().copy()
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def ring_chain(oracle, parts, dtype, devop, arg, n):
+    """NCCL's ring / chain accumulation, operand for operand: the first hop
+    folds Fn(pre(x1), pre(x0)) (local input, the left neighbour's raw input),
+    every later hop Fn(pre(local), received), postOp on the last
+    (reduce_scatter.h:49-64, reduce.h:44-67, prims_simple.h genericOp)."""
+    if n == 1:
+        return oracle.reduce_multi([parts[0]], dtype, devop, arg, n_pre_op_srcs=1, post_op=devop == 4)[0]
+    acc = None
+    for k in range(1, n):
+        last = k == n - 1
+        if k == 1:
+            acc = oracle.reduce_multi([parts[1], parts[0]], dtype, devop, arg, n_pre_op_srcs=2,
+                                      post_op=last and devop == 4)[0]
+        else:
+            acc = oracle.reduce_multi([parts[k], acc], dtype, devop, arg, n_pre_op_srcs=1,
+                                      post_op=last and devop == 4)[0]
+    return acc
+
+
+@pytest.mark.parametrize("n,grid", [(2, ""), (3, ""), (3, "2"), (8, ""), (8, "3")])
+def test_multiprocess_ring_fifo_reduce_scatter_and_reduce(nbx, oracle, n, grid, monkeypatch):
+    """NCCL_ALGO=Ring: ReduceScatter block b folded along the ring b+1, ..., b
+    and Reduce along the chain root+1, ..., root, through the step FIFO —
+    bitwise NCCL's operand order (ring_chain). NBX_RING_MAX_GRID=2/3 makes each
+    workgroup's slice span many FIFO entries, so the 4-slot FIFO wraps and the
+    head credits gate the producer."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NCCL_ALGO", "Ring")
+    monkeypatch.setenv("NCCL_PROTO", "Simple")
+    monkeypatch.setenv("NBX_RING_MAX_GRID", grid or "32")
+    res = _run_ranks(nbx, n, _child_ring_fifo)
+    for i, (kind, dtype, op, count, root) in enumerate(RING_FIFO_CASES):
+        root = root % n
+        xs = [_ring_fifo_input(kind, dtype, count, n, r) for r in range(n)]
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        exp = {}
+        if kind == "rs":
+            for b in range(n):
+                order = [(b + 1 + k) % n for k in range(n)]
+                exp[b] = ring_chain(oracle, [xs[j][b * count:(b + 1) * count] for j in order], dtype, devop, arg, n)
+        else:
+            order = [(root + 1 + k) % n for k in range(n)]
+            exp[root] = ring_chain(oracle, [xs[j] for j in order], dtype, devop, arg, n)
+        for it in range(2):
+            for r, e in exp.items():
+                got = res[r][(it, i)]
+                assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (it, kind, dtype, op, count, r)
+
+
 # config D at full size (8 ranks x 1 GiB, direct and ring) and config E:
 # tests/test_configs_gpu.py
 
@@ -221,7 +320,7 @@ LL_CASES = [
     ("ar", 0, 0, 77, 3), ("rs", 7, 0, 1000, 0), ("rs", 6, 4, 333, 2), ("rs", 0, 2, 5, 1), ("rs", 4, 4, 4096, 0),
     ("rs", 7, 0, 20000, 0), ("red", 7, 0, 1000, 0), ("red", 9, 4, 777, 0), ("red", 2, 3, 64, 0),
     ("red", 7, 0, 123, 4), ("red", 7, 1, 4096, 0), ("ar", 7, 0, 64, 0),
-    # LL128 one-shot range: odd lengths so 56-byte lines straddle 16-byte blocks
+    # LL128 one-shot range: odd lengths so 48-byte lines straddle 16-byte blocks
     ("ar", 7, 0, 50003, 0), ("ar", 6, 4, 77777, 2), ("ar", 4, 2, 30000, 8), ("rs", 7, 0, 30001, 4),
     ("rs", 2, 2, 131072, 0), ("red", 7, 0, 99999, 0), ("red", 8, 4, 100000, 8),
     # LL128 two-shot AllReduce / Reduce (> 256 KiB with > 2 ranks; one-shot with 2 ranks)
@@ -541,6 +640,24 @@ def _child_selftest(uid_bytes, rank, n, q):
     except Exception:
         import traceback
         q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("tear,delay_us", [(0, 0), (1, 200), (1, 5000)])
+def test_ll128_torn_line_is_waited_on(nbx, torch_gpu, tear, delay_us):
+    """A deliberately torn LL128 line (nbxDebugLL128TearTest: the writer stores
+    the line's last 32 bytes — the flag half of the r1 one-flag layout — waits,
+    then the first 32 bytes) against the collectives' own line reader: with a
+    flag in every 16-byte chunk the reader waits for the second half and folds
+    exactly the new payload, never the stale chunks."""
+    import ctypes
+    lib = nbx.load_library()
+    lib.nbxDebugLL128TearTest.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_longlong)]
+    lib.nbxDebugLL128TearTest.restype = ctypes.c_int
+    after = ctypes.c_longlong(0)
+    rc = lib.nbxDebugLL128TearTest(delay_us, tear, ctypes.byref(after))
+    assert rc == 0, {1: "stale chunks folded", 2: "accepted before the second half", 3: "reader timed out"}.get(rc, rc)
+    if tear:
+        assert after.value >= 0   # accepted after the second half was issued (100 MHz ticks)
 
 
 @pytest.mark.parametrize("n,fail", [(3, False), (3, True), (8, False)])
