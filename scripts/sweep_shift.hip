@@ -247,6 +247,84 @@ __global__ __launch_bounds__(256) void kshift63(Args a) {
   }
 }
 
+// reference point: the same fold with every source aligned to the
+// destination (pack q of each source, no shift) — the aligned kernel's rate
+// at this size, same process, same buffers
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kaligned(Args a) {
+  const uint64_t n = a.nPacks, tile = (uint64_t)U * 256, stride = (uint64_t)gridDim.x * tile;
+  for (uint64_t p0 = blockIdx.x * tile + threadIdx.x; p0 < n; p0 += stride) {
+    u32x4 v[NSRC][U];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t q = p0 + (uint64_t)u * 256;
+        v[s][u] = __builtin_nontemporal_load(a.base[s] + (q < n ? q : n - 1));
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = p0 + (uint64_t)u * 256;
+      u32x4 acc = v[0][u];
+#pragma unroll
+      for (int s = 1; s < NSRC; s++) acc = add4(acc, v[s][u]);
+      if (q < n) a.dst[q] = acc;
+    }
+  }
+}
+
+// LDS-staged: a workgroup's tile of U*256 output packs needs source packs
+// [p0, p0 + U*256] of every source; they are loaded aligned (nontemporal, the
+// workgroup's extra last pack by thread 0) and written to LDS, and each lane
+// reads its 16 output bytes back at byte offset 16 (q - p0) + sh as five
+// dwords + one byte funnel shift. Every pack is loaded once and no lane
+// exchange is needed; the cost is LDS traffic and two barriers per tile.
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kshiftLds(Args a) {
+  constexpr int T = U * 256;
+  __shared__ u32x4 sm[NSRC][T + 1];
+  const uint64_t n = a.nPacks, stride = (uint64_t)gridDim.x * T;
+  const int tid = (int)threadIdx.x;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * T; b0 < n; b0 += stride) {
+    u32x4 v[NSRC][U], ex[NSRC];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t q = b0 + (uint64_t)u * 256 + tid;
+        v[s][u] = __builtin_nontemporal_load(a.base[s] + (q < n ? q : n - 1));
+      }
+      if (tid == 0) ex[s] = a.base[s][b0 + T < n ? b0 + T : n];   // pack n holds the range's last bytes
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();   // the previous tile's LDS reads are done
+#pragma unroll
+    for (int s = 0; s < NSRC; s++) {
+#pragma unroll
+      for (int u = 0; u < U; u++) sm[s][u * 256 + tid] = v[s][u];
+      if (tid == 0) sm[s][T] = ex[s];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = b0 + (uint64_t)u * 256 + tid;
+      u32x4 acc;
+#pragma unroll
+      for (int s = 0; s < NSRC; s++) {
+        const uint32_t o = (uint32_t)(u * 256 + tid) * 16u + a.sh[s];
+        const uint32_t* w = (const uint32_t*)&sm[s][0] + (o >> 2);
+        const uint32_t b = o & 3u;
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = b ? w[4] : 0u;
+        const u32x4 x = {__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
+                         __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(w4, w3, b)};
+        acc = s == 0 ? x : add4(acc, x);
+      }
+      if (q < n) a.dst[q] = acc;
+    }
+  }
+}
+
 struct Variant {
   std::string name;
   const void* fn;
@@ -288,7 +366,17 @@ int run(int cus, int rounds, int iters, int mib) {
       {"dpp-pre u2 bpc4", (const void*)&kshiftPre<NSRC, 2>, 2, 4},
       {"dpp-pre u1 bpc8", (const void*)&kshiftPre<NSRC, 1>, 1, 8},
       {"63-lane u4 bpc2", (const void*)&kshift63<NSRC, 4>, -4, 2},
+      {"dpp-pre u4 bpc1", (const void*)&kshiftPre<NSRC, 4>, 4, 1},
+      {"dpp-pre u1 bpc4", (const void*)&kshiftPre<NSRC, 1>, 1, 4},
+      {"lds u1 bpc4", (const void*)&kshiftLds<NSRC, 1>, 1, 4},
+      {"lds u2 bpc2", (const void*)&kshiftLds<NSRC, 2>, 2, 2},
+      {"lds u2 bpc3", (const void*)&kshiftLds<NSRC, 2>, 2, 3},
+      {"lds u4 bpc1", (const void*)&kshiftLds<NSRC, 4>, 4, 1},
   };
+  // the aligned fold (reference rate, not a realigning kernel): its output
+  // differs, so it is timed but not compared
+  const Variant aligned = NSRC >= 4 ? Variant{"ALIGNED u4 bpc1 (reference)", (const void*)&kaligned<NSRC, 4>, 4, 1}
+                                    : Variant{"ALIGNED u1 bpc4 (reference)", (const void*)&kaligned<NSRC, 1>, 1, 4};
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -332,6 +420,7 @@ int run(int cus, int rounds, int iters, int mib) {
       bad++;
     }
   }
+  vs.push_back(aligned);
   std::vector<std::vector<float>> t(vs.size());
   for (int rd = 0; rd < rounds; rd++)
     for (size_t i = 0; i < vs.size(); i++) {
