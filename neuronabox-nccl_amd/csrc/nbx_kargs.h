@@ -8,8 +8,13 @@ namespace nbx {
 
 constexpr int kBlock = 256;      // workgroup = 4 wave64
 constexpr int kMaxKSrcs = 8;     // sources per kernel pass
-constexpr int kShiftUDpp = 2;    // packs per lane in the per-source-count realigning kernels (kReduceShiftedN)
-constexpr int kShiftDppMinSrcs = 4;  // fewest sources for the DPP realigning shape
+// realigning kernel (kReduceShiftedLds): waves per workgroup, packs per lane
+// per tile (2 from 3 sources, else 1) and workgroups per CU (1 from 3 sources,
+// else 2) — profiles/r2/sweep_shift_256MiB_r2f.txt
+constexpr int kShiftLdsWaves = 4;
+constexpr int kShiftLdsStages = 2;
+constexpr int shiftLdsUnroll(int nSrcs) { return nSrcs >= 3 ? 2 : 1; }
+constexpr int shiftLdsBlocksPerCU(int nSrcs) { return nSrcs >= 3 ? 1 : 2; }
 constexpr int kMaxKDsts = 8;     // destinations: NCCL_MAX_DIRECT_ARITY + 1 (device.h:147, all_reduce.h:343-360)
 
 struct KArgs {
@@ -61,7 +66,7 @@ struct KernelSet {
   const void* packs[2][kMaxKSrcs];  // [0 = small tile, 1 = big tile][nSrcs-1]
   const void* elts;
   const void* shifted;              // sources realigned against 16-B aligned destinations (kReduceShifted, run-time source count; fallback)
-  const void* shiftedN[kMaxKSrcs];   // the same per source count, [nSrcs-1] (kReduceShiftedN: DPP shape from 4)
+  const void* shiftedN[kMaxKSrcs];   // the same per source count, [nSrcs-1] (kReduceShiftedLds: LDS-DMA staging)
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)

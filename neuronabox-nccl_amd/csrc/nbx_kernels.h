@@ -179,25 +179,19 @@ __global__ __launch_bounds__(kBlock) void kReduceElts(KArgs a) {
 // Sources misaligned against the destinations (common_kernel.h:229-238 falls
 // back to sizeof(T) packs there). Here the destinations (which share one
 // alignment) stay 16-B packs, and each source is read as 16-B aligned packs
-// and realigned in registers: output pack q needs packs q and q+1 of the
-// source's aligned-down base, funnel-shifted by the source's byte offset
+// and realigned: output pack q needs packs q and q+1 of the source's
+// aligned-down base, funnel-shifted by the source's byte offset
 // (v_alignbyte_b32; the offset is per source, so the shift case is uniform).
-// Lanes of a wave own consecutive packs, so pack q+1 is the next lane's q.
-// Two shapes (scripts/sweep_shift.hip, profiles/r1/sweep_shift.txt):
-//  * two loads (1-3 sources): each lane loads q and q+1 itself with plain
-//    (temporal) loads; the second mostly hits L2 (it is the next lane's
-//    first). kReduceShifted is this shape with a run-time source count
-//    (1 pack per lane, 8 workgroups per CU; the fallback);
-//  * DPP (4-8 sources): each lane loads q only (nontemporal) and takes
-//    q+1 from the next lane by a DPP wave shift (wave_shl:1, VALU, no LDS);
-//    lane 63 and the lane holding the last pack load q+1 themselves, issued
-//    with the main loads so the shift waits on no second round trip.
-// kReduceShiftedN<Fn, NSRC, kDpp> is one kernel per source count, 2 packs per
-// lane (4 workgroups per CU for two loads, 2 for DPP). HBM traffic stays the
-// algorithmic bytes either way. Memory safety: a 16-B
-// aligned pack never crosses a page, and every pack loaded holds at least one
-// byte of the source range (pack indices are clamped to the last one), so no
-// load can touch an unmapped page.
+// Two kernels:
+//  * kReduceShiftedLds<Fn, NSRC> (the default, below the fallback): the
+//    sources staged through LDS by LDS-DMA, one kernel per source count;
+//  * kReduceShifted<Fn>: the run-time source count fallback — each lane loads
+//    q and q+1 itself with plain (temporal) loads, the second mostly an L2
+//    hit (it is the next lane's first); 1 pack per lane, 8 workgroups per CU
+//    (launch variant 1 or NBX_SHIFT_N=0).
+// Memory safety: a 16-B aligned pack never crosses a page, and every pack
+// loaded holds at least one byte of the source range (pack indices are
+// clamped to the last one), so no load can touch an unmapped page.
 __device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint32_t m) {
   const uint32_t b = m & 3u;   // byte shift inside a dword (0: plain dword select)
   const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -221,14 +215,6 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4& lo, const u32x4& hi, uint
       break;
   }
   return r;
-}
-
-// lane i receives lane i+1's value (DPP wave_shl:1); lane 63 gets 0
-__device__ __forceinline__ u32x4 fromNextLane(const u32x4& v) {
-  return u32x4{(uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x130, 0xf, 0xf, false),
-               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, 0x130, 0xf, 0xf, false),
-               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, 0x130, 0xf, 0xf, false),
-               (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, 0x130, 0xf, 0xf, false)};
 }
 
 template <class Fn>
@@ -291,111 +277,122 @@ __global__ __launch_bounds__(kBlock) void kReduceShifted(KArgs a) {
   }
 }
 
-// Per-source-count realigning kernel, 2 packs per lane: kDpp = true is the
-// DPP next-lane shape (4-8 sources), kDpp = false the two-load shape (1-3
-// sources; +4 % over kReduceShifted at 2 sources in scripts/sweep_shift.hip).
-template <class Fn, int NSRC, bool kDpp>
-__global__ __launch_bounds__(kBlock) void kReduceShiftedN(KArgs a) {
+// Per-source-count realigning kernel: the sources go through LDS by LDS-DMA.
+// A wave's tile is U x 64 output packs (destination side, 16-B aligned); it
+// needs packs [p0, p0 + U*64] of each source's aligned-down base: U full
+// global_load_lds_dwordx4 (nt; 64 lanes x 16 B straight into LDS, no VGPRs)
+// plus one single-lane DMA for the extra pack, per source, into a stage
+// buffer private to the wave. With kShiftLdsStages stages the wave issues
+// tile j+1's DMA, waits (vmcnt) until tile j has landed, reads each output's
+// 16 bytes back at byte offset 16 (q - p0) + sh (five dwords + a byte funnel
+// shift), folds in source order and stores. No lane exchange, no second load
+// of a pack, and several tiles in flight per wave at no register cost.
+// Measured at 256 MiB per input (scripts/sweep_shift.hip,
+// profiles/r2/sweep_shift_256MiB_r2f.txt): 95 % (8 sources) / 97 % (4) /
+// 97 % (2) of the aligned kernel on the same buffers, against 81 / 86 / 88 %
+// for the DPP / two-load register shapes it replaces. Memory safety: pack
+// indices clamp to the last pack holding a byte of the source range (pack n
+// when the source is shifted, n - 1 when it is not), so no load leaves it.
+template <class Fn, int NSRC>
+__global__ __launch_bounds__(kShiftLdsWaves * 64) void kReduceShiftedLds(KArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
-  // 64-bit SumPostDiv (integer Avg) keeps 1 pack per lane: its division code
-  // on top of the 2-pack arrays spilled (tests/test_code_object.py); the tile
-  // is the kernel's own, so the host's grid only sets the workgroup count
-  constexpr int U = (Fn::kHasPost && sizeof(E) == 8) ? 1 : kShiftUDpp;
+  constexpr int U = shiftLdsUnroll(NSRC), S = kShiftLdsStages, W = kShiftLdsWaves;
+  constexpr int P = U * 64 + 1;   // packs per source per stage
+  constexpr uint64_t kTile = (uint64_t)U * 64;
+  __shared__ u32x4 sm[W][S][NSRC][P];
   acquirePeerData(a);
   const Fn fn(loadArg<Fn>(a));
   const uint64_t headBytes = (uint64_t)a.headElts * sizeof(E);
-  constexpr int nSrcs = NSRC;   // a compile-time count sizes the arrays (occupancy)
-  const int nDsts = a.nDsts;
+  const uint64_t n = a.nPacks;
   const u32x4* base[NSRC];
   uint32_t sh[NSRC];
+  uint64_t lim[NSRC];
 #pragma unroll
   for (int s = 0; s < NSRC; s++) {
     const uintptr_t q = (uintptr_t)a.src[s] + headBytes;
     sh[s] = (uint32_t)(q & 15u);
     base[s] = (const u32x4*)(q - sh[s]);
+    lim[s] = sh[s] ? n : n - 1;
   }
   u32x4* dst[kMaxKDsts];
 #pragma unroll
   for (int d = 0; d < kMaxKDsts; d++) dst[d] = (u32x4*)((char*)a.dst[d] + headBytes);
+  const int nDsts = a.nDsts;
   const bool doPost = Fn::kHasPost && a.postOp;
   const uint32_t preMask = a.preMask;
-  const uint64_t n = a.nPacks;
-  const uint32_t lane = threadIdx.x & 63u;
-  constexpr uint64_t tile = (uint64_t)U * kBlock;
-  const uint64_t stride = (uint64_t)gridDim.x * tile;
-  // the whole workgroup iterates while its tile starts inside the range, so
-  // every lane of a wave is active at the shift (indices past n are clamped
-  // for the loads and masked for the stores)
-  for (uint64_t p0 = (uint64_t)blockIdx.x * tile + threadIdx.x; p0 - threadIdx.x < n; p0 += stride) {
-    u32x4 lo[NSRC][U], hi[NSRC][U];
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+  const uint64_t nTiles = (n + kTile - 1) / kTile;
+  const uint64_t nWaves = (uint64_t)gridDim.x * W, gw = (uint64_t)blockIdx.x * W + (uint64_t)wave;
+  auto issue = [&](uint64_t t, int st) {
+    const uint64_t p0 = t * kTile;
 #pragma unroll
     for (int s = 0; s < NSRC; s++) {
-      {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          uint64_t q = p0 + (uint64_t)u * kBlock;
-          if (q >= n) q = n - 1;
-          if constexpr (kDpp) {
-            lo[s][u] = ldPack(base[s] + q);
-            if (sh[s] && (lane == 63u || q + 1 >= n)) hi[s][u] = base[s][q + 1];
-          } else {   // plain (temporal) loads: the second one must find the line in L2
-            lo[s][u] = base[s][q];
-            hi[s][u] = sh[s] ? base[s][q + 1] : lo[s][u];
-          }
-        }
+      for (int u = 0; u < U; u++) {
+        const uint64_t q = p0 + (uint64_t)(u * 64 + lane);
+        __builtin_amdgcn_global_load_lds((const void*)(base[s] + (q < lim[s] ? q : lim[s])),
+                                         (__attribute__((address_space(3))) void*)&sm[wave][st][s][u * 64], 16, 0,
+                                         2 /* nt */);
+      }
+      if (lane == 0) {
+        const uint64_t q = p0 + kTile;
+        __builtin_amdgcn_global_load_lds((const void*)(base[s] + (q < lim[s] ? q : lim[s])),
+                                         (__attribute__((address_space(3))) void*)&sm[wave][st][s][kTile], 16, 0, 2);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
+  };
+#pragma unroll
+  for (int k = 0; k < S - 1; k++) {
+    const uint64_t t = gw + (uint64_t)k * nWaves;
+    if (t < nTiles) issue(t, k);
+  }
+  int st = 0;
+  for (uint64_t t = gw; t < nTiles; t += nWaves) {
+    if (t + (uint64_t)(S - 1) * nWaves < nTiles) {
+      issue(t + (uint64_t)(S - 1) * nWaves, (st + S - 1) % S);
+      // everything but the newer tiles' DMA (NSRC x (U + 1) instructions each)
+      // has landed; stores counted in vmcnt only make the wait stricter
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * NSRC * (U + 1)) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t q = p0 + (uint64_t)u * kBlock;
-      const bool own = lane == 63u || (q >= n ? n - 1 : q) + 1 >= n;
-      // the shift runs on every lane (a lane reading a disabled lane would get 0),
-      // then lanes that loaded pack q+1 themselves keep their own
-      u32x4 acc = lo[0][u];
-      if (sh[0]) {
-        u32x4 h = hi[0][u];
-        if constexpr (kDpp) {
-          const u32x4 x = fromNextLane(lo[0][u]);
-          if (!own) h = x;
-        }
-        acc = funnel16(lo[0][u], h, sh[0]);
-      }
-      if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.prePack(acc);
-#pragma unroll
-      for (int s = 1; s < NSRC; s++) {
-        {
-          u32x4 t = lo[s][u];
-          if (sh[s]) {
-            u32x4 h = hi[s][u];
-            if constexpr (kDpp) {
-              const u32x4 x = fromNextLane(lo[s][u]);
-              if (!own) h = x;
-            }
-            t = funnel16(lo[s][u], h, sh[s]);
-          }
-          if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) t = fn.prePack(t);
-          acc = fn.redPack(acc, t);
-        }
-      }
-      if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
+      const uint64_t q = t * kTile + (uint64_t)(u * 64 + lane);
       if (q < n) {
+        u32x4 acc;
+#pragma unroll
+        for (int s = 0; s < NSRC; s++) {
+          const uint32_t o = (uint32_t)(u * 64 + lane) * 16u + sh[s];
+          const uint32_t* w = (const uint32_t*)&sm[wave][st][s][0] + (o >> 2);
+          const uint32_t b = o & 3u;
+          const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = b ? w[4] : 0u;
+          u32x4 x = {__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
+                     __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(w4, w3, b)};
+          if constexpr (Fn::kHasPre) if ((preMask >> s) & 1u) x = fn.prePack(x);
+          if (s == 0) acc = x;
+          else acc = fn.redPack(acc, x);
+        }
+        if constexpr (Fn::kHasPost) if (doPost) acc = fn.postPack(acc);
         stPack(dst[0] + q, acc);
 #pragma unroll
         for (int d = 1; d < kMaxKDsts; d++)
           if (d < nDsts) stPack(dst[d] + q, acc);
       }
     }
+    // this stage's LDS reads have returned before a later iteration refills it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    st = st + 1 == S ? 0 : st + 1;
   }
-  // head (before the destinations' 16-B boundary) and tail elements
+  // head (before the destination's 128-B boundary) and tail elements
   if (blockIdx.x == gridDim.x - 1) {
     const int head = a.headElts;
     const uint64_t tailStart = (uint64_t)head + n * EPP;
     const int tail = (int)(a.nElts - tailStart);
-    const int t = (int)threadIdx.x;
-    if (t < head) reduceElt(fn, a, nSrcs, (uint64_t)t);
-    else if (t < head + tail) reduceElt(fn, a, nSrcs, tailStart + (uint64_t)(t - head));
+    const int th = (int)threadIdx.x;
+    if (th < head) reduceElt(fn, a, NSRC, (uint64_t)th);
+    else if (th < head + tail) reduceElt(fn, a, NSRC, tailStart + (uint64_t)(th - head));
   }
 }
 
@@ -506,10 +503,10 @@ constexpr int bigUnroll() {
   return u < CAP ? u : CAP;
 }
 
-// per-source-count realigning kernels: DPP shape from kShiftDppMinSrcs sources
+// per-source-count realigning kernels (LDS-DMA staging)
 template <class Fn, int NSRC>
 inline const void* shiftedNFor() {
-  return (const void*)&kReduceShiftedN<Fn, NSRC, (NSRC >= kShiftDppMinSrcs)>;
+  return (const void*)&kReduceShiftedLds<Fn, NSRC>;
 }
 
 template <class Fn, int... I>

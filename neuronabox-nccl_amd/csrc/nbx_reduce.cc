@@ -96,16 +96,16 @@ int maxBlocksPerCU(bool big, int loadsPerLane, bool classic = false) {
   return b < 1 ? 1 : (b > 8 ? 8 : b);
 }
 
-// Realigning kernels (profiles/r1/sweep_shift.txt): 8 workgroups per CU for
-// the run-time-count kernel; per source count, 2 for the DPP shape and 4 for
-// the two-load shape.
+// Realigning kernels: 8 workgroups per CU for the run-time-count kernel
+// (profiles/r1/sweep_shift.txt); per source count, the LDS-DMA kernel's
+// shiftLdsBlocksPerCU (profiles/r2/sweep_shift_256MiB_r2f.txt).
 int shiftedBlocksPerCU(bool perCount, int nSrcs) {
   int v = g_maxBlocksPerCU.load(std::memory_order_relaxed);
   if (v > 0) return v;
   static const int env = envInt("NBX_BLOCKS_PER_CU", 0);
   if (env > 0) return env;
   if (!perCount) return 8;
-  return nSrcs >= kShiftDppMinSrcs ? 2 : 4;
+  return shiftLdsBlocksPerCU(nSrcs);
 }
 
 bool isFloatType(int dt) {
@@ -121,6 +121,22 @@ int typeSize(int dt) {
     case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
     default: return -1;
   }
+}
+
+// Elements folded one by one before the 16-B pack body, so that the body of
+// dsts[0] starts on a 128-B cache-line boundary (NBX_PEEL_BYTES: 16 keeps
+// the smallest peel). Streams that start mid-line cost every wave
+// instruction a partial line at each end: all pointers one element off ran
+// 9 % slower at 256 MiB per input than aligned ones with a 16-B peel, and a
+// destination body on a line boundary gains 2-5 % for the realigning kernels
+// (profiles/r2/realign_probe_r2d.jsonl, sweep_shift_256MiB_r2d.txt).
+size_t peelElts(uintptr_t dst, int eb) {
+  static const unsigned line = [] {
+    const int v = envInt("NBX_PEEL_BYTES", 128);
+    return (unsigned)(v == 16 || v == 32 || v == 64 || v == 128 || v == 256 ? v : 128);
+  }();
+  const unsigned mis = (unsigned)(dst & (line - 1));
+  return mis ? (size_t)((line - mis) / (unsigned)eb) : 0;
 }
 
 bool overlaps(const void* a, const void* b, size_t bytes) {
@@ -159,7 +175,7 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
   void* args[] = {&a};
   hipError_t err;
   if (shared) {
-    size_t head = mis ? (size_t)((16u - mis) / (unsigned)eb) : 0;
+    size_t head = peelElts((uintptr_t)dsts[0], eb);
     if (head > count) head = count;
     const size_t nPacks = (count - head) / (size_t)epp;
     a.headElts = (int)head;
@@ -188,26 +204,26 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     if (dstShared && ks.shifted != nullptr) {
       // destinations share one alignment: 16-B packs on their side, the
       // sources realigned in registers (kReduceShifted)
-      size_t head = dmis ? (size_t)((16u - dmis) / (unsigned)eb) : 0;
+      size_t head = peelElts((uintptr_t)dsts[0], eb);
       if (head > count) head = count;
       const size_t nPacks = (count - head) / (size_t)epp;
       a.headElts = (int)head;
       a.nPacks = nPacks;
-      // one kernel per source count, 2 packs per lane: 4+ sources take the
-      // next-lane pack by DPP, 1-3 load it (DESIGN §4,
-      // profiles/r1/mixed_alignment_dpp_r1w.jsonl). NBX_SHIFT_N=0 or launch
-      // variant 1 (small tiles) selects the run-time-count kernel (1 pack per
-      // lane, 8 workgroups/CU).
+      // one kernel per source count staging the sources through LDS by
+      // LDS-DMA (profiles/r2/sweep_shift_256MiB_r2f.txt);
+      // NBX_SHIFT_N=0 or launch variant 1 (small tiles) selects the
+      // run-time-count register kernel (1 pack per lane, 8 workgroups/CU)
       static const int useN = envInt("NBX_SHIFT_N", 1);
       const bool small = g_variant.load(std::memory_order_relaxed) == 1;
       const void* fn = (useN && !small) ? ks.shiftedN[nSrcs - 1] : nullptr;
-      const size_t tile = (size_t)(fn ? kShiftUDpp : 1) * kBlock;
+      const size_t tile = fn ? (size_t)shiftLdsUnroll(nSrcs) * 64 * kShiftLdsWaves : (size_t)kBlock;
       size_t blocks = (nPacks + tile - 1) / tile;
       if (blocks == 0) blocks = 1;
       const size_t maxBlocks = (size_t)cus * (size_t)shiftedBlocksPerCU(fn != nullptr, nSrcs);
       const size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
+      const unsigned threads = fn ? (unsigned)(kShiftLdsWaves * 64) : (unsigned)kBlock;
       if (!fn) fn = ks.shifted;
-      err = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
+      err = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(threads), args, 0, stream);
     } else {
       size_t blocks = (count + kBlock - 1) / kBlock;
       size_t maxBlocks = (size_t)cus * (size_t)maxBlocksPerCU(false, nSrcs, /*classic=*/true);

@@ -28,9 +28,12 @@ def main():
     srcs = [torch.rand(n + 64, device="cuda") for _ in range(8)]
     out = torch.empty(n + 64, device="cuda")
     for nsrc in (int(x) for x in os.environ.get("NSRCS", "8,4,2").split(",")):
-        for label, doff in (("aligned", 0), ("realigned_dst+1", 1)):
+        # aligned; every pointer one element off (shared misalignment: head
+        # peel, body on a 16-B but not a 128-B boundary); destination one
+        # element off (realigned sources)
+        for label, soff, doff in (("aligned", 0, 0), ("shared_off+1", 1, 1), ("realigned_dst+1", 0, 1)):
             d = (ctypes.c_void_p * 1)(out.data_ptr() + 4 * doff)
-            s = (ctypes.c_void_p * nsrc)(*[t.data_ptr() for t in srcs[:nsrc]])
+            s = (ctypes.c_void_p * nsrc)(*[t.data_ptr() + 4 * soff for t in srcs[:nsrc]])
             call = lambda: lib.nbxReduceMulti(d, 1, s, nsrc, n, 7, op, 0, 0, ctypes.c_void_p(st.cuda_stream))
             call()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

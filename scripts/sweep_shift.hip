@@ -293,9 +293,9 @@ __global__ __launch_bounds__(256) void kshiftLds(Args a) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const uint64_t q = b0 + (uint64_t)u * 256 + tid;
-        v[s][u] = __builtin_nontemporal_load(a.base[s] + (q < n ? q : n - 1));
+        v[s][u] = __builtin_nontemporal_load(a.base[s] + (q < n ? q : n));   // pack n holds the range's last bytes
       }
-      if (tid == 0) ex[s] = a.base[s][b0 + T < n ? b0 + T : n];   // pack n holds the range's last bytes
+      if (tid == 0) ex[s] = a.base[s][b0 + T < n ? b0 + T : n];
     }
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();   // the previous tile's LDS reads are done
@@ -325,6 +325,101 @@ __global__ __launch_bounds__(256) void kshiftLds(Args a) {
   }
 }
 
+// LDS-DMA realign: a wave's tile is U x 64 output packs; it needs source
+// packs [p0, p0 + U*64] — U full DMA instructions (global_load_lds_dwordx4,
+// nt, 64 lanes x 16 B straight into LDS) plus one single-lane DMA for the
+// extra pack — per source, into a stage buffer private to the wave. S stages:
+// the wave issues tile j+S-1's DMA, waits (vmcnt) for tile j, reads each
+// output's 16 bytes back from LDS at byte offset 16 (q - p0) + sh (five
+// dwords + one byte funnel shift), folds and stores. Nothing goes through
+// VGPRs on the load side, so several tiles can be in flight per wave.
+typedef __attribute__((address_space(3))) void* lds_ptr;
+#define WAIT_VM(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory")
+template <int N>
+__device__ __forceinline__ void waitVm() {
+  if constexpr (N == 9) WAIT_VM(9);
+  else if constexpr (N == 18) WAIT_VM(18);
+  else if constexpr (N == 24) WAIT_VM(24);
+  else if constexpr (N == 27) WAIT_VM(27);
+  else if constexpr (N == 36) WAIT_VM(36);
+  else if constexpr (N == 40) WAIT_VM(40);
+  else if constexpr (N == 32) WAIT_VM(32);
+  else if constexpr (N == 48) WAIT_VM(48);
+  else if constexpr (N == 80) WAIT_VM(63);
+  else if constexpr (N == 10) WAIT_VM(10);
+  else if constexpr (N == 12) WAIT_VM(12);
+  else if constexpr (N == 15) WAIT_VM(15);
+  else if constexpr (N == 6) WAIT_VM(6);
+  else if constexpr (N == 20) WAIT_VM(20);
+  else if constexpr (N == 30) WAIT_VM(30);
+  else if constexpr (N == 5) WAIT_VM(5);
+  else if constexpr (N == 3) WAIT_VM(3);
+  else if constexpr (N == 4) WAIT_VM(4);
+  else if constexpr (N == 8) WAIT_VM(8);
+  else if constexpr (N == 16) WAIT_VM(16);
+  else WAIT_VM(0);
+}
+
+template <int NSRC, int U, int S, int W>
+__global__ __launch_bounds__(W * 64) void kshiftDma(Args a) {
+  constexpr int P = U * 64 + 1;   // packs per source per stage
+  __shared__ u32x4 sm[W][S][NSRC][P];
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  constexpr uint64_t kTile = (uint64_t)U * 64;
+  const uint64_t n = a.nPacks;
+  const uint64_t nTiles = (n + kTile - 1) / kTile;
+  const uint64_t nWaves = (uint64_t)gridDim.x * W, gw = (uint64_t)blockIdx.x * W + wave;
+  auto issue = [&](uint64_t t, int st) {
+    const uint64_t p0 = t * kTile;
+#pragma unroll
+    for (int s = 0; s < NSRC; s++) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t q = p0 + u * 64 + lane;
+        q = q < n ? q : n;   // pack n holds the range's last bytes
+        __builtin_amdgcn_global_load_lds((const void*)(a.base[s] + q), (lds_ptr)&sm[wave][st][s][u * 64], 16, 0, 2);
+      }
+      if (lane == 0) {
+        const uint64_t q = p0 + kTile < n ? p0 + kTile : n;
+        __builtin_amdgcn_global_load_lds((const void*)(a.base[s] + q), (lds_ptr)&sm[wave][st][s][kTile], 16, 0, 2);
+      }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < S - 1; k++) {
+    const uint64_t t = gw + (uint64_t)k * nWaves;
+    if (t < nTiles) issue(t, k);
+  }
+  int st = 0;
+  for (uint64_t t = gw; t < nTiles; t += nWaves) {
+    const uint64_t ahead = t + (uint64_t)(S - 1) * nWaves;
+    if (ahead < nTiles) {
+      issue(ahead, (st + S - 1) % S);
+      waitVm<(S - 1) * NSRC * (U + 1)>();   // lane 0 issued U+1 per source: the other lanes' counts are smaller, so stricter
+    } else {
+      waitVm<0>();
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t q = t * kTile + u * 64 + lane;
+      u32x4 acc;
+#pragma unroll
+      for (int s = 0; s < NSRC; s++) {
+        const uint32_t o = (uint32_t)(u * 64 + lane) * 16u + a.sh[s];
+        const uint32_t* w = (const uint32_t*)&sm[wave][st][s][0] + (o >> 2);
+        const uint32_t b = o & 3u;
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = b ? w[4] : 0u;
+        const u32x4 x = {__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
+                         __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(w4, w3, b)};
+        acc = s == 0 ? x : add4(acc, x);
+      }
+      if (q < n) a.dst[q] = acc;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    st = st + 1 == S ? 0 : st + 1;
+  }
+}
+
 struct Variant {
   std::string name;
   const void* fn;
@@ -344,8 +439,8 @@ int run(int cus, int rounds, int iters, int mib) {
   // destination one element past a 16-B boundary: 3 head elements, then
   // packs; source element k of the body sits 12 B into pack (k*4+12)/16
   float *dstRaw, *refRaw;
-  CK(hipMalloc(&dstRaw, (count + 64) * 4));
-  CK(hipMalloc(&refRaw, (count + 64) * 4));
+  CK(hipMalloc(&dstRaw, (count + 128) * 4));
+  CK(hipMalloc(&refRaw, (count + 128) * 4));
   const size_t head = 3;
   const uint64_t nPacks = (count - head) / 4;
   Args a;
@@ -372,6 +467,15 @@ int run(int cus, int rounds, int iters, int mib) {
       {"lds u2 bpc2", (const void*)&kshiftLds<NSRC, 2>, 2, 2},
       {"lds u2 bpc3", (const void*)&kshiftLds<NSRC, 2>, 2, 3},
       {"lds u4 bpc1", (const void*)&kshiftLds<NSRC, 4>, 4, 1},
+      {"dma W4 U2 S2 bpc1", (const void*)&kshiftDma<NSRC, 2, 2, 4>, -4002, 1},
+      {"dma W4 U1 S3 bpc1", (const void*)&kshiftDma<NSRC, 1, 3, 4>, -4001, 1},
+      {"dma W2 U4 S2 bpc1", (const void*)&kshiftDma<NSRC, 4, 2, 2>, -2004, 1},
+      {"dma W2 U2 S2 bpc2", (const void*)&kshiftDma<NSRC, 2, 2, 2>, -2002, 2},
+      {"dma W4 U1 S2 bpc2", (const void*)&kshiftDma<NSRC, 1, 2, 4>, -4001, 2},
+      {"dma W2 U2 S3 bpc1", (const void*)&kshiftDma<NSRC, 2, 3, 2>, -2002, 1},
+      {"dma W1 U4 S3 bpc1", (const void*)&kshiftDma<NSRC, 4, 3, 1>, -1004, 1},
+      {"dma W1 U4 S2 bpc2", (const void*)&kshiftDma<NSRC, 4, 2, 1>, -1004, 2},
+      {"dma W2 U4 S1 bpc2", (const void*)&kshiftDma<NSRC, 4, 1, 2>, -2004, 2},
   };
   // the aligned fold (reference rate, not a realigning kernel): its output
   // differs, so it is timed but not compared
@@ -381,15 +485,30 @@ int run(int cus, int rounds, int iters, int mib) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
+  // destination body: DSTOFF bytes into its (256-B aligned) allocation; 16 =
+  // the library's layout for a destination one element off (body on the
+  // next 16-B boundary), 128 / 256 = a body on a cache-line boundary
+  const char* dv = getenv("DSTOFF");
+  const size_t dstOff = dv ? (size_t)atoi(dv) : 16;
+  printf("destination body at byte %zu of its allocation\n", dstOff);
   auto launch = [&](const Variant& v, float* outRaw) {
     Args b = a;
-    b.dst = (u32x4*)(outRaw + 1 + head);   // dst + 1 element is 4 B off; its body starts 3 elements later
-    // unroll < 0: 63-lane variant, a workgroup covers 4 x 63 x |unroll| packs
-    uint64_t tile = v.unroll > 0 ? (uint64_t)v.unroll * 256 : (uint64_t)(-v.unroll) * 252;
+    b.dst = (u32x4*)((char*)outRaw + dstOff);
+    // unroll < 0: 63-lane variant, a workgroup covers 4 x 63 x |unroll| packs;
+    // <= -1000: LDS-DMA variant, -(1000 x waves + U): waves x U x 64 packs
+    int threads = 256;
+    uint64_t tile;
+    if (v.unroll > 0) tile = (uint64_t)v.unroll * 256;
+    else if (v.unroll > -1000) tile = (uint64_t)(-v.unroll) * 252;
+    else {
+      const int w = (-v.unroll) / 1000, u = (-v.unroll) % 1000;
+      threads = 64 * w;
+      tile = (uint64_t)w * u * 64;
+    }
     uint64_t grid = std::min<uint64_t>((nPacks + tile - 1) / tile, (uint64_t)cus * v.blocksPerCU);
     int ns = NSRC;
     void* args[] = {&b, &ns};
-    CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(256), args, 0, 0));
+    CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(threads), args, 0, 0));
   };
   CK(hipMemset(refRaw, 0, (count + 64) * 4));
   launch(vs[0], refRaw);
@@ -404,7 +523,7 @@ int run(int cus, int rounds, int iters, int mib) {
     for (uint64_t k = 0; k < nPacks * 4; k++) {
       float acc = hs[0][head + k];
       for (int s = 1; s < NSRC; s++) acc = acc + hs[s][head + k];
-      if (memcmp(&acc, &r[1 + head + k], 4) != 0) {
+      if (memcmp(&acc, &r[dstOff / 4 + k], 4) != 0) {
         if (bad < 4) printf("host mismatch at %llu\n", (unsigned long long)k);
         bad++;
       }

@@ -195,13 +195,64 @@ def test_realigned_sources(nbx, oracle, torch_gpu, dtype, count):
 @pytest.mark.parametrize("dtype,nsrc,count", [(7, 8, 3_000_001), (7, 4, 2_097_155), (6, 5, 4_194_309),
                                               (9, 3, 1_048_583), (10, 8, 8_388_617)])
 def test_realigned_sources_grid_stride(nbx, oracle, torch_gpu, dtype, nsrc, count):
-    """Realigned sources at sizes where the workgroups stride past the grid
-    (more packs than 4 workgroups/CU x 2 x 256 cover in one pass): the DPP
-    next-lane shape at 4+ sources, the two-load shape below; ragged last tile."""
+    """Realigned sources at sizes where the waves stride past the grid (more
+    tiles than one pass of the LDS-DMA kernel covers): stage reuse, the
+    lane-0 extra pack of every tile, ragged last tile."""
     eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
     srcs = oracle.random_inputs(dtype, nsrc, count, seed=nsrc * 7 + dtype)
     src_off = [(k * 3 * eb) % 16 for k in range(nsrc)]
     run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, src_off=src_off, dst_off=[eb % 16])
+
+
+def _hip():
+    lib = ctypes.CDLL("libamdhip64.so")
+    lib.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    lib.hipFree.argtypes = [ctypes.c_void_p]
+    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    return lib
+
+
+@pytest.mark.parametrize("dtype,nsrc", [(7, 2), (7, 5), (7, 8), (10, 3), (10, 8), (6, 4)])
+def test_realigned_source_ends_at_allocation_end(nbx, oracle, torch_gpu, dtype, nsrc):
+    """every source is its own hipMalloc of exactly 1 MiB (a page
+    multiple) and its range ends exactly at the allocation's end, at an offset
+    that differs from the destination's — so the realigning kernel's last
+    packs (the lane-0 extra pack, the clamped indices) sit right at the edge.
+    The result must equal the oracle (and the kernel must not fault: every
+    16-B pack it loads holds a byte of the source range)."""
+    torch = torch_gpu
+    hip = _hip()
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    size = 1 << 20
+    bufs = []
+    try:
+        srcs, ptrs = [], []
+        for k in range(nsrc):
+            p = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p), size) == 0
+            bufs.append(p.value)
+            off = (4 + 3 * k * eb) % 16 or eb            # source start mod 16, never 0 here
+            count = (size - 4096 - off) // eb            # range ends at the allocation end
+            srcs.append(None)
+            ptrs.append((p.value, off, count))
+        count = min(c for _, _, c in ptrs)
+        host = oracle.random_inputs(dtype, nsrc, count, seed=4000 + dtype * 10 + nsrc)
+        sp = []
+        for (b, _, _), h in zip(ptrs, host):
+            start = b + size - count * eb                # last byte of the range = last byte of the allocation
+            assert hip.hipMemcpy(ctypes.c_void_p(start), h.ctypes.data, count * eb, 1) == 0   # H2D
+            sp.append(start)
+        out = torch.full((count * eb + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+        dp = out.data_ptr() + (0 if (sp[0] % 16) else eb)    # destination alignment differs from source 0's
+        op = nbx.DevRedOpFull()
+        nbx.reduce_multi([dp], sp, count, dtype, op, 0, False, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        exp = oracle.reduce_multi(host, dtype, 0, threads=8)[0]
+        o = dp - out.data_ptr()
+        assert_same(out[o:o + count * eb].cpu().numpy().view(exp.dtype), exp, dtype)
+    finally:
+        for b in bufs:
+            hip.hipFree(ctypes.c_void_p(b))
 
 
 @pytest.mark.parametrize("dtype", [7, 6, 4])
