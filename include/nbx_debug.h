@@ -62,6 +62,16 @@ ncclResult_t nbxDebugStream(int kind, void* dst, const void* const* srcs, int nS
  * acceptance time minus second-half issue time (100 MHz ticks). */
 int nbxDebugLL128TearTest(int delayUs, int tear, long long* acceptAfterTornTicks);
 
+/* Batched-reduce launch form (nbxReduceMultiBatch): 1 = work-list kernels
+ * (bucket records in a pinned host table, any number of buckets per launch;
+ * the default, env NBX_BATCH_LIST), 0 = kernel-argument tables only; any
+ * other value only queries. Returns the mode in force before the call. */
+int nbxDebugSetBatchMode(int mode);
+
+/* Work-list table slots of `device` in `state` (0 free, 1 read by an eager
+ * launch that may still run, 2 owned by a captured graph); -1 bad device. */
+int nbxDebugBatchListSlots(int device, int state);
+
 #ifdef __cplusplus
 }
 #endif

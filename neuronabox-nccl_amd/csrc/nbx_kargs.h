@@ -60,6 +60,37 @@ struct BatchArgs {
   uint64_t w[kBatchWords];
 };
 
+// Work-list form of the batch (kReduceBatchList): the bucket records live in a
+// table outside the kernel arguments (pinned host memory the kernel reads in
+// place — NCCL's work FIFO, enqueue.cc:759 uploadWork / common.h:146-176), so
+// one launch takes any number of buckets. Fixed-size records (kBatchRecWords
+// words, 16-B aligned): tileBegin, tileEnd, count | head << 56 | nDsts << 60,
+// 8 source slots, 8 destination slots. Workgroup b owns the contiguous tiles
+// [b*T/G, (b+1)*T/G) and starts at record wgStart[b] (computed on the host),
+// so no workgroup scans the table: it reads one record per bucket it touches.
+constexpr int kBatchRecWords = 20;
+constexpr int kBatchListSlotBytes = 64 << 10;   // one table (records + wgStart) per slot
+
+constexpr int kBatchListHeaderBytes = 64;        // slot header: done word (written by the GPU)
+
+struct BatchListArgs {
+  const uint64_t* recs;      // kBatchRecWords words per bucket
+  const uint32_t* wgStart;   // first record of each workgroup
+  uint64_t totalTiles;
+  uint64_t arg;
+  const void* argPtr;
+  // completion signal of an eager launch (arrive == nullptr: none): the last
+  // workgroup to finish resets *arrive and stores seq into *doneWord (the
+  // slot header, host memory) — every record has been read by then
+  uint32_t* arrive;
+  uint64_t* doneWord;
+  uint64_t seq;
+  uint32_t preMask;
+  int32_t postOp;
+  int32_t acquireSystem;
+  int32_t pad;
+};
+
 // Launch table for one functor (kernel entry points as host handles).
 
 struct KernelSet {
@@ -73,6 +104,7 @@ struct KernelSet {
   const void* ring;                 // pipelined ring AllReduce (nbx_ring.h)
   const void* ringFifo;             // step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h)
   const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]
+  const void* batchList[kMaxKSrcs]; // batched buckets from a work-list table (kReduceBatchList), [nSrcs-1]
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
   int eltBytes;
   int valid;

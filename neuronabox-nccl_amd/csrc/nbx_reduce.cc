@@ -14,6 +14,7 @@
 //     (common_kernel.h:79-137).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstddef>
 #include <cstdio>
@@ -21,6 +22,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <vector>
 
 #include "../../include/nbx_reduce.h"
 #include "nbx_registry.h"
@@ -583,6 +585,197 @@ struct BatchPacker {
   }
 };
 
+// Work-list tables (kReduceBatchList) live in pinned, coherent host memory
+// that the kernel reads in place: one arena of kListSlots fixed-size slots per
+// device, allocated on first use outside stream capture. A slot written for an
+// eager launch is reusable once that launch's last workgroup has stored the
+// launch's sequence number into the slot's header (the done word) — a plain
+// host read, no HIP call, so it also works while a stream is being captured.
+// A slot written during capture belongs to the graph (every replay reads it)
+// and gets no done signal; a user object retained by the graph hands it back
+// when the graph is destroyed. Nothing ever waits for a slot: with none free
+// (all in flight or owned by graphs, or a capture before the arena exists)
+// the caller falls back to kernel-argument batches.
+constexpr int kListSlots = 64;
+
+struct ListArena {
+  std::mutex mu;
+  char* base = nullptr;
+  uint32_t* arrive = nullptr;           // device memory: per-slot workgroup arrival counters
+  uint64_t issued[kListSlots] = {};     // sequence of the last eager launch per slot
+  uint64_t seq = 0;
+  std::atomic<int> state[kListSlots];   // 0 free, 1 eager (done word pending), 2 owned by a graph
+  int cursor = 0;
+  ListArena() {
+    for (auto& s : state) s.store(0);
+  }
+  volatile uint64_t* doneWord(int i) { return (volatile uint64_t*)(base + (size_t)i * kBatchListSlotBytes); }
+};
+ListArena g_lists[kMaxDevices];
+
+void releaseGraphSlot(void* p) { static_cast<std::atomic<int>*>(p)->store(0); }
+
+// A free slot of this device's arena (index, *ptr = its memory), or -1.
+int acquireListSlot(int dev, bool capturing, char** ptr) {
+  if (dev < 0 || dev >= kMaxDevices) return -1;
+  ListArena& A = g_lists[dev];
+  std::lock_guard<std::mutex> lk(A.mu);
+  if (A.base == nullptr) {
+    if (capturing) return -1;   // no allocation inside a capture
+    void* p = nullptr;
+    if (hipHostMalloc(&p, (size_t)kListSlots * kBatchListSlotBytes, hipHostMallocCoherent) != hipSuccess) return -1;
+    void* d = nullptr;
+    if (hipMalloc(&d, kListSlots * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(d, 0, kListSlots * sizeof(uint32_t)) != hipSuccess) {
+      if (d) (void)hipFree(d);
+      (void)hipHostFree(p);
+      return -1;
+    }
+    std::memset(p, 0, (size_t)kListSlots * kBatchListSlotBytes);
+    A.base = (char*)p;
+    A.arrive = (uint32_t*)d;
+  }
+  int pick = -1;
+  for (int j = 0; j < kListSlots && pick < 0; j++) {
+    const int i = (A.cursor + j) % kListSlots;
+    const int s = A.state[i].load();
+    if (s == 0 || (s == 1 && *A.doneWord(i) == A.issued[i])) pick = i;
+  }
+  if (pick < 0) return -1;
+  A.state[pick].store(2);   // reserved until released by the launch
+  A.cursor = (pick + 1) % kListSlots;
+  *ptr = A.base + (size_t)pick * kBatchListSlotBytes;
+  return pick;
+}
+
+// After the launch that reads slot i: eager -> pending its done word;
+// captured -> the graph owns it until destroyed; launch failed -> free again.
+void releaseListSlot(int dev, int i, hipGraph_t graph, bool launched) {
+  ListArena& A = g_lists[dev];
+  if (!launched) {
+    A.state[i].store(0);
+    return;
+  }
+  if (graph != nullptr) {
+    hipUserObject_t obj = nullptr;
+    if (hipUserObjectCreate(&obj, &A.state[i], releaseGraphSlot, 1, hipUserObjectNoDestructorSync) == hipSuccess &&
+        hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) == hipSuccess)
+      return;   // state stays 2 until the graph lets go of it
+    return;     // could not attach: the slot stays the graph's for good (never reused)
+  }
+  A.state[i].store(1);
+}
+
+// NBX_BATCH_LIST: 1 (default) = work-list launches, 0 = kernel-argument
+// batches only (also settable through nbxDebugSetBatchMode).
+std::atomic<int> g_batchMode{-1};
+bool batchListEnabled() {
+  int m = g_batchMode.load(std::memory_order_relaxed);
+  if (m < 0) {
+    m = envInt("NBX_BATCH_LIST", 1) != 0 ? 1 : 0;
+    int expect = -1;
+    g_batchMode.compare_exchange_strong(expect, m);
+    m = g_batchMode.load();
+  }
+  return m != 0;
+}
+
+// Slots of the device's work-list arena by state (free / eager / graph-owned).
+int listSlotCount(int dev, int state) {
+  if (dev < 0 || dev >= kMaxDevices) return -1;
+  ListArena& A = g_lists[dev];
+  std::lock_guard<std::mutex> lk(A.mu);
+  if (A.base == nullptr) return state == 0 ? kListSlots : 0;
+  int n = 0;
+  for (auto& s : A.state) n += s.load() == state;
+  return n;
+}
+
+// Launches the buckets of one source count as work-list kernels (as many
+// launches as slots they need). Returns the number of buckets launched from
+// the front of `ts` (fewer than ts.size() when no slot was free).
+ncclResult_t launchBatchList(const KernelSet& ks, int nSrcs, const std::vector<const nbxReduceTask*>& ts,
+                             const nbxDevRedOpFull& op, uint32_t preMask, int postOp, int acq, hipStream_t st,
+                             size_t* done) {
+  *done = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  if (hipStreamGetCaptureInfo_v2(st, &cs, nullptr, &graph, nullptr, nullptr) != hipSuccess) {
+    cs = hipStreamCaptureStatusNone;
+    graph = nullptr;
+  }
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  if (capturing && (cs != hipStreamCaptureStatusActive || graph == nullptr)) return ncclSuccess;
+  const uint64_t maxG = (uint64_t)cuCount(dev) * (uint64_t)maxBlocksPerCU(false, nSrcs, acq != 0);
+  const size_t recCap = ((size_t)kBatchListSlotBytes - kBatchListHeaderBytes - (size_t)maxG * sizeof(uint32_t)) /
+                        ((size_t)kBatchRecWords * 8);
+  const int eb = ks.eltBytes;
+  const uint64_t epp = (uint64_t)(16 / eb);
+  size_t i = 0;
+  while (i < ts.size()) {
+    char* mem = nullptr;
+    const int slot = acquireListSlot(dev, capturing, &mem);
+    if (slot < 0) return ncclSuccess;
+    const size_t nRec = std::min(recCap, ts.size() - i);
+    uint64_t* recs = (uint64_t*)(mem + kBatchListHeaderBytes);
+    uint64_t tiles = 0;
+    for (size_t r = 0; r < nRec; r++) {
+      const nbxReduceTask& t = *ts[i + r];
+      const unsigned mis = (unsigned)((uintptr_t)t.srcs[0] & 15u);
+      uint64_t head = mis ? (uint64_t)((16u - mis) / (unsigned)eb) : 0;
+      if (head > t.count) head = t.count;
+      const uint64_t nPacks = (t.count - head) / epp;
+      const uint64_t bt = (nPacks + kBatchTilePacks - 1) / kBatchTilePacks;
+      uint64_t* w = recs + r * kBatchRecWords;
+      w[0] = tiles;
+      tiles += bt ? bt : 1;   // a bucket below one pack still owns a tile (its elements)
+      w[1] = tiles;
+      w[2] = (uint64_t)t.count | head << 56 | (uint64_t)t.nDsts << 60;
+      for (int s = 0; s < kMaxKSrcs; s++) w[3 + s] = s < nSrcs ? (uint64_t)(uintptr_t)t.srcs[s] : 0;
+      for (int d = 0; d < kMaxKDsts; d++) w[3 + kMaxKSrcs + d] = d < t.nDsts ? (uint64_t)(uintptr_t)t.dsts[d] : 0;
+    }
+    const uint64_t G = tiles < maxG ? tiles : maxG;
+    uint32_t* wgStart = (uint32_t*)(recs + nRec * kBatchRecWords);
+    size_t k = 0;
+    for (uint64_t b = 0; b < G; b++) {   // first record of workgroup b: the one holding tile b*T/G
+      const uint64_t t0 = b * tiles / G;
+      while (recs[k * kBatchRecWords + 1] <= t0) k++;
+      wgStart[b] = (uint32_t)k;
+    }
+    BatchListArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.recs = recs;
+    a.wgStart = wgStart;
+    a.totalTiles = tiles;
+    a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
+    a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
+    a.preMask = preMask;
+    a.postOp = postOp;
+    a.acquireSystem = acq;
+    if (!capturing) {   // eager: the kernel signals the slot free (under the arena lock: seq order)
+      ListArena& A = g_lists[dev];
+      std::lock_guard<std::mutex> lk(A.mu);
+      A.issued[slot] = ++A.seq;
+      a.seq = A.seq;
+      a.arrive = A.arrive + slot;
+      a.doneWord = (uint64_t*)A.doneWord(slot);
+    }
+    void* args[] = {&a};
+    const hipError_t err =
+        hipLaunchKernel(ks.batchList[nSrcs - 1], dim3((unsigned)G), dim3(kBlock), args, 0, st);
+    releaseListSlot(dev, slot, capturing ? graph : nullptr, err == hipSuccess);
+    if (err != hipSuccess) {
+      std::fprintf(stderr, "nbx: batch-list kernel launch failed: %s\n", hipGetErrorString(err));
+      return ncclUnhandledCudaError;
+    }
+    i += nRec;
+    *done = i;
+  }
+  return ncclSuccess;
+}
+
 ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDataType_t datatype,
                                   nbxDevRedOpFull op, int nPreOpSrcs, int postOp, ncclStream_t stream, int flags) {
   if (nTasks < 0 || (nTasks > 0 && tasks == nullptr)) return ncclInvalidArgument;
@@ -611,6 +804,8 @@ ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDa
   (void)hipGetDevice(&dev);
   const uint64_t cus = (uint64_t)cuCount(dev);
   std::unique_ptr<BatchPacker> packers[kMaxKSrcs];
+  std::vector<const nbxReduceTask*> lists[kMaxKSrcs];
+  const bool useList = batchListEnabled();
   for (int i = 0; i < nTasks; i++) {
     const nbxReduceTask& t = tasks[i];
     if (t.count == 0) continue;
@@ -626,19 +821,27 @@ ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDa
       if (r != ncclSuccess) return r;
       continue;
     }
-    std::unique_ptr<BatchPacker>& pk = packers[t.nSrcs - 1];
-    if (!pk) {
-      uint32_t mask = 0;
-      if (pre)
-        for (int s = 0; s < t.nSrcs; s++)
-          if (s < nPreOpSrcs) mask |= 1u << s;
-      pk.reset(new BatchPacker(ks, t.nSrcs, op, mask, post, acq, st));
-    }
-    r = pk->add(t);
-    if (r != ncclSuccess) return r;
+    lists[t.nSrcs - 1].push_back(&t);
   }
   for (int q = 0; q < kMaxKSrcs; q++) {
-    if (!packers[q]) continue;
+    if (lists[q].empty()) continue;
+    const int ns = q + 1;
+    uint32_t mask = 0;
+    if (pre)
+      for (int s = 0; s < ns; s++)
+        if (s < nPreOpSrcs) mask |= 1u << s;
+    size_t done = 0;
+    if (useList) {
+      r = launchBatchList(ks, ns, lists[q], op, mask, post, acq, st, &done);
+      if (r != ncclSuccess) return r;
+    }
+    if (done == lists[q].size()) continue;
+    // the rest as kernel-argument batches (work lists off, or no table slot free)
+    packers[q].reset(new BatchPacker(ks, ns, op, mask, post, acq, st));
+    for (size_t j = done; j < lists[q].size(); j++) {
+      r = packers[q]->add(*lists[q][j]);
+      if (r != ncclSuccess) return r;
+    }
     r = packers[q]->flush();
     if (r != ncclSuccess) return r;
   }
@@ -699,5 +902,15 @@ __attribute__((visibility("default"))) int nbxKernelCount(void) {
 }
 
 __attribute__((visibility("default"))) int nbxAbiVersion(void) { return 1; }
+
+__attribute__((visibility("default"))) int nbxDebugSetBatchMode(int mode) {
+  const int prev = batchListEnabled() ? 1 : 0;
+  if (mode == 0 || mode == 1) g_batchMode.store(mode);
+  return prev;
+}
+
+__attribute__((visibility("default"))) int nbxDebugBatchListSlots(int device, int state) {
+  return listSlotCount(device, state);
+}
 
 }  // extern "C"

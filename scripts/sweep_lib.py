@@ -253,8 +253,10 @@ def main():
                             lib.nbxReduceMultiBatch(tasks, len(calls), dt, op, 0, 0, ctypes.c_void_p(stream))
 
                     res = {}
-                    for mode in ("single", "batch_auto", "batch_all"):
+                    for mode in ("single", "batch_auto", "batch_kernarg", "batch_all"):
                         nbx.set_launch_config(0, 1 if mode == "batch_all" else 0)
+                        # batch_kernarg: the kernel-argument tables instead of work lists
+                        lib.nbxDebugSetBatchMode(0 if mode == "batch_kernarg" else 1)
                         # eager (host launch rate included) and graph-replayed (device time)
                         t = [timed(torch, lambda: enqueue(mode, st), iters) for _ in range(args.rounds)]
                         g = torch.cuda.CUDAGraph()
@@ -267,6 +269,7 @@ def main():
                                     enqueue(mode, cs.cuda_stream)
                         tg = [timed(torch, g.replay, max(1, iters // 10)) / 10 for _ in range(args.rounds)]
                         nbx.set_launch_config(0, 0)
+                        lib.nbxDebugSetBatchMode(1)
                         t.sort()
                         tg.sort()
                         res[mode] = t[len(t) // 2]

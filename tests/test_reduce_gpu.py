@@ -479,6 +479,89 @@ def test_batch_mixed_bucket_sweep_fp16_bf16(nbx, oracle, torch_gpu):
         nbx.set_launch_config(0, 0)
 
 
+@pytest.mark.parametrize("mode", [1, 0])
+def test_batch_work_list_and_kernarg_forms(nbx, oracle, torch_gpu, mode):
+    """Both launch forms of nbxReduceMultiBatch on the same ragged sets: work
+    lists (mode 1: records in a pinned host table, ~370 buckets per table, so
+    450 two-source buckets need two launches) and kernel-argument tables (mode
+    0: 101 two-source / 28 eight-source-eight-destination records per launch)."""
+    lib = nbx.load_library()
+    prev = lib.nbxDebugSetBatchMode(mode)
+    try:
+        rng = np.random.default_rng(31 + mode)
+        buckets = [(2, 1, int(rng.integers(1, 5000)), 0, 0, 4000 + i) for i in range(450)]
+        buckets += [(8, 8, int(rng.integers(1, 20000)), 8, 8, 5000 + i) for i in range(40)]
+        buckets += [(5, 2, int(rng.integers(1, 300000)), 4, 4, 6000 + i) for i in range(6)]
+        run_batch(nbx, oracle, torch_gpu, 7, 0, 0, buckets)
+        run_batch(nbx, oracle, torch_gpu, 6, 0, 0, [(8, 1, 32768, 0, 0, 7000 + i) for i in range(128)])
+    finally:
+        lib.nbxDebugSetBatchMode(prev)
+
+
+def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
+    """Work-list table slots: eager calls recycle them (more calls in flight
+    than the arena's 64 slots wait for the oldest), a call captured into a
+    graph keeps its slot for the graph's lifetime — eager calls issued between
+    replays never overwrite it — and every replay reads it in place."""
+    torch = torch_gpu
+    lib = nbx.load_library()
+    dev_id = torch.cuda.current_device()
+    prev = lib.nbxDebugSetBatchMode(1)
+    try:
+        dtype, nsrc = 7, 4
+        counts = [3000, 70000, 5, 40001]
+        srcs = [[torch.empty(c, dtype=torch.float32, device="cuda") for _ in range(nsrc)] for c in counts]
+        outs = [torch.empty(c, dtype=torch.float32, device="cuda") for c in counts]
+        buckets = [([o.data_ptr()], [t.data_ptr() for t in ss], c) for ss, o, c in zip(srcs, outs, counts)]
+        other_in = [torch.rand(1000, device="cuda") for _ in range(2)]
+        other_out = [torch.empty(1000, device="cuda") for _ in range(3)]
+        other = [([o.data_ptr()], [t.data_ptr() for t in other_in], 1000) for o in other_out]
+        op = nbx.DevRedOpFull()
+        s = torch.cuda.Stream()
+
+        def fill(it):
+            host = []
+            for k, (ss, c) in enumerate(zip(srcs, counts)):
+                xs = oracle.random_inputs(dtype, nsrc, c, seed=300 * it + k)
+                for t, x in zip(ss, xs):
+                    t.copy_(torch.from_numpy(x))
+                host.append(xs)
+            return host
+
+        def check(host):
+            for xs, o in zip(host, outs):
+                assert_same(o.cpu().numpy(), oracle.reduce_multi(xs, dtype, 0)[0], dtype)
+
+        host = fill(0)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            for _ in range(150):   # > 64 slots in flight: the arena waits for the oldest
+                nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
+        s.synchronize()
+        check(host)
+        owned0 = lib.nbxDebugBatchListSlots(dev_id, 2)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
+        assert lib.nbxDebugBatchListSlots(dev_id, 2) == owned0 + 1
+        for it in (1, 2):
+            host = fill(it)
+            with torch.cuda.stream(s):
+                for _ in range(100):   # recycles every other slot, never the graph's
+                    nbx.reduce_multi_batch(other, dtype, op, 0, False, s.cuda_stream)
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            check(host)
+        del g
+        torch.cuda.synchronize()
+        # the graph's slot comes back once the graph is destroyed (if the
+        # runtime runs user-object destructors; otherwise it stays owned)
+        assert lib.nbxDebugBatchListSlots(dev_id, 2) in (owned0, owned0 + 1)
+    finally:
+        lib.nbxDebugSetBatchMode(prev)
+
+
 def test_invalid_arguments(nbx, torch_gpu):
     torch = torch_gpu
     a = torch.zeros(64, device="cuda")
