@@ -63,13 +63,17 @@ ncclResult_t nbxDebugStream(int kind, void* dst, const void* const* srcs, int nS
 int nbxDebugLL128TearTest(int delayUs, int tear, long long* acceptAfterTornTicks);
 
 /* Batched-reduce launch form (nbxReduceMultiBatch): 1 = work-list kernels
- * (bucket records in a pinned host table, any number of buckets per launch;
- * the default, env NBX_BATCH_LIST), 0 = kernel-argument tables only; any
- * other value only queries. Returns the mode in force before the call. */
+ * (bucket records in a table in device memory, or pinned host memory without
+ * a large BAR, up to 384 buckets per launch; the default, env NBX_BATCH_LIST;
+ * sets of <= 16 buckets that fit one kernel-argument table still use it),
+ * 0 = kernel-argument tables only; any other value only queries. Returns the
+ * mode in force before the call. */
 int nbxDebugSetBatchMode(int mode);
 
 /* Work-list table slots of `device` in `state` (0 free, 1 read by an eager
- * launch that may still run, 2 owned by a captured graph); -1 bad device. */
+ * launch that may still run, 2 owned by a captured graph); state 3: launches
+ * so far that found no free slot and fell back to kernel-argument tables;
+ * -1 bad device. */
 int nbxDebugBatchListSlots(int device, int state);
 
 #ifdef __cplusplus

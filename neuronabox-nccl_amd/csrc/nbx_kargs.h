@@ -48,6 +48,9 @@ constexpr int kBatchTilePacks = 256;   // one 16-B pack per lane per tile (kBloc
 constexpr int kBatchHeaderBytes = 40;
 constexpr int kBatchWords = (4096 - kBatchHeaderBytes) / 8;
 constexpr uint64_t kBatchCountMask = (1ull << 56) - 1;
+// up to this many buckets of one source count (fitting one table) use the
+// kernel-argument form even when work lists are on (profiles/r2/batch_list_*)
+constexpr int kBatchKernargMaxBuckets = 16;
 
 struct BatchArgs {
   uint64_t arg;
@@ -61,34 +64,34 @@ struct BatchArgs {
 };
 
 // Work-list form of the batch (kReduceBatchList): the bucket records live in a
-// table outside the kernel arguments (pinned host memory the kernel reads in
-// place — NCCL's work FIFO, enqueue.cc:759 uploadWork / common.h:146-176), so
-// one launch takes any number of buckets. Fixed-size records (kBatchRecWords
+// table outside the kernel arguments (NCCL's work FIFO, enqueue.cc:759
+// uploadWork / common.h:146-176), so one launch takes up to kListMaxRecs
+// buckets (and a call any number, in as many launches). The host writes the
+// table straight into uncached device memory through the large BAR (pinned
+// host memory where the BAR is small). Fixed-size records (kBatchRecWords
 // words, 16-B aligned): tileBegin, tileEnd, count | head << 56 | nDsts << 60,
-// 8 source slots, 8 destination slots. Workgroup b owns the contiguous tiles
-// [b*T/G, (b+1)*T/G) and starts at record wgStart[b] (computed on the host),
-// so no workgroup scans the table: it reads one record per bucket it touches.
+// 8 source slots, 8 destination slots. The records' running tile totals also
+// travel in the kernel arguments (scalar-cache hits, fresh every launch):
+// workgroups take chunks of `chunk` consecutive tiles round-robin (chunk 1 =
+// grid stride, the whole GPU on one window of memory, as for one bucket), and
+// a wave finds the record of a tile by comparing 64 tile totals at once
+// (ballot), so skipping many small buckets costs one step, not one per record.
 constexpr int kBatchRecWords = 20;
-constexpr int kBatchListSlotBytes = 64 << 10;   // one table (records + wgStart) per slot
-
-constexpr int kBatchListHeaderBytes = 64;        // slot header: done word (written by the GPU)
+constexpr int kListMaxRecs = 384;
+constexpr int kBatchListSlotBytes = kListMaxRecs * kBatchRecWords * 8;   // one table per slot
 
 struct BatchListArgs {
   const uint64_t* recs;      // kBatchRecWords words per bucket
-  const uint32_t* wgStart;   // first record of each workgroup
   uint64_t totalTiles;
   uint64_t arg;
   const void* argPtr;
-  // completion signal of an eager launch (arrive == nullptr: none): the last
-  // workgroup to finish resets *arrive and stores seq into *doneWord (the
-  // slot header, host memory) — every record has been read by then
-  uint32_t* arrive;
-  uint64_t* doneWord;
-  uint64_t seq;
   uint32_t preMask;
   int32_t postOp;
   int32_t acquireSystem;
-  int32_t pad;
+  int32_t nRecs;
+  uint32_t chunk;            // consecutive tiles per workgroup turn
+  uint32_t pad;
+  uint32_t tileEnd[kListMaxRecs];   // running tile totals (recs[k][1]); totals < 2^32
 };
 
 // Launch table for one functor (kernel entry points as host handles).

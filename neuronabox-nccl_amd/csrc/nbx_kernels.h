@@ -483,11 +483,14 @@ __global__ __launch_bounds__(kBlock) void kReduceBatch(BatchArgs a) {
 }
 
 // Work-list batch (nbx_kargs.h BatchListArgs): the same per-tile work as
-// kReduceBatch, but the records come from a table in memory and each
-// workgroup owns a contiguous run of tiles whose first record the host
-// computed, so the launch holds any number of buckets and no workgroup walks
-// the records before its own. Record loads are uniform (scalar loads); a
-// workgroup reads one record per bucket it touches.
+// kReduceBatch, records from a table in memory. Workgroups take chunks of
+// `chunk` consecutive tiles round-robin over the tiles of every bucket; when a
+// wave's tile leaves the current bucket it compares 64 running tile totals
+// from the kernel arguments at once (one per lane) and takes the first lane
+// whose total exceeds the tile (ballot) — the records are in tile order, so
+// one step skips up to 64 buckets — then reads that record from the table.
+// Every wave of the workgroup computes the same record independently (no LDS,
+// no barrier).
 template <class Fn, int NSRC>
 __global__ __launch_bounds__(kBlock) void kReduceBatchList(BatchListArgs a) {
   using E = typename Fn::Elt;
@@ -496,61 +499,61 @@ __global__ __launch_bounds__(kBlock) void kReduceBatchList(BatchListArgs a) {
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
   const bool doPost = Fn::kHasPost && a.postOp;
   const uint32_t preMask = a.preMask;
-  const uint64_t T = a.totalTiles, G = gridDim.x, b = blockIdx.x;
-  const uint64_t t0 = b * T / G, t1 = (b + 1) * T / G;
-  int64_t k = (int64_t)a.wgStart[b] - 1;
+  const uint64_t T = a.totalTiles, C = a.chunk, step = (uint64_t)gridDim.x * C;
+  const int nRecs = a.nRecs, lane = (int)(threadIdx.x & 63u);
+  int k = -1;
   uint64_t tBegin = 0, tEnd = 0, nElts = 0, n = 0;
   int nDsts = 1, head = 0;
   const E* sb[NSRC];
   E* db[kMaxKDsts];
   const u32x4* src[NSRC];
   u32x4* dst[kMaxKDsts];
-  for (uint64_t tile = t0; tile < t1; tile++) {
-    while (tile >= tEnd) {   // next record (uniform; the records are in tile order)
-      k++;
-      const uint64_t* r = a.recs + (uint64_t)k * kBatchRecWords;
-      tBegin = r[0];
-      tEnd = r[1];
-      const uint64_t meta = r[2];
-      nDsts = (int)(meta >> 60);
-      nElts = meta & kBatchCountMask;
-      head = (int)((meta >> 56) & 15u);
-      n = (nElts - (uint64_t)head) / EPP;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * C; c0 < T; c0 += step) {
+    const uint64_t c1 = c0 + C < T ? c0 + C : T;
+    for (uint64_t tile = c0; tile < c1; tile++) {
+      if (tile >= tEnd) {   // next bucket holding this tile (uniform per wave)
+        for (int base = k + 1;; base += 64) {
+          const int idx = base + lane;
+          const uint64_t e = idx < nRecs ? (uint64_t)a.tileEnd[idx] : ~0ull;
+          const uint64_t m = __ballot(e > tile);
+          if (m != 0) {
+            k = __builtin_amdgcn_readfirstlane(base + (int)__builtin_ctzll(m));
+            break;
+          }
+        }
+        const uint64_t* r = a.recs + (uint64_t)k * kBatchRecWords;
+        tBegin = r[0];
+        tEnd = r[1];
+        const uint64_t meta = r[2];
+        nDsts = (int)(meta >> 60);
+        nElts = meta & kBatchCountMask;
+        head = (int)((meta >> 56) & 15u);
+        n = (nElts - (uint64_t)head) / EPP;
 #pragma unroll
-      for (int s = 0; s < NSRC; s++) {
-        sb[s] = (const E*)r[3 + s];
-        src[s] = (const u32x4*)(sb[s] + head);
+        for (int s = 0; s < NSRC; s++) {
+          sb[s] = (const E*)r[3 + s];
+          src[s] = (const u32x4*)(sb[s] + head);
+        }
+#pragma unroll
+        for (int d = 0; d < kMaxKDsts; d++) {
+          db[d] = (E*)r[3 + kMaxKSrcs + (d < nDsts ? d : 0)];
+          dst[d] = (u32x4*)(db[d] + head);
+        }
       }
+      const uint64_t p = (tile - tBegin) * kBatchTilePacks + threadIdx.x;
+      if (p < n) {
+        u32x4 v[NSRC][1];
 #pragma unroll
-      for (int d = 0; d < kMaxKDsts; d++) {
-        db[d] = (E*)r[3 + kMaxKSrcs + (d < nDsts ? d : 0)];
-        dst[d] = (u32x4*)(db[d] + head);
+        for (int s = 0; s < NSRC; s++) v[s][0] = ldPack(src[s] + p);
+        foldStore<Fn, NSRC, 1>(fn, v, preMask, doPost, dst, nDsts, p);
       }
-    }
-    const uint64_t p = (tile - tBegin) * kBatchTilePacks + threadIdx.x;
-    if (p < n) {
-      u32x4 v[NSRC][1];
-#pragma unroll
-      for (int s = 0; s < NSRC; s++) v[s][0] = ldPack(src[s] + p);
-      foldStore<Fn, NSRC, 1>(fn, v, preMask, doPost, dst, nDsts, p);
-    }
-    if (tile == tEnd - 1) {   // the bucket's last tile: its head and tail elements
-      const uint64_t tailStart = (uint64_t)head + n * EPP;
-      const int tail = (int)(nElts - tailStart);
-      const int th = (int)threadIdx.x;
-      if (th < head) batchElt<Fn, NSRC>(fn, sb, db, nDsts, preMask, doPost, (uint64_t)th);
-      else if (th < head + tail)
-        batchElt<Fn, NSRC>(fn, sb, db, nDsts, preMask, doPost, tailStart + (uint64_t)(th - head));
-    }
-  }
-  // eager launch: the last workgroup out tells the host the table slot is free
-  if (a.arrive != nullptr) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t prev = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev + 1 == gridDim.x) {
-        __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.doneWord, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (tile == tEnd - 1) {   // the bucket's last tile: its head and tail elements
+        const uint64_t tailStart = (uint64_t)head + n * EPP;
+        const int tail = (int)(nElts - tailStart);
+        const int th = (int)threadIdx.x;
+        if (th < head) batchElt<Fn, NSRC>(fn, sb, db, nDsts, preMask, doPost, (uint64_t)th);
+        else if (th < head + tail)
+          batchElt<Fn, NSRC>(fn, sb, db, nDsts, preMask, doPost, tailStart + (uint64_t)(th - head));
       }
     }
   }

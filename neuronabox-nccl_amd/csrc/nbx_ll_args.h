@@ -39,7 +39,7 @@ struct LLArgs {
   const volatile int* abortWord;
   volatile int* errWord;
   uint64_t timeoutTicks;
-  // LL128 (kLL128Coll only): 64-byte lines, 56 payload bytes + 8-byte flag
+  // LL128 (kLL128Coll only): 64-byte lines, 4 x {12 payload bytes + 4-byte flag}
   uint64_t* const* peerL128;  // device table: rank -> LL128 buffer base
   uint64_t* myL128;
   uint64_t l128SlotLines;     // lines per (parity, source) slot

@@ -585,35 +585,64 @@ struct BatchPacker {
   }
 };
 
-// Work-list tables (kReduceBatchList) live in pinned, coherent host memory
-// that the kernel reads in place: one arena of kListSlots fixed-size slots per
-// device, allocated on first use outside stream capture. A slot written for an
-// eager launch is reusable once that launch's last workgroup has stored the
-// launch's sequence number into the slot's header (the done word) — a plain
-// host read, no HIP call, so it also works while a stream is being captured.
-// A slot written during capture belongs to the graph (every replay reads it)
-// and gets no done signal; a user object retained by the graph hands it back
-// when the graph is destroyed. Nothing ever waits for a slot: with none free
-// (all in flight or owned by graphs, or a capture before the arena exists)
-// the caller falls back to kernel-argument batches.
-constexpr int kListSlots = 64;
+// Work-list tables (kReduceBatchList): one arena of kListSlots fixed-size
+// slots per device, allocated on first use outside stream capture. Where the
+// device's memory is CPU-visible (large BAR) the arena is uncached device
+// memory the host writes directly — a workgroup's dependent record read then
+// costs ~110 ns instead of ~1.2 us from pinned host memory
+// (scripts/probe_table_mem.hip, profiles/r2/probe_table_mem_r2.txt); uncached,
+// so no GPU cache can keep an earlier table of a reused slot. Otherwise the
+// arena is pinned, coherent host memory the kernel reads in place.
+// A slot written for an eager launch is reusable once the event recorded after
+// that launch has completed; every eager call sweeps a few slots' events so
+// completed slots return to the free pool (a capture cannot query events). A
+// slot written while the stream is being captured belongs to the graph (every
+// replay reads it); a user object retained by the graph hands it back when
+// the graph is destroyed. Nothing ever waits for a slot: with none free the
+// caller falls back to kernel-argument batches.
+constexpr int kListSlots = 128;
+constexpr int kListSweep = 8;   // eager calls query at most this many in-flight slots
 
 struct ListArena {
   std::mutex mu;
   char* base = nullptr;
-  uint32_t* arrive = nullptr;           // device memory: per-slot workgroup arrival counters
-  uint64_t issued[kListSlots] = {};     // sequence of the last eager launch per slot
-  uint64_t seq = 0;
-  std::atomic<int> state[kListSlots];   // 0 free, 1 eager (done word pending), 2 owned by a graph
-  int cursor = 0;
+  bool onDevice = false;
+  hipEvent_t ev[kListSlots] = {};
+  std::atomic<int> state[kListSlots];   // 0 free, 1 eager (event pending), 2 owned by a graph
+  std::atomic<long> fallbacks{0};       // launches that found no free slot
+  int cursor = 0, sweep = 0;
   ListArena() {
     for (auto& s : state) s.store(0);
   }
-  volatile uint64_t* doneWord(int i) { return (volatile uint64_t*)(base + (size_t)i * kBatchListSlotBytes); }
 };
 ListArena g_lists[kMaxDevices];
 
 void releaseGraphSlot(void* p) { static_cast<std::atomic<int>*>(p)->store(0); }
+
+bool allocArena(ListArena& A, int dev) {
+  const size_t bytes = (size_t)kListSlots * kBatchListSlotBytes;
+  int largeBar = 0;
+  static const int want = envInt("NBX_BATCH_TABLE_DEVICE", 1);
+  void* p = nullptr;
+  if (want && hipDeviceGetAttribute(&largeBar, hipDeviceAttributeIsLargeBar, dev) == hipSuccess && largeBar &&
+      hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess) {
+    A.onDevice = true;
+  } else {
+    p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocCoherent) != hipSuccess) return false;
+    A.onDevice = false;
+  }
+  for (int i = 0; i < kListSlots; i++) {
+    if (hipEventCreateWithFlags(&A.ev[i], hipEventDisableTiming) != hipSuccess) {
+      for (int j = 0; j < i; j++) (void)hipEventDestroy(A.ev[j]);
+      if (A.onDevice) (void)hipFree(p);
+      else (void)hipHostFree(p);
+      return false;
+    }
+  }
+  A.base = (char*)p;
+  return true;
+}
 
 // A free slot of this device's arena (index, *ptr = its memory), or -1.
 int acquireListSlot(int dev, bool capturing, char** ptr) {
@@ -622,35 +651,50 @@ int acquireListSlot(int dev, bool capturing, char** ptr) {
   std::lock_guard<std::mutex> lk(A.mu);
   if (A.base == nullptr) {
     if (capturing) return -1;   // no allocation inside a capture
-    void* p = nullptr;
-    if (hipHostMalloc(&p, (size_t)kListSlots * kBatchListSlotBytes, hipHostMallocCoherent) != hipSuccess) return -1;
-    void* d = nullptr;
-    if (hipMalloc(&d, kListSlots * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(d, 0, kListSlots * sizeof(uint32_t)) != hipSuccess) {
-      if (d) (void)hipFree(d);
-      (void)hipHostFree(p);
-      return -1;
+    if (!allocArena(A, dev)) return -1;
+  }
+  if (!capturing) {   // return a few completed slots to the free pool
+    for (int j = 0; j < kListSweep; j++) {
+      const int i = A.sweep;
+      A.sweep = (A.sweep + 1) % kListSlots;
+      if (A.state[i].load() == 1 && hipEventQuery(A.ev[i]) == hipSuccess) A.state[i].store(0);
     }
-    std::memset(p, 0, (size_t)kListSlots * kBatchListSlotBytes);
-    A.base = (char*)p;
-    A.arrive = (uint32_t*)d;
   }
   int pick = -1;
   for (int j = 0; j < kListSlots && pick < 0; j++) {
     const int i = (A.cursor + j) % kListSlots;
-    const int s = A.state[i].load();
-    if (s == 0 || (s == 1 && *A.doneWord(i) == A.issued[i])) pick = i;
+    if (A.state[i].load() == 0) pick = i;
   }
-  if (pick < 0) return -1;
+  if (pick < 0 && !capturing) {   // the oldest in-flight slot, if it has completed
+    for (int j = 0; j < kListSlots && pick < 0; j++) {
+      const int i = (A.cursor + j) % kListSlots;
+      if (A.state[i].load() == 1) {
+        if (hipEventQuery(A.ev[i]) == hipSuccess) pick = i;
+        break;
+      }
+    }
+  }
+  if (pick < 0) {
+    A.fallbacks++;
+    return -1;
+  }
   A.state[pick].store(2);   // reserved until released by the launch
   A.cursor = (pick + 1) % kListSlots;
   *ptr = A.base + (size_t)pick * kBatchListSlotBytes;
   return pick;
 }
 
-// After the launch that reads slot i: eager -> pending its done word;
-// captured -> the graph owns it until destroyed; launch failed -> free again.
-void releaseListSlot(int dev, int i, hipGraph_t graph, bool launched) {
+// Make the host's writes into a device-memory slot land before the launch
+// (posted PCIe writes, write-combined mapping): fence, then read one back.
+void publishListSlot(int dev, const volatile uint32_t* last) {
+  if (!g_lists[dev].onDevice) return;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  (void)*last;
+}
+
+// After the launch that reads slot i: eager -> its event; captured -> the
+// graph owns it until destroyed; launch failed -> free again.
+void releaseListSlot(int dev, int i, hipStream_t st, hipGraph_t graph, bool launched) {
   ListArena& A = g_lists[dev];
   if (!launched) {
     A.state[i].store(0);
@@ -662,6 +706,11 @@ void releaseListSlot(int dev, int i, hipGraph_t graph, bool launched) {
         hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) == hipSuccess)
       return;   // state stays 2 until the graph lets go of it
     return;     // could not attach: the slot stays the graph's for good (never reused)
+  }
+  if (hipEventRecord(A.ev[i], st) != hipSuccess) {
+    (void)hipStreamSynchronize(st);
+    A.state[i].store(0);
+    return;
   }
   A.state[i].store(1);
 }
@@ -685,6 +734,7 @@ int listSlotCount(int dev, int state) {
   if (dev < 0 || dev >= kMaxDevices) return -1;
   ListArena& A = g_lists[dev];
   std::lock_guard<std::mutex> lk(A.mu);
+  if (state == 3) return (int)A.fallbacks.load();
   if (A.base == nullptr) return state == 0 ? kListSlots : 0;
   int n = 0;
   for (auto& s : A.state) n += s.load() == state;
@@ -709,63 +759,64 @@ ncclResult_t launchBatchList(const KernelSet& ks, int nSrcs, const std::vector<c
   const bool capturing = cs != hipStreamCaptureStatusNone;
   if (capturing && (cs != hipStreamCaptureStatusActive || graph == nullptr)) return ncclSuccess;
   const uint64_t maxG = (uint64_t)cuCount(dev) * (uint64_t)maxBlocksPerCU(false, nSrcs, acq != 0);
-  const size_t recCap = ((size_t)kBatchListSlotBytes - kBatchListHeaderBytes - (size_t)maxG * sizeof(uint32_t)) /
-                        ((size_t)kBatchRecWords * 8);
+  // 4 consecutive tiles per workgroup turn: the best of 1 / 4 / 16 on every
+  // config-C bucket set (profiles/r2/batch_list_chunk_r2p.jsonl)
+  static const uint64_t chunkEnv = (uint64_t)envInt("NBX_BATCH_CHUNK", 4);
+  const uint64_t chunk = chunkEnv < 1 ? 1 : chunkEnv;
   const int eb = ks.eltBytes;
   const uint64_t epp = (uint64_t)(16 / eb);
+  static_assert(sizeof(BatchListArgs) <= 4096, "work-list arguments must fit the kernel-argument segment");
+  BatchListArgs a;
   size_t i = 0;
   while (i < ts.size()) {
+    // this launch's buckets: up to kListMaxRecs, running tile totals < 2^32
+    size_t nRec = 0;
+    uint64_t tiles = 0;
+    while (nRec < (size_t)kListMaxRecs && i + nRec < ts.size()) {
+      const nbxReduceTask& t = *ts[i + nRec];
+      const unsigned mis = (unsigned)((uintptr_t)t.srcs[0] & 15u);
+      uint64_t head = mis ? (uint64_t)((16u - mis) / (unsigned)eb) : 0;
+      if (head > t.count) head = t.count;
+      const uint64_t bt = ((t.count - head) / epp + kBatchTilePacks - 1) / kBatchTilePacks;
+      const uint64_t next = tiles + (bt ? bt : 1);   // a bucket below one pack still owns a tile
+      if (next > 0xffffffffull) break;
+      tiles = next;
+      a.tileEnd[nRec++] = (uint32_t)tiles;
+    }
+    if (nRec == 0) return ncclSuccess;   // a bucket of >= 2^32 tiles: the caller's fallback
     char* mem = nullptr;
     const int slot = acquireListSlot(dev, capturing, &mem);
     if (slot < 0) return ncclSuccess;
-    const size_t nRec = std::min(recCap, ts.size() - i);
-    uint64_t* recs = (uint64_t*)(mem + kBatchListHeaderBytes);
-    uint64_t tiles = 0;
+    uint64_t* recs = (uint64_t*)mem;   // write-only: the slot may be device memory behind the BAR
     for (size_t r = 0; r < nRec; r++) {
       const nbxReduceTask& t = *ts[i + r];
       const unsigned mis = (unsigned)((uintptr_t)t.srcs[0] & 15u);
       uint64_t head = mis ? (uint64_t)((16u - mis) / (unsigned)eb) : 0;
       if (head > t.count) head = t.count;
-      const uint64_t nPacks = (t.count - head) / epp;
-      const uint64_t bt = (nPacks + kBatchTilePacks - 1) / kBatchTilePacks;
       uint64_t* w = recs + r * kBatchRecWords;
-      w[0] = tiles;
-      tiles += bt ? bt : 1;   // a bucket below one pack still owns a tile (its elements)
-      w[1] = tiles;
+      w[0] = r ? a.tileEnd[r - 1] : 0;
+      w[1] = a.tileEnd[r];
       w[2] = (uint64_t)t.count | head << 56 | (uint64_t)t.nDsts << 60;
       for (int s = 0; s < kMaxKSrcs; s++) w[3 + s] = s < nSrcs ? (uint64_t)(uintptr_t)t.srcs[s] : 0;
       for (int d = 0; d < kMaxKDsts; d++) w[3 + kMaxKSrcs + d] = d < t.nDsts ? (uint64_t)(uintptr_t)t.dsts[d] : 0;
     }
-    const uint64_t G = tiles < maxG ? tiles : maxG;
-    uint32_t* wgStart = (uint32_t*)(recs + nRec * kBatchRecWords);
-    size_t k = 0;
-    for (uint64_t b = 0; b < G; b++) {   // first record of workgroup b: the one holding tile b*T/G
-      const uint64_t t0 = b * tiles / G;
-      while (recs[k * kBatchRecWords + 1] <= t0) k++;
-      wgStart[b] = (uint32_t)k;
-    }
-    BatchListArgs a;
-    std::memset(&a, 0, sizeof(a));
+    const uint64_t chunks = (tiles + chunk - 1) / chunk;
+    const uint64_t G = chunks < maxG ? chunks : maxG;
     a.recs = recs;
-    a.wgStart = wgStart;
+    a.nRecs = (int)nRec;
+    a.chunk = (uint32_t)chunk;
+    a.pad = 0;
     a.totalTiles = tiles;
     a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
     a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
     a.preMask = preMask;
     a.postOp = postOp;
     a.acquireSystem = acq;
-    if (!capturing) {   // eager: the kernel signals the slot free (under the arena lock: seq order)
-      ListArena& A = g_lists[dev];
-      std::lock_guard<std::mutex> lk(A.mu);
-      A.issued[slot] = ++A.seq;
-      a.seq = A.seq;
-      a.arrive = A.arrive + slot;
-      a.doneWord = (uint64_t*)A.doneWord(slot);
-    }
+    publishListSlot(dev, (const volatile uint32_t*)(recs + nRec * kBatchRecWords - 1));
     void* args[] = {&a};
     const hipError_t err =
         hipLaunchKernel(ks.batchList[nSrcs - 1], dim3((unsigned)G), dim3(kBlock), args, 0, st);
-    releaseListSlot(dev, slot, capturing ? graph : nullptr, err == hipSuccess);
+    releaseListSlot(dev, slot, st, capturing ? graph : nullptr, err == hipSuccess);
     if (err != hipSuccess) {
       std::fprintf(stderr, "nbx: batch-list kernel launch failed: %s\n", hipGetErrorString(err));
       return ncclUnhandledCudaError;
@@ -831,7 +882,16 @@ ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDa
       for (int s = 0; s < ns; s++)
         if (s < nPreOpSrcs) mask |= 1u << s;
     size_t done = 0;
-    if (useList) {
+    // a handful of buckets that fit one kernel-argument table run faster from
+    // it (records in the scalar cache, a short cursor walk); longer lists,
+    // whose cursor walk dominates, take the work list
+    bool fitsKernarg = lists[q].size() <= (size_t)kBatchKernargMaxBuckets;
+    if (fitsKernarg) {
+      size_t words = 0;
+      for (const nbxReduceTask* t : lists[q]) words += (size_t)(2 + ns + t->nDsts);
+      fitsKernarg = words <= (size_t)kBatchWords;
+    }
+    if (useList && !fitsKernarg) {
       r = launchBatchList(ks, ns, lists[q], op, mask, post, acq, st, &done);
       if (r != ncclSuccess) return r;
     }

@@ -499,22 +499,23 @@ def test_batch_work_list_and_kernarg_forms(nbx, oracle, torch_gpu, mode):
 
 
 def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
-    """Work-list table slots: eager calls recycle them (more calls in flight
-    than the arena's 64 slots wait for the oldest), a call captured into a
-    graph keeps its slot for the graph's lifetime — eager calls issued between
-    replays never overwrite it — and every replay reads it in place."""
+    """Work-list table slots: eager calls recycle them (with more calls in
+    flight than the arena's 64 slots the rest fall back to kernel-argument
+    batches, never wait), a call captured into a graph keeps its slot for the
+    graph's lifetime — eager calls issued between replays never overwrite it —
+    and every replay reads it in place."""
     torch = torch_gpu
     lib = nbx.load_library()
     dev_id = torch.cuda.current_device()
     prev = lib.nbxDebugSetBatchMode(1)
     try:
         dtype, nsrc = 7, 4
-        counts = [3000, 70000, 5, 40001]
+        counts = [3000, 70000, 5, 40001] * 5   # 20 buckets: more than the kernel-argument form takes (16)
         srcs = [[torch.empty(c, dtype=torch.float32, device="cuda") for _ in range(nsrc)] for c in counts]
         outs = [torch.empty(c, dtype=torch.float32, device="cuda") for c in counts]
         buckets = [([o.data_ptr()], [t.data_ptr() for t in ss], c) for ss, o, c in zip(srcs, outs, counts)]
         other_in = [torch.rand(1000, device="cuda") for _ in range(2)]
-        other_out = [torch.empty(1000, device="cuda") for _ in range(3)]
+        other_out = [torch.empty(1000, device="cuda") for _ in range(20)]
         other = [([o.data_ptr()], [t.data_ptr() for t in other_in], 1000) for o in other_out]
         op = nbx.DevRedOpFull()
         s = torch.cuda.Stream()
@@ -539,6 +540,11 @@ def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
                 nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
         s.synchronize()
         check(host)
+        with torch.cuda.stream(s):
+            for _ in range(20):   # each eager call returns a few completed slots to the free pool
+                nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
+                s.synchronize()
+        assert lib.nbxDebugBatchListSlots(dev_id, 0) > 0
         owned0 = lib.nbxDebugBatchListSlots(dev_id, 2)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
