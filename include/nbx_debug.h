@@ -66,8 +66,8 @@ int nbxDebugLL128TearTest(int delayUs, int tear, long long* acceptAfterTornTicks
  * (bucket records in a table in device memory, or pinned host memory without
  * a large BAR, up to 384 buckets per launch; the default, env NBX_BATCH_LIST;
  * sets of <= 16 buckets that fit one kernel-argument table still use it),
- * 0 = kernel-argument tables only; any other value only queries. Returns the
- * mode in force before the call. */
+ * 2 = work lists for every set, 0 = kernel-argument tables only; any other
+ * value only queries. Returns the mode in force before the call. */
 int nbxDebugSetBatchMode(int mode);
 
 /* Work-list table slots of `device` in `state` (0 free, 1 read by an eager

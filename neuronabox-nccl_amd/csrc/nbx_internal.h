@@ -2,9 +2,29 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <mutex>
+#include <utility>
+
 #include "../../include/nbx_reduce.h"
 
 namespace nbx {
+struct KArgs;
+// Dynamic tiles (nbx_tiles.h forEachTile): begin() gives the launch its
+// stream's counter and base (a.dynCtr / a.dynBase) and holds the counter lock
+// until done(), which advances the base by the launch's tile count if the
+// launch went out. begin() returns false (static grid stride) while the
+// stream is being captured, for hipStreamPerThread, or with
+// NBX_DYNAMIC_TILES=0 (nbx_reduce.cc).
+class DynLaunch {
+ public:
+  bool begin(int dev, hipStream_t st, uint64_t nTiles, KArgs& a);
+  void done(bool launched);
+
+ private:
+  std::unique_lock<std::mutex> lk_;
+  std::pair<uint32_t*, uint32_t>* slot_ = nullptr;
+  uint64_t tiles_ = 0;
+};
 struct LLArgs;
 struct RingArgs;
 struct RingFifoArgs;

@@ -31,6 +31,12 @@ struct KArgs {
   int32_t headElts;   // elements before the 16-B aligned body
   int32_t variant;    // 0 = small tile (U = 1), 1 = big tile
   int32_t acquireSystem;  // 1: system-scope acquire at kernel start (sources include peer GPU memory)
+  // dynamic tiles (dynCtr != nullptr): tiles past the first gridDim.x come
+  // from a per-stream counter that every launch on that stream advances by
+  // exactly its tile count; this launch's tiles are counter - dynBase
+  uint32_t* dynCtr;
+  uint32_t dynBase;
+  int32_t pad;
 };
 
 // Batched reduce (nbxReduceMultiBatch): several independent buckets with the

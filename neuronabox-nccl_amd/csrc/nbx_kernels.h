@@ -23,6 +23,7 @@
 #include "nbx_functors.h"
 #include "nbx_kargs.h"
 #include "nbx_ll.h"
+#include "nbx_tiles.h"
 
 namespace nbx {
 
@@ -129,8 +130,8 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
   const uint32_t preMask = a.preMask;
   const uint64_t n = a.nPacks;
   constexpr uint64_t kTile = (uint64_t)U * kBlock;
-  const uint64_t stride = (uint64_t)gridDim.x * kTile;
-  for (uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x; p < n; p += stride) {
+  forEachTile(a, (n + kTile - 1) / kTile, [&](uint64_t t) {
+    const uint64_t p = t * kTile + threadIdx.x;
     if (p + (uint64_t)(U - 1) * kBlock < n) {
       // full tile: issue every load first, then fold
       u32x4 v[NSRC][U];
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void kReducePacks(KArgs a) {
         }
       }
     }
-  }
+  });
 
   // head (< EPP elements before the aligned body) and tail (< EPP after it)
   if (blockIdx.x == gridDim.x - 1) {

@@ -22,6 +22,8 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "../../include/nbx_reduce.h"
@@ -146,6 +148,26 @@ bool overlaps(const void* a, const void* b, size_t bytes) {
   return x < y + bytes && y < x + bytes;
 }
 
+// Dynamic tiles (kernels' forEachTile): one 32-bit counter per (device,
+// stream) in device memory. Every launch on a stream advances its counter by
+// exactly its tile count, so the host knows each launch's base without the
+// kernel resetting anything; launches on one stream run in order, so no two
+// launches ever share a counter concurrently. The lock is held from reading
+// the base to the launch, so calls racing on one stream from several threads
+// still enqueue in base order. Not used while the stream is being captured
+// (a replay would reuse a stale base), for hipStreamPerThread (one handle,
+// many streams), or with NBX_DYNAMIC_TILES=0.
+constexpr int kDynCounters = 4096;
+
+struct DynTiles {
+  std::mutex mu;
+  uint32_t* pool = nullptr;
+  int used = 0;
+  bool failed = false;
+  std::unordered_map<hipStream_t, std::pair<uint32_t*, uint32_t>> next;   // stream -> (counter, base)
+};
+DynTiles g_dyn[kMaxDevices];
+
 // One kernel pass over <= kMaxKSrcs sources.
 ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const void* const* srcs,
                         int nSrcs, size_t count, const nbxDevRedOpFull& op, uint32_t preMask,
@@ -197,8 +219,11 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
     if (grid == 0) grid = 1;
     a.variant = big ? 1 : 0;
+    DynLaunch dyn;
+    if (big) dyn.begin(dev, stream, tiles, a);
     err = hipLaunchKernel((const void*)ks.packs[big ? 1 : 0][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args,
                           0, stream);
+    dyn.done(err == hipSuccess);
   } else {
     const unsigned dmis = (unsigned)((uintptr_t)dsts[0] & 15u);
     bool dstShared = true;
@@ -241,6 +266,48 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
 }
 
 }  // namespace
+
+namespace nbx {
+bool DynLaunch::begin(int dev, hipStream_t st, uint64_t nTiles, KArgs& a) {
+  static const int on = envInt("NBX_DYNAMIC_TILES", 1);
+  if (!on || dev < 0 || dev >= kMaxDevices || st == hipStreamPerThread || nTiles == 0 || nTiles > 0xffffffffull)
+    return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  DynTiles& D = g_dyn[dev];
+  lk_ = std::unique_lock<std::mutex>(D.mu);
+  if (D.pool == nullptr) {
+    void* p = nullptr;
+    if (D.failed || hipMalloc(&p, kDynCounters * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(p, 0, kDynCounters * sizeof(uint32_t)) != hipSuccess) {
+      if (p) (void)hipFree(p);
+      D.failed = true;
+      lk_.unlock();
+      return false;
+    }
+    D.pool = (uint32_t*)p;
+  }
+  auto it = D.next.find(st);
+  if (it == D.next.end()) {
+    if (D.used >= kDynCounters) {
+      lk_.unlock();
+      return false;
+    }
+    it = D.next.emplace(st, std::make_pair(D.pool + D.used++, 0u)).first;
+  }
+  slot_ = &it->second;
+  tiles_ = nTiles;
+  a.dynCtr = slot_->first;
+  a.dynBase = slot_->second;
+  return true;
+}
+
+void DynLaunch::done(bool launched) {
+  if (slot_ && launched) slot_->second += (uint32_t)tiles_;   // mod 2^32, as the kernel's arithmetic
+  slot_ = nullptr;
+  if (lk_.owns_lock()) lk_.unlock();
+}
+}  // namespace nbx
 
 namespace nbx {
 // Workgroup cap of the LL-family kernels from an env knob, clamped to [1, 1024].
@@ -715,19 +782,22 @@ void releaseListSlot(int dev, int i, hipStream_t st, hipGraph_t graph, bool laun
   A.state[i].store(1);
 }
 
-// NBX_BATCH_LIST: 1 (default) = work-list launches, 0 = kernel-argument
-// batches only (also settable through nbxDebugSetBatchMode).
+// NBX_BATCH_LIST: 1 (default) = work-list launches (sets of <= 16 buckets
+// that fit one kernel-argument table excepted), 2 = work lists for every set,
+// 0 = kernel-argument batches only (also settable through nbxDebugSetBatchMode).
 std::atomic<int> g_batchMode{-1};
-bool batchListEnabled() {
+int batchMode() {
   int m = g_batchMode.load(std::memory_order_relaxed);
   if (m < 0) {
-    m = envInt("NBX_BATCH_LIST", 1) != 0 ? 1 : 0;
+    const int e = envInt("NBX_BATCH_LIST", 1);
+    m = e == 0 ? 0 : (e == 2 ? 2 : 1);
     int expect = -1;
     g_batchMode.compare_exchange_strong(expect, m);
     m = g_batchMode.load();
   }
-  return m != 0;
+  return m;
 }
+bool batchListEnabled() { return batchMode() != 0; }
 
 // Slots of the device's work-list arena by state (free / eager / graph-owned).
 int listSlotCount(int dev, int state) {
@@ -885,7 +955,7 @@ ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDa
     // a handful of buckets that fit one kernel-argument table run faster from
     // it (records in the scalar cache, a short cursor walk); longer lists,
     // whose cursor walk dominates, take the work list
-    bool fitsKernarg = lists[q].size() <= (size_t)kBatchKernargMaxBuckets;
+    bool fitsKernarg = batchMode() != 2 && lists[q].size() <= (size_t)kBatchKernargMaxBuckets;
     if (fitsKernarg) {
       size_t words = 0;
       for (const nbxReduceTask* t : lists[q]) words += (size_t)(2 + ns + t->nDsts);
@@ -964,8 +1034,8 @@ __attribute__((visibility("default"))) int nbxKernelCount(void) {
 __attribute__((visibility("default"))) int nbxAbiVersion(void) { return 1; }
 
 __attribute__((visibility("default"))) int nbxDebugSetBatchMode(int mode) {
-  const int prev = batchListEnabled() ? 1 : 0;
-  if (mode == 0 || mode == 1) g_batchMode.store(mode);
+  const int prev = batchMode();
+  if (mode >= 0 && mode <= 2) g_batchMode.store(mode);
   return prev;
 }
 

@@ -12,6 +12,7 @@
 #include "../../include/nbx_debug.h"
 #include "nbx_functors.h"
 #include "nbx_kargs.h"
+#include "nbx_tiles.h"
 
 namespace nbx {
 namespace {
@@ -27,9 +28,9 @@ __global__ __launch_bounds__(kBlock) void kStreamRead(KArgs a) {
   for (int s = 0; s < NSRC; s++) src[s] = (const u32x4*)a.src[s];
   const uint64_t n = a.nPacks;
   constexpr uint64_t kTile = (uint64_t)U * kBlock;
-  const uint64_t stride = (uint64_t)gridDim.x * kTile;
   u32x4 acc = {0, 0, 0, 0};
-  for (uint64_t p = (uint64_t)blockIdx.x * kTile + threadIdx.x; p + (uint64_t)(U - 1) * kBlock < n; p += stride) {
+  forEachTile(a, n / kTile, [&](uint64_t t) {
+    const uint64_t p = t * kTile + threadIdx.x;
     u32x4 v[NSRC][U];
 #pragma unroll
     for (int s = 0; s < NSRC; s++)
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(kBlock) void kStreamRead(KArgs a) {
     for (int s = 0; s < NSRC; s++)
 #pragma unroll
       for (int u = 0; u < U; u++) acc ^= v[s][u];
-  }
+  });
   if (acc.x == (uint32_t)a.arg && acc.y == (uint32_t)(a.arg >> 32) && acc.z == 0x9e3779b9u)
     ((u32x4*)a.dst[0])[blockIdx.x * kBlock + threadIdx.x] = acc;
 }
@@ -94,7 +95,9 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t nbxDebugStream(in
   if (grid == 0) return ncclSuccess;
   void* args[] = {&a};
   const void* fn = kind == 0 ? (const void*)&kStreamRead<kMaxKSrcs, 4> : (const void*)&kStreamWrite<1>;
-  if (hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kBlock), args, 0, (hipStream_t)stream) != hipSuccess)
-    return ncclUnhandledCudaError;
-  return ncclSuccess;
+  // static tiles: for a read-only stream the grid stride is the faster
+  // schedule (7.07-7.10 vs 6.61 TB/s with dynamic tiles, profiles/r2/bench_dyn_ab_r2u.jsonl),
+  // so the ceiling stays the higher of the two
+  const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(kBlock), args, 0, (hipStream_t)stream);
+  return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
 }

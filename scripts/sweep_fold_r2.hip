@@ -101,6 +101,41 @@ __global__ __launch_bounds__(256) void kburst(Args a) {
   }
 }
 
+// dynamic tiles: the first G tiles are static (one per workgroup), the rest
+// are taken from a global counter, fetched one tile ahead (thread 0, into a
+// double-buffered LDS word) so the atomic's latency hides behind the loads —
+// CUs that stream faster take more tiles and all finish together
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kdyn(Args a, unsigned* ctr) {
+  __shared__ unsigned nxt[2];
+  const uint64_t tile = (uint64_t)U * 256, nTiles = a.nPacks / tile;
+  uint64_t t = blockIdx.x;
+  int par = 0;
+  while (t < nTiles) {
+    if (threadIdx.x == 0) nxt[par] = atomicAdd(ctr, 1u) + gridDim.x;
+    tileFold<NSRC, U, 256>(a, t * tile + threadIdx.x);
+    __syncthreads();
+    t = nxt[par];
+    par ^= 1;
+  }
+}
+
+// per-wave dynamic tiles: a wave owns a tile of U x 64 packs; lane 0 fetches
+// the wave's next tile one ahead (readfirstlane broadcast), no LDS, no barrier
+template <int NSRC, int U>
+__global__ __launch_bounds__(256) void kdynwave(Args a, unsigned* ctr) {
+  const uint64_t tile = (uint64_t)U * 64, nTiles = a.nPacks / tile;
+  const int lane = threadIdx.x & 63;
+  const uint64_t nWaves = (uint64_t)gridDim.x * 4;
+  uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  while (t < nTiles) {
+    unsigned nx = 0;
+    if (lane == 0) nx = atomicAdd(ctr, 1u) + (unsigned)nWaves;
+    tileFold<NSRC, U, 64>(a, t * tile + lane);
+    t = (uint64_t)__builtin_amdgcn_readfirstlane(nx);
+  }
+}
+
 struct Variant {
   std::string name;
   const void* fn;
@@ -138,12 +173,32 @@ int main(int argc, char** argv) {
       {"burst4 u2 bpc1", (const void*)&kburst<8, 2, 4>, 256, 2048, 1},
       {"w512 u2 bpc1", (const void*)&kstride<8, 2, 512, 0>, 512, 1024, 1},
       {"w512 u4 bpc1", (const void*)&kstride<8, 4, 512, 0>, 512, 2048, 1},
+      {"dynamic u4 bpc1", (const void*)&kdyn<8, 4>, 256, 1024, 1},
+      {"dynamic u2 bpc2", (const void*)&kdyn<8, 2>, 256, 512, 2},
+      {"dynamic-wave u4 bpc1", (const void*)&kdynwave<8, 4>, 256, 1024, 1},
+      {"dynamic-wave u8 bpc1", (const void*)&kdynwave<8, 8>, 256, 2048, 1},
       {"production u4 bpc1 (again)", (const void*)&kstride<8, 4, 256, 0>, 256, 1024, 1},
   };
+  // dynamic variants: one zeroed counter per launch (4096 launches' worth)
+  unsigned* ctrs;
+  CK(hipMalloc(&ctrs, 4096 * 64));
+  CK(hipMemset(ctrs, 0, 4096 * 64));
+  int ctrNext = 0;
   auto launch = [&](const Variant& v, float* out) {
     Args b = a;
     b.dst = (f32x4*)out;
     uint64_t grid = std::min<uint64_t>((b.nPacks + v.tilePacks - 1) / v.tilePacks, (uint64_t)cus * v.blocksPerCU);
+    if (v.name.rfind("dynamic", 0) == 0) {
+      if (ctrNext >= 4096) {
+        CK(hipDeviceSynchronize());
+        CK(hipMemset(ctrs, 0, 4096 * 64));
+        ctrNext = 0;
+      }
+      unsigned* c = ctrs + 16 * ctrNext++;
+      void* args[] = {&b, &c};
+      CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.threads), args, 0, 0));
+      return;
+    }
     void* args[] = {&b};
     CK(hipLaunchKernel(v.fn, dim3((unsigned)grid), dim3(v.threads), args, 0, 0));
   };

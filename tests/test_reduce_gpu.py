@@ -353,21 +353,28 @@ def run_batch(nbx, oracle, torch, dtype, devop, arg, buckets, npre=0, post=False
             assert (t[do + count * eb:].cpu().numpy() == 0xA5).all() and (t[:do].cpu().numpy() == 0xA5).all()
 
 
+@pytest.mark.parametrize("form", [0, 2])
 @pytest.mark.parametrize("dtype", ALL_TYPES)
-def test_batch_all_types_ops(nbx, oracle, torch_gpu, dtype):
+def test_batch_all_types_ops(nbx, oracle, torch_gpu, dtype, form):
     """Batched buckets: every op, ragged sizes (below one pack, one tile +- 1,
-    several tiles), 1-8 sources and 1-3 destinations in one call."""
-    rng = np.random.default_rng(dtype)
-    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
-    epp = 16 // eb
-    for devop in devops_for(dtype):
-        arg = op_arg(oracle, dtype, devop, rng)
-        buckets = []
-        for i, count in enumerate([1, epp - 1, epp, 256 * epp - 1, 256 * epp + 1, 3001, 70001]):
-            nsrc = 1 + (i + devop) % 8
-            buckets.append((nsrc, 1 + i % 3, count, 0, 0, 100 * dtype + 10 * devop + i))
-        run_batch(nbx, oracle, torch_gpu, dtype, devop, arg, buckets, npre=2 if devop == 3 else 0,
-                  post=devop == 4)
+    several tiles), 1-8 sources and 1-3 destinations in one call — through the
+    kernel-argument tables (form 0) and the work-list kernel (form 2)."""
+    lib = nbx.load_library()
+    prev = lib.nbxDebugSetBatchMode(form)
+    try:
+        rng = np.random.default_rng(dtype)
+        eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+        epp = 16 // eb
+        for devop in devops_for(dtype):
+            arg = op_arg(oracle, dtype, devop, rng)
+            buckets = []
+            for i, count in enumerate([1, epp - 1, epp, 256 * epp - 1, 256 * epp + 1, 3001, 70001]):
+                nsrc = 1 + (i + devop) % 8
+                buckets.append((nsrc, 1 + i % 3, count, 0, 0, 100 * dtype + 10 * devop + i))
+            run_batch(nbx, oracle, torch_gpu, dtype, devop, arg, buckets, npre=2 if devop == 3 else 0,
+                      post=devop == 4)
+    finally:
+        lib.nbxDebugSetBatchMode(prev)
 
 
 @pytest.mark.parametrize("dtype", [6, 9, 7, 4])
@@ -412,13 +419,23 @@ def test_batch_large_sets(nbx, oracle, torch_gpu, dtype, nsrc):
     run_batch(nbx, oracle, torch_gpu, dtype, 0, 0, buckets)
 
 
+@pytest.mark.parametrize("form", [1, 2])
 @pytest.mark.parametrize("dtype", [7, 6, 9])
-def test_batch_device_scalar_and_graph_replay(nbx, oracle, torch_gpu, dtype):
+def test_batch_device_scalar_and_graph_replay(nbx, oracle, torch_gpu, dtype, form):
     """Batched PreMulSum with the scalar in device memory (dereferenced by the
     batch kernel while it runs), captured into a HIP graph and replayed after
     the scalar and the inputs change: the kernel-argument table is captured by
-    value, the scalar and data are read at replay time."""
-    torch = torch_gpu
+    value (form 1: four buckets use it), the work-list table (form 2) is owned
+    by the graph; the scalar and data are read at replay time."""
+    lib = nbx.load_library()
+    prev = lib.nbxDebugSetBatchMode(form)
+    try:
+        _batch_scalar_graph(nbx, oracle, torch_gpu, dtype)
+    finally:
+        lib.nbxDebugSetBatchMode(prev)
+
+
+def _batch_scalar_graph(nbx, oracle, torch, dtype):
     st_np = oracle.NP_STORAGE[dtype]
     eb = np.dtype(st_np).itemsize
     counts = [5000, 40000, 123, 77777]
@@ -763,3 +780,57 @@ def test_beyond_32bit_counts(nbx, torch_gpu):
     nbx.reduce_multi([o.data_ptr()], [x.data_ptr(), y.data_ptr()], m, 7, op, 0, False, st)
     torch.cuda.synchronize()
     assert torch.equal(o, x + y)
+
+
+def test_dynamic_tiles_across_streams_and_graphs(nbx, oracle, torch_gpu):
+    """Big-tile launches take their tiles from a per-stream counter whose
+    per-launch base the host tracks (nbx_tiles.h): many launches of different
+    sizes on three streams at once, a > 8-source multi-pass call, and a graph
+    capture (static tiles) replayed between eager calls on the same stream all
+    stay bit-exact."""
+    torch = torch_gpu
+    dtype = 7
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    sizes = [(1 << 20) + 17, 3 << 20, (1 << 21) + 4099]
+    cases = []
+    for k, n in enumerate(sizes):
+        srcs = oracle.random_inputs(dtype, 8, n, seed=900 + k)
+        exp = oracle.reduce_multi(srcs, dtype, 0, threads=8)[0]
+        ts = [torch.from_numpy(x).cuda() for x in srcs]
+        out = torch.empty(n, dtype=torch.float32, device="cuda")
+        cases.append((ts, out, exp, n))
+    op = nbx.DevRedOpFull()
+    torch.cuda.synchronize()
+    for rep in range(12):   # interleaved sizes on three streams, no host sync in between
+        for k, (ts, out, exp, n) in enumerate(cases):
+            s = streams[(k + rep) % 3]
+            with torch.cuda.stream(s):
+                out.zero_()
+                nbx.reduce_multi([out.data_ptr()], [t.data_ptr() for t in ts], n, dtype, op, 0, False, s.cuda_stream)
+            for s2 in streams:   # the next writer of `out` waits for this one
+                s2.wait_stream(s)
+    torch.cuda.synchronize()
+    for ts, out, exp, n in cases:
+        assert_same(out.cpu().numpy(), exp, dtype)
+    # multi-pass (> 8 sources) and a captured launch replayed between eager ones
+    srcs = oracle.random_inputs(dtype, 12, (1 << 21) + 5, seed=950)
+    exp = oracle.reduce_multi(srcs, dtype, 0, threads=8)[0]
+    ts = [torch.from_numpy(x).cuda() for x in srcs]
+    out = torch.empty(exp.size, dtype=torch.float32, device="cuda")
+    s = streams[0]
+    call = lambda: nbx.reduce_multi([out.data_ptr()], [t.data_ptr() for t in ts], exp.size, dtype, op, 0, False,
+                                    s.cuda_stream)
+    with torch.cuda.stream(s):
+        call()
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        call()
+    for _ in range(3):
+        with torch.cuda.stream(s):
+            out.zero_()
+            g.replay()
+            call()
+            g.replay()
+        s.synchronize()
+        assert_same(out.cpu().numpy(), exp, dtype)
