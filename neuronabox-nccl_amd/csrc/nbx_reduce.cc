@@ -219,6 +219,9 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
     if (grid == 0) grid = 1;
     a.variant = big ? 1 : 0;
+    // dynamic tiles for big tiles only: small tiles (1-3 sources, 3-5
+    // workgroups per CU, 16x the atomics) collapse to 0.7-1.4 TB/s on the
+    // counter's contention (profiles/r2/probe_dyn_r2x.jsonl)
     DynLaunch dyn;
     if (big) dyn.begin(dev, stream, tiles, a);
     err = hipLaunchKernel((const void*)ks.packs[big ? 1 : 0][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args,
