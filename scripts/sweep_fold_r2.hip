@@ -15,7 +15,7 @@
 //                 walk neighbouring tiles
 //   w512        : 512-thread workgroups (8 waves per CU), U = 2
 //
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off scripts/sweep_fold_r2.hip -o scripts/sweep_fold_r2
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -mllvm -amdgpu-atomic-optimizer-strategy=None scripts/sweep_fold_r2.hip -o scripts/sweep_fold_r2
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
@@ -112,8 +112,31 @@ __global__ __launch_bounds__(256) void kdyn(Args a, unsigned* ctr) {
   uint64_t t = blockIdx.x;
   int par = 0;
   while (t < nTiles) {
-    if (threadIdx.x == 0) nxt[par] = atomicAdd(ctr, 1u) + gridDim.x;
+    unsigned got = 0;
+    if (threadIdx.x == 0) got = atomicAdd(ctr, 1u);
     tileFold<NSRC, U, 256>(a, t * tile + threadIdx.x);
+    if (threadIdx.x == 0) nxt[par] = got + gridDim.x;
+    __syncthreads();
+    t = nxt[par];
+    par ^= 1;
+  }
+}
+
+// hybrid: the first PCT % of the tiles as a static grid stride (no atomics,
+// no barriers), the rest dynamic from the counter
+template <int NSRC, int U, int PCT>
+__global__ __launch_bounds__(256) void khyb(Args a, unsigned* ctr) {
+  __shared__ unsigned nxt[2];
+  const uint64_t tile = (uint64_t)U * 256, nTiles = a.nPacks / tile, G = gridDim.x;
+  const uint64_t nStatic = (nTiles * PCT / 100) / G * G;   // whole rounds
+  uint64_t t = blockIdx.x;
+  for (; t < nStatic; t += G) tileFold<NSRC, U, 256>(a, t * tile + threadIdx.x);
+  int par = 0;
+  while (t < nTiles) {
+    unsigned got = 0;
+    if (threadIdx.x == 0) got = atomicAdd(ctr, 1u);
+    tileFold<NSRC, U, 256>(a, t * tile + threadIdx.x);
+    if (threadIdx.x == 0) nxt[par] = got + (unsigned)(nStatic + G);
     __syncthreads();
     t = nxt[par];
     par ^= 1;
@@ -175,8 +198,12 @@ int main(int argc, char** argv) {
       {"w512 u4 bpc1", (const void*)&kstride<8, 4, 512, 0>, 512, 2048, 1},
       {"dynamic u4 bpc1", (const void*)&kdyn<8, 4>, 256, 1024, 1},
       {"dynamic u2 bpc2", (const void*)&kdyn<8, 2>, 256, 512, 2},
-      {"dynamic-wave u4 bpc1", (const void*)&kdynwave<8, 4>, 256, 1024, 1},
-      {"dynamic-wave u8 bpc1", (const void*)&kdynwave<8, 8>, 256, 2048, 1},
+      {"dynamic u2 bpc1", (const void*)&kdyn<8, 2>, 256, 512, 1},
+      {"dynamic u8 bpc1", (const void*)&kdyn<8, 8>, 256, 2048, 1},
+      {"dynamic hybrid50 u4 bpc1", (const void*)&khyb<8, 4, 50>, 256, 1024, 1},
+      {"dynamic hybrid75 u4 bpc1", (const void*)&khyb<8, 4, 75>, 256, 1024, 1},
+      {"dynamic hybrid90 u4 bpc1", (const void*)&khyb<8, 4, 90>, 256, 1024, 1},
+      {"dynamic u4 bpc1 (again)", (const void*)&kdyn<8, 4>, 256, 1024, 1},
       {"production u4 bpc1 (again)", (const void*)&kstride<8, 4, 256, 0>, 256, 1024, 1},
   };
   // dynamic variants: one zeroed counter per launch (4096 launches' worth)
