@@ -834,3 +834,45 @@ def test_dynamic_tiles_across_streams_and_graphs(nbx, oracle, torch_gpu):
             g.replay()
         s.synchronize()
         assert_same(out.cpu().numpy(), exp, dtype)
+
+
+def test_dynamic_tiles_threads_sharing_a_stream(nbx, oracle, torch_gpu):
+    """Host threads racing nbxReduceMulti calls onto ONE stream: each call
+    reads its stream counter's base and launches under one lock, so bases stay
+    in enqueue order and every call's tiles are its own (ctypes drops the GIL
+    during the call, so the threads really overlap)."""
+    import threading
+    torch = torch_gpu
+    dtype = 7
+    s = torch.cuda.Stream()
+    n = (1 << 20) + 333
+    srcs = oracle.random_inputs(dtype, 8, n, seed=977)
+    exp = oracle.reduce_multi(srcs, dtype, 0, threads=8)[0]
+    ts = [torch.from_numpy(x).cuda() for x in srcs]
+    outs = [torch.zeros(n, dtype=torch.float32, device="cuda") for _ in range(16)]
+    torch.cuda.synchronize()
+    lib = nbx.load_library()
+    sp = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in ts])
+    op = nbx.DevRedOpFull()
+    errs = []
+
+    def worker(k):
+        try:
+            for rep in range(6):
+                o = outs[(k * 4 + rep) % 16]
+                dp = (ctypes.c_void_p * 1)(o.data_ptr())
+                rc = lib.nbxReduceMulti(dp, 1, sp, 8, ctypes.c_size_t(n), dtype, op, 0, 0, ctypes.c_void_p(s.cuda_stream))
+                if rc != 0:
+                    errs.append(rc)
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    s.synchronize()
+    assert not errs, errs
+    for o in outs:
+        assert_same(o.cpu().numpy(), exp, dtype)
