@@ -252,6 +252,9 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
       const size_t maxBlocks = (size_t)cus * (size_t)shiftedBlocksPerCU(fn != nullptr, nSrcs);
       const size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
       const unsigned threads = fn ? (unsigned)(kShiftLdsWaves * 64) : (unsigned)kBlock;
+      // static tiles: dynamic workgroup tiles (4 wave tiles) were measured
+      // at 1.1-4.9 TB/s here — 4-8x the big kernel's atomics on one counter
+      // (profiles/r2/realign_dyn_r3a.jsonl)
       if (!fn) fn = ks.shifted;
       err = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(threads), args, 0, stream);
     } else {
