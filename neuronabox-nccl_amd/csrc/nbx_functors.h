@@ -172,6 +172,10 @@ struct FnBase {
   // cap on the big-tile unroll: VALU-heavy functors gain nothing from more
   // loads in flight and only grow code size
   static constexpr int kUnrollCap = 16;
+  // big-tile workgroups per CU (at least): VALU-heavy functors run two, so a
+  // second wave per SIMD has its loads in flight while the first folds
+  // (profiles/r2/probe_dtypes_r3f.jsonl)
+  static constexpr int kBigBlocksPerCU = 1;
   __device__ E pre(E a) const { return a; }
   __device__ E post(E a) const { return a; }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const { return packRed(*static_cast<const D*>(this), a, b); }
@@ -269,14 +273,35 @@ struct FnProdF : FnBase<FnProdF<Ty>, typename Ty::Elt> {
 template <class Ty>
 struct FnMinMaxF : FnBase<FnMinMaxF<Ty>, typename Ty::Elt> {
   static constexpr int kUnrollCap = sizeof(typename Ty::Elt) == 1 ? 4 : 16;
+  static constexpr int kBigBlocksPerCU = 2;   // compare + NaN test + select per element
   using E = typename Ty::Elt;
   bool isMin;  // reduce_kernel.h:47: (opArg & 1) == 0
   __device__ explicit FnMinMaxF(uint64_t arg) : isMin((arg & 1ull) == 0ull) {}
-  __device__ E red(E a, E b) const {
-    auto x = Ty::wide(a);
-    auto y = Ty::wide(b);
-    bool pickA = isMin ? (x < y || isNan(y)) : (x > y || isNan(y));
+  // fminf / fmaxf as pinned (a NaN operand yields the other, a tie returns the
+  // second operand); bitwise | so no short-circuit turns into a branch
+  template <bool MIN>
+  __device__ static E pick(E a, E b) {
+    const auto x = Ty::wide(a);
+    const auto y = Ty::wide(b);
+    const bool pickA = (MIN ? (x < y) : (x > y)) | isNan(y);
     return pickA ? a : b;   // narrowing a widened value is exact: keep the bits
+  }
+  __device__ E red(E a, E b) const { return isMin ? pick<true>(a, b) : pick<false>(a, b); }
+  // the min/max choice is uniform: decided once per pack, never per element
+  // (written per element it compiled into divergent branches: 5.0 vs 6.3 TB/s
+  // at config B, profiles/r2/probe_dtypes_r3d.jsonl)
+  __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
+    PackU<E> x, y;
+    x.v = a;
+    y.v = b;
+    if (isMin) {
+#pragma unroll
+      for (int i = 0; i < (int)(16 / sizeof(E)); i++) x.e[i] = pick<true>(x.e[i], y.e[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < (int)(16 / sizeof(E)); i++) x.e[i] = pick<false>(x.e[i], y.e[i]);
+    }
+    return x.v;
   }
 };
 template <class Ty>
@@ -308,6 +333,7 @@ __device__ __forceinline__ u32x4 fp8PackMap2(u32x4 a, u32x4 b, Op op) {
 template <class Ty>
 struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
   static constexpr int kUnrollCap = 4;
+  static constexpr int kBigBlocksPerCU = 2;   // widen, op, narrow per element
   __device__ explicit FnSumF8(uint64_t) {}
   __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
@@ -317,6 +343,7 @@ struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
 template <class Ty>
 struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
   static constexpr int kUnrollCap = 4;
+  static constexpr int kBigBlocksPerCU = 2;   // widen, op, narrow per element
   __device__ explicit FnProdF8(uint64_t) {}
   __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) * Ty::wide(b)); }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
@@ -326,6 +353,7 @@ struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
 template <class Ty>
 struct FnPreMulSumF8 : FnBase<FnPreMulSumF8<Ty>, uint8_t> {
   static constexpr int kUnrollCap = 4;
+  static constexpr int kBigBlocksPerCU = 2;   // widen, op, narrow per element
   static constexpr bool kHasPre = true;
   float scalar;
   __device__ explicit FnPreMulSumF8(uint64_t arg) : scalar(Ty::wide((uint8_t)arg)) {}

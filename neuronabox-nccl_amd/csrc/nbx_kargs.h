@@ -115,6 +115,7 @@ struct KernelSet {
   const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]
   const void* batchList[kMaxKSrcs]; // batched buckets from a work-list table (kReduceBatchList), [nSrcs-1]
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source
+  int bigBlocksPerCU;               // Fn::kBigBlocksPerCU (at least this many big-tile workgroups per CU)
   int eltBytes;
   int valid;
 };

@@ -612,6 +612,7 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.ring = (const void*)&kRingAllReduce<Fn>;
   ks.ringFifo = (const void*)&kRingFifo<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
+  ks.bigBlocksPerCU = Fn::kBigBlocksPerCU;
   ks.valid = 1;
   return ks;
 }

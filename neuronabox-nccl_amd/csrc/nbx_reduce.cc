@@ -214,8 +214,11 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     const bool big = force == 2 || (force == 0 && (nSrcs > 3 || acquireSystem) && bigTiles >= (size_t)cus);
     const size_t tile = big ? bigTile : (size_t)kBlock;
     const size_t tiles = (nPacks + tile - 1) / tile;
-    const size_t maxBlocks =
-        (size_t)cus * (size_t)maxBlocksPerCU(big, nSrcs * (big ? ks.unroll[nSrcs - 1] : 1), acquireSystem != 0);
+    int perCU = maxBlocksPerCU(big, nSrcs * (big ? ks.unroll[nSrcs - 1] : 1), acquireSystem != 0);
+    static const bool envPerCU = envInt("NBX_BLOCKS_PER_CU", 0) > 0;
+    if (big && !envPerCU && g_maxBlocksPerCU.load(std::memory_order_relaxed) == 0 && perCU < ks.bigBlocksPerCU)
+      perCU = ks.bigBlocksPerCU;   // VALU-heavy functors: a second wave per SIMD
+    const size_t maxBlocks = (size_t)cus * (size_t)perCU;
     size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
     if (grid == 0) grid = 1;
     a.variant = big ? 1 : 0;
