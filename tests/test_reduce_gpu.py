@@ -517,7 +517,7 @@ def test_batch_work_list_and_kernarg_forms(nbx, oracle, torch_gpu, mode):
 
 def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
     """Work-list table slots: eager calls recycle them (with more calls in
-    flight than the arena's 64 slots the rest fall back to kernel-argument
+    flight than the arena's 128 slots the rest fall back to kernel-argument
     batches, never wait), a call captured into a graph keeps its slot for the
     graph's lifetime — eager calls issued between replays never overwrite it —
     and every replay reads it in place."""
@@ -552,11 +552,14 @@ def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
 
         host = fill(0)
         torch.cuda.synchronize()
+        fb0 = lib.nbxDebugBatchListSlots(dev_id, 3)
         with torch.cuda.stream(s):
-            for _ in range(150):   # > 64 slots in flight: the arena waits for the oldest
+            torch.cuda._sleep(200_000_000)   # hold the stream so the calls below pile up
+            for _ in range(300):   # > 128 slots in flight: the rest fall back to kernel-argument tables
                 nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
         s.synchronize()
         check(host)
+        assert lib.nbxDebugBatchListSlots(dev_id, 3) > fb0   # the fallback ran, and came out right
         with torch.cuda.stream(s):
             for _ in range(20):   # each eager call returns a few completed slots to the free pool
                 nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
