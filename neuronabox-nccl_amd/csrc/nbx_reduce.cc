@@ -224,7 +224,9 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     a.variant = big ? 1 : 0;
     // dynamic tiles for big tiles only: small tiles (1-3 sources, 3-5
     // workgroups per CU, 16x the atomics) collapse to 0.7-1.4 TB/s on the
-    // counter's contention (profiles/r2/probe_dyn_r2x.jsonl)
+    // counter's contention (profiles/r2/probe_dyn_r2x.jsonl), and fetching
+    // chunks of 4-16 consecutive small tiles per atomic still lost 15-60 % to
+    // the static grid stride (profiles/r2/probe_dyn_small_chunk_r3k.jsonl)
     DynLaunch dyn;
     if (big) dyn.begin(dev, stream, tiles, a);
     err = hipLaunchKernel((const void*)ks.packs[big ? 1 : 0][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args,
