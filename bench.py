@@ -555,7 +555,10 @@ def main():
         "pct_hbm_peak": round(100.0 * (ALG_BYTES / (wall / args.steps)) / (HBM_PEAK_GBS * 1e9), 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "kReducePacks<FnSumF<TyF32>, NSRC=8, U=4>", "kernel_avg_ms": round(kern_avg_ms, 5),
+                     "kernel": "kReducePacks<FnSumF<TyF32>, NSRC=8, U=4>",
+                     "tile_schedule": "static" if os.environ.get("NBX_DYNAMIC_TILES", "1") == "0"
+                     else "dynamic (per-stream tile counter)",
+                     "kernel_avg_ms": round(kern_avg_ms, 5),
                      "alg_bytes_per_launch": ALG_BYTES},
         "cpu_baseline": None,
         "collective": None,
