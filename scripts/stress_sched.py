@@ -18,11 +18,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--ops", type=int, default=600)
     ap.add_argument("--seed", type=int, default=1)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     import torch
     from __graft_entry__ import _load_package
     nbx = _load_package()
@@ -114,8 +114,8 @@ def main():
            "seconds": round(time.time() - t0, 1)}
     del graphs
     print(json.dumps(res), flush=True)
-    return 0 if bad == 0 else 1
+    return 0 if bad == 0 else 1, res
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main()[0])
