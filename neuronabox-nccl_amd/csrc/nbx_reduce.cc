@@ -112,6 +112,30 @@ int shiftedBlocksPerCU(bool perCount, int nSrcs) {
   return shiftLdsBlocksPerCU(nSrcs);
 }
 
+// The device a launch on `st` runs on (the per-device arenas and tile
+// counters must live there): the stream's own device, the current one for
+// the null / per-thread stream.
+int launchDevice(hipStream_t st) {
+  if (st != nullptr && st != hipStreamPerThread) {
+    hipDevice_t d = 0;
+    if (hipStreamGetDevice(st, &d) == hipSuccess) return (int)d;
+  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev;
+}
+
+// Makes `dev` current for an allocation, restoring the caller's device.
+struct CurDev {
+  int prev = -1;
+  explicit CurDev(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess || prev == dev || hipSetDevice(dev) != hipSuccess) prev = -1;
+  }
+  ~CurDev() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 bool isFloatType(int dt) {
   return dt == ncclFloat16 || dt == ncclFloat32 || dt == ncclFloat64 || dt == ncclBfloat16 ||
          dt == ncclFloat8e4m3 || dt == ncclFloat8e5m2;
@@ -193,8 +217,7 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
   for (int s = 1; s < nSrcs; s++) shared &= (((uintptr_t)srcs[s] & 15u) == mis);
   for (int d = 0; d < nDsts; d++) shared &= (((uintptr_t)dsts[d] & 15u) == mis);
 
-  int dev = 0;
-  (void)hipGetDevice(&dev);
+  const int dev = launchDevice(stream);
   const int cus = cuCount(dev);
   void* args[] = {&a};
   hipError_t err;
@@ -288,6 +311,7 @@ bool DynLaunch::begin(int dev, hipStream_t st, uint64_t nTiles, KArgs& a) {
   DynTiles& D = g_dyn[dev];
   lk_ = std::unique_lock<std::mutex>(D.mu);
   if (D.pool == nullptr) {
+    CurDev cur(dev);
     void* p = nullptr;
     if (D.failed || hipMalloc(&p, kDynCounters * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(p, 0, kDynCounters * sizeof(uint32_t)) != hipSuccess) {
@@ -647,10 +671,8 @@ struct BatchPacker {
     a.preMask = preMask;
     a.postOp = postOp;
     a.acquireSystem = acquireSystem;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
     const uint64_t maxBlocks =
-        (uint64_t)cuCount(dev) * (uint64_t)maxBlocksPerCU(false, nSrcs, acquireSystem != 0);
+        (uint64_t)cuCount(launchDevice(stream)) * (uint64_t)maxBlocksPerCU(false, nSrcs, acquireSystem != 0);
     const uint64_t grid = a.totalTiles < maxBlocks ? a.totalTiles : maxBlocks;
     void* args[] = {&a};
     hipError_t err = hipLaunchKernel(ks.batch[nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args, 0, stream);
@@ -698,6 +720,7 @@ ListArena g_lists[kMaxDevices];
 void releaseGraphSlot(void* p) { static_cast<std::atomic<int>*>(p)->store(0); }
 
 bool allocArena(ListArena& A, int dev) {
+  CurDev cur(dev);
   const size_t bytes = (size_t)kListSlots * kBatchListSlotBytes;
   int largeBar = 0;
   static const int want = envInt("NBX_BATCH_TABLE_DEVICE", 1);
@@ -829,8 +852,7 @@ ncclResult_t launchBatchList(const KernelSet& ks, int nSrcs, const std::vector<c
                              const nbxDevRedOpFull& op, uint32_t preMask, int postOp, int acq, hipStream_t st,
                              size_t* done) {
   *done = 0;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
+  const int dev = launchDevice(st);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   hipGraph_t graph = nullptr;
   if (hipStreamGetCaptureInfo_v2(st, &cs, nullptr, &graph, nullptr, nullptr) != hipSuccess) {
@@ -932,9 +954,7 @@ ncclResult_t reduceMultiBatchImpl(const nbxReduceTask* tasks, int nTasks, ncclDa
   // tile's higher rate; 1-3 sources use the batch kernel's tile shape anyway). Launch variant 1 (force small tiles) batches those too; variant 2
   // (force big tiles) batches nothing.
   const int force = g_variant.load(std::memory_order_relaxed);
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const uint64_t cus = (uint64_t)cuCount(dev);
+  const uint64_t cus = (uint64_t)cuCount(launchDevice(st));
   std::unique_ptr<BatchPacker> packers[kMaxKSrcs];
   std::vector<const nbxReduceTask*> lists[kMaxKSrcs];
   const bool useList = batchListEnabled();
