@@ -91,6 +91,12 @@ __device__ __forceinline__ void foldStore(const Fn& fn, const u32x4 (&v)[NSRC][U
   }
 }
 
+// Source-major issue order (all U packs of source 0, then source 1, ...). The
+// unroll-major order lets the fold start after the first NSRC loads land
+// (the compiler then waits vmcnt(31), (30), ... instead of near 0), which
+// should help the VALU-heavy functors — measured in-process it lost for every
+// dtype at the configs' shapes, fp8 included (f32 6235 -> 5979 GB/s, fp8 e4m3
+// 5704 -> 5668; profiles/r2/ab_load_order_r4b.jsonl).
 template <int NSRC, int U>
 __device__ __forceinline__ void loadTile(u32x4 (&v)[NSRC][U], const u32x4* const (&src)[NSRC], uint64_t p) {
 #pragma unroll
