@@ -76,6 +76,13 @@ int nbxDebugSetBatchMode(int mode);
  * -1 bad device. */
 int nbxDebugBatchListSlots(int device, int state);
 
+/* Dynamic tile scheduling threshold of the big-tile reduce kernel: launches
+ * with at least this many tiles per workgroup take tiles from the stream's
+ * counter, shorter ones run the static grid stride (default 16, env
+ * NBX_DYN_MIN_TILES_PER_WG; 1 makes every big-tile launch dynamic). Values < 1
+ * only query. Returns the threshold in force before the call. */
+int nbxDebugSetDynMinTiles(int tilesPerWorkgroup);
+
 #ifdef __cplusplus
 }
 #endif

@@ -192,6 +192,20 @@ struct DynTiles {
 };
 DynTiles g_dyn[kMaxDevices];
 
+// Tiles per workgroup from which a big-tile launch is dynamic (launchPass);
+// env NBX_DYN_MIN_TILES_PER_WG, nbxDebugSetDynMinTiles.
+std::atomic<int> g_dynMinTiles{0};
+int dynMinTilesPerWG() {
+  int v = g_dynMinTiles.load(std::memory_order_relaxed);
+  if (v < 1) {
+    const int e = envInt("NBX_DYN_MIN_TILES_PER_WG", 16);
+    int expect = v;
+    g_dynMinTiles.compare_exchange_strong(expect, e < 1 ? 1 : e);
+    v = g_dynMinTiles.load();
+  }
+  return v;
+}
+
 // One kernel pass over <= kMaxKSrcs sources.
 ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const void* const* srcs,
                         int nSrcs, size_t count, const nbxDevRedOpFull& op, uint32_t preMask,
@@ -249,9 +263,17 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     // workgroups per CU, 16x the atomics) collapse to 0.7-1.4 TB/s on the
     // counter's contention (profiles/r2/probe_dyn_r2x.jsonl), and fetching
     // chunks of 4-16 consecutive small tiles per atomic still lost 15-60 % to
-    // the static grid stride (profiles/r2/probe_dyn_small_chunk_r3k.jsonl)
+    // the static grid stride (profiles/r2/probe_dyn_small_chunk_r3k.jsonl).
+    // And only for launches of >= 16 tiles per workgroup: every workgroup's
+    // fetch goes to one address, and device-scope atomics on one address
+    // serialize (~11 ns each), so the launch's first and last round of
+    // fetches — one per workgroup, all at once — add ~3 us, which only long
+    // launches win back (8 x fp32 sources: 4 MiB per input 7.50 vs 4.71 us
+    // static, 16 MiB 27.4 vs 24.4 us, 64 MiB 97.4 vs 98.1, 256 MiB 376 vs 395;
+    // scripts/sweep_dyn_xcd.hip, profiles/r2/sweep_dyn_xcd_r4e.txt,
+    // profiles/r2/probe_mid_sizes_r4d.jsonl)
     DynLaunch dyn;
-    if (big) dyn.begin(dev, stream, tiles, a);
+    if (big && tiles >= (size_t)dynMinTilesPerWG() * grid) dyn.begin(dev, stream, tiles, a);
     err = hipLaunchKernel((const void*)ks.packs[big ? 1 : 0][nSrcs - 1], dim3((unsigned)grid), dim3(kBlock), args,
                           0, stream);
     dyn.done(err == hipSuccess);
@@ -1072,6 +1094,12 @@ __attribute__((visibility("default"))) int nbxDebugSetBatchMode(int mode) {
 
 __attribute__((visibility("default"))) int nbxDebugBatchListSlots(int device, int state) {
   return listSlotCount(device, state);
+}
+
+__attribute__((visibility("default"))) int nbxDebugSetDynMinTiles(int tilesPerWorkgroup) {
+  const int prev = dynMinTilesPerWG();
+  if (tilesPerWorkgroup >= 1) g_dynMinTiles.store(tilesPerWorkgroup);
+  return prev;
 }
 
 }  // extern "C"

@@ -22,11 +22,14 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--ops", type=int, default=600)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--dyn-min-tiles", type=int, default=0,
+                    help="nbxDebugSetDynMinTiles for the run (1: every big-tile launch dynamic; 0: library default)")
     args = ap.parse_args(argv)
     import torch
     from __graft_entry__ import _load_package
     nbx = _load_package()
     lib = nbx.load_library()
+    prev_dyn = lib.nbxDebugSetDynMinTiles(args.dyn_min_tiles if args.dyn_min_tiles > 0 else 0)
     torch.cuda.set_device(0)
     rng = random.Random(args.seed)
     streams = [torch.cuda.Stream() for _ in range(4)]
@@ -132,6 +135,8 @@ def main(argv=None):
            "list_fallbacks": lib.nbxDebugBatchListSlots(0, 3), "list_slots_graph_owned": lib.nbxDebugBatchListSlots(0, 2),
            "seconds": round(time.time() - t0, 1), "bad_cases": details[:8]}
     del graphs
+    lib.nbxDebugSetDynMinTiles(prev_dyn)
+    res["dyn_min_tiles"] = args.dyn_min_tiles
     print(json.dumps(res), flush=True)
     return 0 if bad == 0 else 1, res
 

@@ -785,7 +785,20 @@ def test_beyond_32bit_counts(nbx, torch_gpu):
     assert torch.equal(o, x + y)
 
 
-def test_dynamic_tiles_across_streams_and_graphs(nbx, oracle, torch_gpu):
+@pytest.fixture
+def dynamic_tiles_always(nbx):
+    """Every big-tile launch takes the dynamic schedule (by default only
+    launches of >= 16 tiles per workgroup do, nbxDebugSetDynMinTiles), so the
+    tests below exercise the counters at sizes the oracle checks quickly."""
+    lib = nbx.load_library()
+    lib.nbxDebugSetDynMinTiles.restype = ctypes.c_int
+    prev = lib.nbxDebugSetDynMinTiles(1)
+    assert prev >= 1
+    yield
+    lib.nbxDebugSetDynMinTiles(prev)
+
+
+def test_dynamic_tiles_across_streams_and_graphs(nbx, oracle, torch_gpu, dynamic_tiles_always):
     """Big-tile launches take their tiles from a per-stream counter whose
     per-launch base the host tracks (nbx_tiles.h): many launches of different
     sizes on three streams at once, a > 8-source multi-pass call, and a graph
@@ -839,7 +852,7 @@ def test_dynamic_tiles_across_streams_and_graphs(nbx, oracle, torch_gpu):
         assert_same(out.cpu().numpy(), exp, dtype)
 
 
-def test_dynamic_tiles_threads_sharing_a_stream(nbx, oracle, torch_gpu):
+def test_dynamic_tiles_threads_sharing_a_stream(nbx, oracle, torch_gpu, dynamic_tiles_always):
     """Host threads racing nbxReduceMulti calls onto ONE stream: each call
     reads its stream counter's base and launches under one lock, so bases stay
     in enqueue order and every call's tiles are its own (ctypes drops the GIL

@@ -19,7 +19,9 @@ def _stress_module():
     return mod
 
 
-@pytest.mark.parametrize("seed", [11, 12])
-def test_scheduling_stress(torch_gpu, seed):
-    rc, res = _stress_module().main(["--ops", "400", "--seed", str(seed)])
+@pytest.mark.parametrize("seed,dyn_min_tiles", [(11, 0), (12, 1)])
+def test_scheduling_stress(torch_gpu, seed, dyn_min_tiles):
+    """dyn_min_tiles 0: the library's default tile policy; 1: every big-tile
+    launch dynamic (the stress sizes are below the default threshold)."""
+    rc, res = _stress_module().main(["--ops", "400", "--seed", str(seed), "--dyn-min-tiles", str(dyn_min_tiles)])
     assert rc == 0 and res["mismatches"] == 0, res
