@@ -74,9 +74,11 @@ struct BatchArgs {
 // uploadWork / common.h:146-176), so one launch takes up to kListMaxRecs
 // buckets (and a call any number, in as many launches). The host writes the
 // table straight into uncached device memory through the large BAR (pinned
-// host memory where the BAR is small). Fixed-size records (kBatchRecWords
-// words, 16-B aligned): tileBegin, tileEnd, count | head << 56 | nDsts << 60,
-// 8 source slots, 8 destination slots. The records' running tile totals also
+// host memory where the BAR is small). Records of recWords = 3 + nSrcs +
+// (the launch's largest nDsts) words: tileBegin, tileEnd, count | head << 56 |
+// nDsts << 60, the sources, the destinations — at most kBatchRecWords; sized
+// to the launch because every record crosses PCIe (a 2-source bucket's is 48 B
+// instead of 160 B). The records' running tile totals also
 // travel in the kernel arguments (scalar-cache hits, fresh every launch):
 // workgroups take chunks of `chunk` consecutive tiles round-robin (chunk 1 =
 // grid stride, the whole GPU on one window of memory, as for one bucket), and
@@ -87,7 +89,7 @@ constexpr int kListMaxRecs = 384;
 constexpr int kBatchListSlotBytes = kListMaxRecs * kBatchRecWords * 8;   // one table per slot
 
 struct BatchListArgs {
-  const uint64_t* recs;      // kBatchRecWords words per bucket
+  const uint64_t* recs;      // recWords words per bucket
   uint64_t totalTiles;
   uint64_t arg;
   const void* argPtr;
@@ -96,7 +98,7 @@ struct BatchListArgs {
   int32_t acquireSystem;
   int32_t nRecs;
   uint32_t chunk;            // consecutive tiles per workgroup turn
-  uint32_t pad;
+  uint32_t recWords;         // words per record: 3 + nSrcs + max nDsts of the launch
   uint32_t tileEnd[kListMaxRecs];   // running tile totals (recs[k][1]); totals < 2^32
 };
 

@@ -528,7 +528,7 @@ __global__ __launch_bounds__(kBlock) void kReduceBatchList(BatchListArgs a) {
             break;
           }
         }
-        const uint64_t* r = a.recs + (uint64_t)k * kBatchRecWords;
+        const uint64_t* r = a.recs + (uint64_t)k * a.recWords;
         tBegin = r[0];
         tEnd = r[1];
         const uint64_t meta = r[2];
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(kBlock) void kReduceBatchList(BatchListArgs a) {
         }
 #pragma unroll
         for (int d = 0; d < kMaxKDsts; d++) {
-          db[d] = (E*)r[3 + kMaxKSrcs + (d < nDsts ? d : 0)];
+          db[d] = (E*)r[3 + NSRC + (d < nDsts ? d : 0)];
           dst[d] = (u32x4*)(db[d] + head);
         }
       }

@@ -897,8 +897,10 @@ ncclResult_t launchBatchList(const KernelSet& ks, int nSrcs, const std::vector<c
     // this launch's buckets: up to kListMaxRecs, running tile totals < 2^32
     size_t nRec = 0;
     uint64_t tiles = 0;
+    int maxD = 1;
     while (nRec < (size_t)kListMaxRecs && i + nRec < ts.size()) {
       const nbxReduceTask& t = *ts[i + nRec];
+      if (t.nDsts > maxD) maxD = t.nDsts;
       const unsigned mis = (unsigned)((uintptr_t)t.srcs[0] & 15u);
       uint64_t head = mis ? (uint64_t)((16u - mis) / (unsigned)eb) : 0;
       if (head > t.count) head = t.count;
@@ -913,31 +915,32 @@ ncclResult_t launchBatchList(const KernelSet& ks, int nSrcs, const std::vector<c
     const int slot = acquireListSlot(dev, capturing, &mem);
     if (slot < 0) return ncclSuccess;
     uint64_t* recs = (uint64_t*)mem;   // write-only: the slot may be device memory behind the BAR
+    const int recWords = 3 + nSrcs + maxD;   // <= kBatchRecWords
     for (size_t r = 0; r < nRec; r++) {
       const nbxReduceTask& t = *ts[i + r];
       const unsigned mis = (unsigned)((uintptr_t)t.srcs[0] & 15u);
       uint64_t head = mis ? (uint64_t)((16u - mis) / (unsigned)eb) : 0;
       if (head > t.count) head = t.count;
-      uint64_t* w = recs + r * kBatchRecWords;
+      uint64_t* w = recs + r * (size_t)recWords;
       w[0] = r ? a.tileEnd[r - 1] : 0;
       w[1] = a.tileEnd[r];
       w[2] = (uint64_t)t.count | head << 56 | (uint64_t)t.nDsts << 60;
-      for (int s = 0; s < kMaxKSrcs; s++) w[3 + s] = s < nSrcs ? (uint64_t)(uintptr_t)t.srcs[s] : 0;
-      for (int d = 0; d < kMaxKDsts; d++) w[3 + kMaxKSrcs + d] = d < t.nDsts ? (uint64_t)(uintptr_t)t.dsts[d] : 0;
+      for (int s = 0; s < nSrcs; s++) w[3 + s] = (uint64_t)(uintptr_t)t.srcs[s];
+      for (int d = 0; d < maxD; d++) w[3 + nSrcs + d] = d < t.nDsts ? (uint64_t)(uintptr_t)t.dsts[d] : 0;
     }
     const uint64_t chunks = (tiles + chunk - 1) / chunk;
     const uint64_t G = chunks < maxG ? chunks : maxG;
     a.recs = recs;
     a.nRecs = (int)nRec;
     a.chunk = (uint32_t)chunk;
-    a.pad = 0;
+    a.recWords = (uint32_t)recWords;
     a.totalTiles = tiles;
     a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
     a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
     a.preMask = preMask;
     a.postOp = postOp;
     a.acquireSystem = acq;
-    publishListSlot(dev, (const volatile uint32_t*)(recs + nRec * kBatchRecWords - 1));
+    publishListSlot(dev, (const volatile uint32_t*)(recs + nRec * (size_t)recWords - 1));
     void* args[] = {&a};
     const hipError_t err =
         hipLaunchKernel(ks.batchList[nSrcs - 1], dim3((unsigned)G), dim3(kBlock), args, 0, st);
