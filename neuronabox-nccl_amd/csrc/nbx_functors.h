@@ -172,9 +172,10 @@ struct FnBase {
   // cap on the big-tile unroll: VALU-heavy functors gain nothing from more
   // loads in flight and only grow code size
   static constexpr int kUnrollCap = 16;
-  // big-tile workgroups per CU (at least): VALU-heavy functors run two, so a
-  // second wave per SIMD has its loads in flight while the first folds
-  // (profiles/r2/probe_dtypes_r3f.jsonl)
+  // big-tile workgroups per CU (at least): VALU-heavy functors run more, so
+  // another wave per SIMD has its loads in flight while one folds — float
+  // min/max two, fp8 four (profiles/r2/probe_dtypes_r3f.jsonl; fp8 e4m3 sum
+  // 5.75 / 5.80 / 5.84 TB/s at 2 / 3 / 4, ab_blocks_per_cu_r4i.jsonl)
   static constexpr int kBigBlocksPerCU = 1;
   __device__ E pre(E a) const { return a; }
   __device__ E post(E a) const { return a; }
@@ -333,7 +334,7 @@ __device__ __forceinline__ u32x4 fp8PackMap2(u32x4 a, u32x4 b, Op op) {
 template <class Ty>
 struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
   static constexpr int kUnrollCap = 4;
-  static constexpr int kBigBlocksPerCU = 2;   // widen, op, narrow per element
+  static constexpr int kBigBlocksPerCU = 4;   // widen, op, narrow per element (profiles/r2/ab_blocks_per_cu_r4i.jsonl)
   __device__ explicit FnSumF8(uint64_t) {}
   __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) + Ty::wide(b)); }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
@@ -343,7 +344,7 @@ struct FnSumF8 : FnBase<FnSumF8<Ty>, uint8_t> {
 template <class Ty>
 struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
   static constexpr int kUnrollCap = 4;
-  static constexpr int kBigBlocksPerCU = 2;   // widen, op, narrow per element
+  static constexpr int kBigBlocksPerCU = 4;   // widen, op, narrow per element (profiles/r2/ab_blocks_per_cu_r4i.jsonl)
   __device__ explicit FnProdF8(uint64_t) {}
   __device__ uint8_t red(uint8_t a, uint8_t b) const { return Ty::narrow(Ty::wide(a) * Ty::wide(b)); }
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
@@ -353,7 +354,7 @@ struct FnProdF8 : FnBase<FnProdF8<Ty>, uint8_t> {
 template <class Ty>
 struct FnPreMulSumF8 : FnBase<FnPreMulSumF8<Ty>, uint8_t> {
   static constexpr int kUnrollCap = 4;
-  static constexpr int kBigBlocksPerCU = 2;   // widen, op, narrow per element
+  static constexpr int kBigBlocksPerCU = 4;   // widen, op, narrow per element (profiles/r2/ab_blocks_per_cu_r4i.jsonl)
   static constexpr bool kHasPre = true;
   float scalar;
   __device__ explicit FnPreMulSumF8(uint64_t arg) : scalar(Ty::wide((uint8_t)arg)) {}
