@@ -15,6 +15,10 @@ constexpr int kShiftLdsWaves = 4;
 constexpr int kShiftLdsStages = 2;
 constexpr int shiftLdsUnroll(int nSrcs) { return nSrcs >= 3 ? 2 : 1; }
 constexpr int shiftLdsBlocksPerCU(int nSrcs) { return nSrcs >= 3 ? 1 : 2; }
+// its dynamic schedule: wave tiles in kShiftDynClasses classes (t mod C), one
+// counter per class kShiftDynStride words apart (KArgs.dynCtr -> the first)
+constexpr int kShiftDynClasses = 32;
+constexpr int kShiftDynStride = 64;
 constexpr int kMaxKDsts = 8;     // destinations: NCCL_MAX_DIRECT_ARITY + 1 (device.h:147, all_reduce.h:343-360)
 
 struct KArgs {

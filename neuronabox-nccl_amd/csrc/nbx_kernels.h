@@ -349,21 +349,8 @@ __global__ __launch_bounds__(kShiftLdsWaves * 64) void kReduceShiftedLds(KArgs a
       }
     }
   };
-#pragma unroll
-  for (int k = 0; k < S - 1; k++) {
-    const uint64_t t = gw + (uint64_t)k * nWaves;
-    if (t < nTiles) issue(t, k);
-  }
-  int st = 0;
-  for (uint64_t t = gw; t < nTiles; t += nWaves) {
-    if (t + (uint64_t)(S - 1) * nWaves < nTiles) {
-      issue(t + (uint64_t)(S - 1) * nWaves, (st + S - 1) % S);
-      // everything but the newer tiles' DMA (NSRC x (U + 1) instructions each)
-      // has landed; stores counted in vmcnt only make the wait stricter
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * NSRC * (U + 1)) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  // fold wave tile t from stage st (its DMA has landed) and store it
+  auto foldTile = [&](uint64_t t, int st) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t q = t * kTile + (uint64_t)(u * 64 + lane);
@@ -390,7 +377,78 @@ __global__ __launch_bounds__(kShiftLdsWaves * 64) void kReduceShiftedLds(KArgs a
     }
     // this stage's LDS reads have returned before a later iteration refills it
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    st = st + 1 == S ? 0 : st + 1;
+  };
+  if (S != 2 || a.dynCtr == nullptr) {
+    // static schedule: wave gw takes tiles gw, gw + nWaves, ...
+#pragma unroll
+    for (int k = 0; k < S - 1; k++) {
+      const uint64_t t = gw + (uint64_t)k * nWaves;
+      if (t < nTiles) issue(t, k);
+    }
+    int st = 0;
+    for (uint64_t t = gw; t < nTiles; t += nWaves) {
+      if (t + (uint64_t)(S - 1) * nWaves < nTiles) {
+        issue(t + (uint64_t)(S - 1) * nWaves, (st + S - 1) % S);
+        // everything but the newer tiles' DMA (NSRC x (U + 1) instructions each)
+        // has landed; stores counted in vmcnt only make the wait stricter
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * NSRC * (U + 1)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      foldTile(t, st);
+      st = st + 1 == S ? 0 : st + 1;
+    }
+  } else {
+    // dynamic schedule (long eager launches): the wave tiles of class
+    // x = t mod C go to the waves of class x = gw mod C; each wave runs its
+    // first two tiles of the class statically (local indices l0 and l0 + gCls)
+    // and takes every further one from the class counter, one fetch per tile
+    // whose successor it runs, so the class's fetches number exactly
+    // F = nCls - gCls and the one that returns F - 1 is the last: its wave
+    // resets the counter to 0 for the next launch on this stream (no host
+    // base). The fetch for tile k + 2 is issued before tile k + 1's DMA, so
+    // the wait for tile k's DMA covers it and reading it never waits on
+    // tile k + 1's DMA.
+    constexpr uint64_t C = (uint64_t)kShiftDynClasses;
+    const uint64_t x = gw % C;
+    const uint64_t nCls = nTiles > x ? (nTiles - x + C - 1) / C : 0;
+    const uint64_t gCls = nWaves > x ? (nWaves - x + C - 1) / C : 0;
+    const uint64_t F = nCls > gCls ? nCls - gCls : 0;
+    uint32_t* ctr = a.dynCtr + x * (uint64_t)kShiftDynStride;
+    uint64_t lc = gw / C;
+    if (lc < nCls) {
+      uint64_t l1 = lc + gCls;
+      int st = 0;
+      issue(x + C * lc, 0);
+      for (;;) {
+        const bool more = l1 < nCls;
+        uint32_t pend = 0;
+        // the fetch as inline asm: the compiler would otherwise guard the
+        // read of its result with a conservative vmcnt(0) — waiting for the
+        // tile k + 1 DMA issued after it and undoing the two-stage pipeline;
+        // the explicit vmcnt below covers it (it is older than that DMA)
+        if (more && lane == 0)
+          asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(pend) : "v"(ctr), "v"(1u) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        uint64_t l2 = nCls;
+        if (more) {
+          issue(x + C * l1, st ^ 1);
+          // tile k's DMA and the fetch have landed (both older than tile k + 1's
+          // DMA); `pend` as an operand keeps its read after the wait
+          asm volatile("s_waitcnt vmcnt(%1)" : "+v"(pend) : "n"(NSRC * (U + 1)) : "memory");
+          const uint32_t g = __builtin_amdgcn_readfirstlane(pend);
+          if (lane == 0 && (uint64_t)g + 1 == F) atomicExch(ctr, 0u);
+          l2 = (uint64_t)g + 2 * gCls;
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        foldTile(x + C * lc, st);
+        st ^= 1;
+        if (!more) break;
+        lc = l1;
+        l1 = l2;
+      }
+    }
   }
   // head (before the destination's 128-B boundary) and tail elements
   if (blockIdx.x == gridDim.x - 1) {

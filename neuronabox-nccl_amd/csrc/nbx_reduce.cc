@@ -206,6 +206,53 @@ int dynMinTilesPerWG() {
   return v;
 }
 
+// Class counters of the realigning kernel's dynamic schedule: kShiftDynClasses
+// counters kShiftDynStride words apart per (device, stream). The kernel resets
+// each class counter on its last fetch, so a launch always starts from zero
+// and the host tracks no base; launches on one stream run in order, so no two
+// share a block at once. nullptr (static schedule) while the stream is being
+// captured (a captured launch may be replayed on any stream), for
+// hipStreamPerThread, with NBX_DYNAMIC_TILES=0 or once the pool is used up.
+constexpr int kShiftDynBlocks = 64;
+constexpr size_t kShiftDynBlockWords = (size_t)kShiftDynClasses * kShiftDynStride;
+struct ShiftDyn {
+  std::mutex mu;
+  uint32_t* pool = nullptr;
+  int used = 0;
+  bool failed = false;
+  std::unordered_map<hipStream_t, uint32_t*> block;
+};
+ShiftDyn g_shiftDyn[kMaxDevices];
+
+uint32_t* shiftDynCounters(int dev, hipStream_t st) {
+  static const int on = envInt("NBX_DYNAMIC_TILES", 1);
+  if (!on || dev < 0 || dev >= kMaxDevices || st == hipStreamPerThread) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  ShiftDyn& D = g_shiftDyn[dev];
+  std::lock_guard<std::mutex> lk(D.mu);
+  if (D.pool == nullptr) {
+    if (D.failed) return nullptr;
+    CurDev cur(dev);
+    void* p = nullptr;
+    const size_t bytes = (size_t)kShiftDynBlocks * kShiftDynBlockWords * sizeof(uint32_t);
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      D.failed = true;
+      return nullptr;
+    }
+    D.pool = (uint32_t*)p;
+  }
+  auto it = D.block.find(st);
+  if (it != D.block.end()) return it->second;
+  if (D.used >= kShiftDynBlocks) return nullptr;
+  uint32_t* b = D.pool + (size_t)D.used * kShiftDynBlockWords;
+  // zeroed in the stream's own order, ahead of its first launch
+  if (hipMemsetAsync(b, 0, kShiftDynBlockWords * sizeof(uint32_t), st) != hipSuccess) return nullptr;
+  D.used++;
+  D.block.emplace(st, b);
+  return b;
+}
+
 // One kernel pass over <= kMaxKSrcs sources.
 ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const void* const* srcs,
                         int nSrcs, size_t count, const nbxDevRedOpFull& op, uint32_t preMask,
@@ -302,9 +349,15 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
       const size_t maxBlocks = (size_t)cus * (size_t)shiftedBlocksPerCU(fn != nullptr, nSrcs);
       const size_t grid = blocks < maxBlocks ? blocks : maxBlocks;
       const unsigned threads = fn ? (unsigned)(kShiftLdsWaves * 64) : (unsigned)kBlock;
-      // static tiles: dynamic workgroup tiles (4 wave tiles) were measured
-      // at 1.1-4.9 TB/s here — 4-8x the big kernel's atomics on one counter
-      // (profiles/r2/realign_dyn_r3a.jsonl)
+      // dynamic schedule for long eager launches from 3 sources, over
+      // kShiftDynClasses class counters (kReduceShiftedLds): one counter for
+      // all workgroup tiles ran 1.1-4.9 TB/s here — 4-8x the big kernel's
+      // atomics on one address (profiles/r2/realign_dyn_r3a.jsonl). At 256 MiB
+      // per input the classes give 8 sources +4.7 %, 4 sources +1.1 % over
+      // the static stride; 2 sources (1-pack wave tiles, 2 workgroups per CU:
+      // 8x the fetches per byte) lost 28 % to the counters' contention, so
+      // they stay static (profiles/r2/realign_probe_r4q.jsonl)
+      if (fn && nSrcs >= 3 && blocks >= (size_t)dynMinTilesPerWG() * grid) a.dynCtr = shiftDynCounters(dev, stream);
       if (!fn) fn = ks.shifted;
       err = hipLaunchKernel(fn, dim3((unsigned)grid), dim3(threads), args, 0, stream);
     } else {
@@ -335,9 +388,7 @@ bool DynLaunch::begin(int dev, hipStream_t st, uint64_t nTiles, KArgs& a) {
   if (D.pool == nullptr) {
     CurDev cur(dev);
     void* p = nullptr;
-    if (D.failed || hipMalloc(&p, kDynCounters * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(p, 0, kDynCounters * sizeof(uint32_t)) != hipSuccess) {
-      if (p) (void)hipFree(p);
+    if (D.failed || hipMalloc(&p, kDynCounters * sizeof(uint32_t)) != hipSuccess) {
       D.failed = true;
       lk_.unlock();
       return false;
@@ -346,7 +397,10 @@ bool DynLaunch::begin(int dev, hipStream_t st, uint64_t nTiles, KArgs& a) {
   }
   auto it = D.next.find(st);
   if (it == D.next.end()) {
-    if (D.used >= kDynCounters) {
+    // a stream's counter is zeroed in that stream's own order, ahead of its
+    // first launch (a memset on the null stream would not order a
+    // non-blocking stream's kernel after it)
+    if (D.used >= kDynCounters || hipMemsetAsync(D.pool + D.used, 0, sizeof(uint32_t), st) != hipSuccess) {
       lk_.unlock();
       return false;
     }

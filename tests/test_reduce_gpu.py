@@ -204,6 +204,54 @@ def test_realigned_sources_grid_stride(nbx, oracle, torch_gpu, dtype, nsrc, coun
     run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, src_off=src_off, dst_off=[eb % 16])
 
 
+@pytest.mark.parametrize("dtype,nsrc,count", [(7, 8, 3_000_001), (7, 4, 2_097_155), (6, 5, 4_194_309),
+                                              (9, 3, 1_048_583), (10, 8, 8_388_617), (7, 2, 1_500_007),
+                                              (7, 8, 70_001), (7, 3, 5_003)])
+def test_realigned_sources_dynamic_schedule(nbx, oracle, torch_gpu, dynamic_tiles_always, dtype, nsrc, count):
+    """The realigning kernel's dynamic schedule (class counters, forced for
+    every launch here): many tiles per wave, and few (classes with fewer tiles
+    than waves, where every fetch is terminal)."""
+    eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+    srcs = oracle.random_inputs(dtype, nsrc, count, seed=nsrc * 11 + dtype + count % 97)
+    src_off = [(k * 3 * eb + eb) % 16 for k in range(nsrc)]
+    run_case(nbx, oracle, torch_gpu, srcs, dtype, 0, 0, src_off=src_off, dst_off=[0])
+
+
+def test_realigned_dynamic_back_to_back_and_streams(nbx, oracle, torch_gpu, dynamic_tiles_always):
+    """Class counters reset themselves on each class's last fetch: launches
+    of different sizes issued back to back on one stream (no host sync), and
+    on two streams at once, all come out exact — a counter left non-zero would
+    make the next launch skip tiles (its outputs keep the sentinel)."""
+    torch = torch_gpu
+    dtype, nsrc = 7, 8
+    lib = nbx.load_library()
+    cases = []
+    for k, n in enumerate([2_000_003, 9_001, 1_048_577, 3_000_017, 50_021]):
+        srcs = oracle.random_inputs(dtype, nsrc, n, seed=1200 + k)
+        exp = oracle.reduce_multi(srcs, dtype, 0, threads=8)[0]
+        # sources one element into their buffers, destination aligned: realigned
+        ts = [torch.from_numpy(np.concatenate([np.zeros(1, np.float32), x])).cuda() for x in srcs]
+        out = torch.full((n,), -7.0, dtype=torch.float32, device="cuda")
+        cases.append((ts, out, exp, n))
+    op = nbx.DevRedOpFull()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+
+    def call(ts, out, n, st):
+        sp = (ctypes.c_void_p * nsrc)(*[t.data_ptr() + 4 for t in ts])
+        dp = (ctypes.c_void_p * 1)(out.data_ptr())
+        assert lib.nbxReduceMulti(dp, 1, sp, nsrc, ctypes.c_size_t(n), dtype, op, 0, 0, ctypes.c_void_p(st)) == 0
+
+    for rep in range(3):
+        for k, (ts, out, exp, n) in enumerate(cases):   # back to back, alternating streams by case
+            call(ts, out, n, streams[(k + rep) % 2].cuda_stream)
+        torch.cuda.synchronize()
+        for ts, out, exp, n in cases:
+            assert_same(out.cpu().numpy(), exp, dtype)
+            out.fill_(-7.0)
+        torch.cuda.synchronize()
+
+
 def _hip():
     lib = ctypes.CDLL("libamdhip64.so")
     lib.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
