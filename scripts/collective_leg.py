@@ -116,12 +116,18 @@ def protocol_sweep(ids, rank, world, st, shared_gpu, res):
             idx = torch.arange(n, dtype=torch.int32, device="cuda")
             x = ((idx * 5 + 3 * rank) % 512).to(torch.float32)
             want = sum(((idx * 5 + 3 * r) % 512).to(torch.float32) for r in range(world))
-            y = torch.empty_like(x)
+            y = torch.full_like(x, -1.0)   # sentinel: an element nobody wrote stays -1
             c.all_reduce(x.data_ptr(), y.data_ptr(), n, 7, 0, st)
             torch.cuda.synchronize()
             if not torch.equal(y, want):
                 res["ok"] = False
-                res["errors"].append(f"sweep {name} {b} B: output differs")
+                bad = (y != want).nonzero().flatten()
+                i0, i1 = int(bad[0]), int(bad[-1])
+                own = ((idx * 5 + 3 * rank) % 512).to(torch.float32)
+                res["errors"].append(
+                    f"sweep {name} {b} B: output differs at {bad.numel()} of {n} elements [{i0}, {i1}] "
+                    f"(got {float(y[i0])} want {float(want[i0])}; unwritten {int((y[bad] == -1.0).sum())}, "
+                    f"equal to this rank's input {int((y[bad] == own[bad]).sum())})")
             iters = 50 if b <= (1 << 20) else 20
             for _ in range(5):
                 c.all_reduce(x.data_ptr(), y.data_ptr(), n, 7, 0, st)
