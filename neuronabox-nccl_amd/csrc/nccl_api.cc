@@ -1356,7 +1356,21 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
   NCCLCHECK(mpEvictMappings(mp, all[me].seq, capturing));
   std::vector<const char*> sendP;
   std::vector<char*> recvP;
+  const size_t mapsBefore = mp->maps.size();
   NCCLCHECK(mpMapCall(comm, c, all, capturing, &sendP, &recvP));
+  if (traceOn()) {   // NBX_TRACE=1: every rank's send / recv as this rank sees them
+    auto hsh = [](const hipIpcMemHandle_t& h) {
+      uint64_t x = 1469598103934665603ull;
+      for (size_t i = 0; i < sizeof(h); i++) x = (x ^ (unsigned char)((const char*)&h)[i]) * 1099511628211ull;
+      return x;
+    };
+    for (int j = 0; j < n; j++)
+      NBX_TRACE("mp simple seq=%llu rank %d count=%zu: rank %d send %p (h %016llx off %llu) recv %p (h %016llx off %llu)%s",
+                (unsigned long long)all[me].seq, me, c.count, j, (const void*)sendP[j],
+                (unsigned long long)hsh(all[j].sendH), (unsigned long long)all[j].sendOff, (void*)recvP[j],
+                (unsigned long long)hsh(all[j].recvH), (unsigned long long)all[j].recvOff,
+                mp->maps.size() != mapsBefore ? " [new mapping]" : "");
+  }
   // 1. every rank's stream has reached the collective (its inputs are written,
   //    its output may be written by peers)
   NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
