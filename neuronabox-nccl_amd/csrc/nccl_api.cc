@@ -89,6 +89,13 @@ void warn(const char* fmt, ...) {
   if (debugLevel() >= 2) std::fprintf(stderr, "NCCL WARN %s\n", buf);
 }
 
+// NBX_IPC_MAP_SYNC=0 skips the device synchronization after a new peer
+// mapping (mpRunSimple; A/B of the first-use failure only).
+bool noMapSync() {
+  static bool off = [] { const char* v = std::getenv("NBX_IPC_MAP_SYNC"); return v && std::strcmp(v, "0") == 0; }();
+  return off;
+}
+
 bool traceOn() {
   static bool on = [] { const char* v = std::getenv("NBX_TRACE"); return v && *v && *v != '0'; }();
   return on;
@@ -1358,6 +1365,13 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
   std::vector<char*> recvP;
   const size_t mapsBefore = mp->maps.size();
   NCCLCHECK(mpMapCall(comm, c, all, capturing, &sendP, &recvP));
+  // A mapping opened by this call: let the device settle before the first
+  // kernel touches it. Without this, the first call through a fresh mapping
+  // sometimes read zeros / garbage from the peer's buffer and its stores to
+  // it vanished (bench N = 2 rehearsals, 5 of 16; every later call through the
+  // same mapping was exact) — the behaviour of a page-table entry the GPU does
+  // not see yet. New mappings come once per peer buffer.
+  if (mp->maps.size() != mapsBefore && !capturing && !noMapSync()) HIPCHECK(hipDeviceSynchronize());
   if (traceOn()) {   // NBX_TRACE=1: every rank's send / recv as this rank sees them
     auto hsh = [](const hipIpcMemHandle_t& h) {
       uint64_t x = 1469598103934665603ull;
