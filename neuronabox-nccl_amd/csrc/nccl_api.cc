@@ -89,13 +89,6 @@ void warn(const char* fmt, ...) {
   if (debugLevel() >= 2) std::fprintf(stderr, "NCCL WARN %s\n", buf);
 }
 
-// NBX_IPC_MAP_SYNC=0 skips the device synchronization after a new peer
-// mapping (mpRunSimple; A/B of the first-use failure only).
-bool noMapSync() {
-  static bool off = [] { const char* v = std::getenv("NBX_IPC_MAP_SYNC"); return v && std::strcmp(v, "0") == 0; }();
-  return off;
-}
-
 bool traceOn() {
   static bool on = [] { const char* v = std::getenv("NBX_TRACE"); return v && *v && *v != '0'; }();
   return on;
@@ -853,6 +846,29 @@ ncclResult_t mpSetupShmx(ncclComm* c, const ncclUniqueId& id) {
   return ncclSuccess;
 }
 
+// Closing a peer-buffer mapping frees its virtual range, and the next import
+// in this process can land at the same address. A call through such a
+// reused address read zeros / garbage from the peer's buffer and its stores
+// to it vanished (bench N = 2 rehearsals: 8 of 22 runs, always the first call
+// through a new mapping whose address an earlier, closed mapping had used —
+// a stale translation for the old mapping). Retired mappings are
+// therefore kept open, up to NBX_IPC_RETIRED_MAX (4096) process-wide, oldest
+// closed first, so addresses are not reused while their translations may be live.
+void retirePeerMapping(void* base) {
+  static std::mutex mu;
+  static std::deque<void*> retired;
+  static const size_t maxRetired = [] {
+    const char* v = std::getenv("NBX_IPC_RETIRED_MAX");
+    return (v && *v) ? (size_t)std::strtoull(v, nullptr, 10) : (size_t)4096;
+  }();
+  std::lock_guard<std::mutex> g(mu);
+  retired.push_back(base);
+  while (retired.size() > maxRetired) {
+    (void)hipIpcCloseMemHandle(retired.front());
+    retired.pop_front();
+  }
+}
+
 ncclResult_t ipcHandleOf(const void* p, hipIpcMemHandle_t* h, uint64_t* off) {
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
@@ -1127,7 +1143,7 @@ void mpFree(ncclComm* c) {
   if (!mp) return;
   DevGuard g(c->device);
   (void)hipDeviceSynchronize();
-  for (auto& kv : mp->maps) (void)hipIpcCloseMemHandle(kv.second.base);
+  for (auto& kv : mp->maps) retirePeerMapping(kv.second.base);
   for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : mp->peerL128Maps) (void)hipIpcCloseMemHandle(p);
@@ -1264,7 +1280,7 @@ ncclResult_t mpEvictMappings(MpState* mp, uint64_t seq, bool capturing) {
   HIPCHECK(hipDeviceSynchronize());
   for (auto it = mp->maps.begin(); it != mp->maps.end();) {
     if (it->second.lastUse != MpState::kPinned && it->second.lastUse + 1 < seq) {
-      (void)hipIpcCloseMemHandle(it->second.base);
+      retirePeerMapping(it->second.base);
       it = mp->maps.erase(it);
     } else {
       ++it;
@@ -1365,13 +1381,6 @@ ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCa
   std::vector<char*> recvP;
   const size_t mapsBefore = mp->maps.size();
   NCCLCHECK(mpMapCall(comm, c, all, capturing, &sendP, &recvP));
-  // A mapping opened by this call: let the device settle before the first
-  // kernel touches it. Without this, the first call through a fresh mapping
-  // sometimes read zeros / garbage from the peer's buffer and its stores to
-  // it vanished (bench N = 2 rehearsals, 5 of 16; every later call through the
-  // same mapping was exact) — the behaviour of a page-table entry the GPU does
-  // not see yet. New mappings come once per peer buffer.
-  if (mp->maps.size() != mapsBefore && !capturing && !noMapSync()) HIPCHECK(hipDeviceSynchronize());
   if (traceOn()) {   // NBX_TRACE=1: every rank's send / recv as this rank sees them
     auto hsh = [](const hipIpcMemHandle_t& h) {
       uint64_t x = 1469598103934665603ull;
