@@ -18,13 +18,6 @@ extern "C" {
  * that multi-process ncclCommInitRank uses (the role of src/bootstrap.cc). */
 ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds);
 
-/* Attaches rank `rank` of `nranks` to the shared-memory exchange segment
- * `name` (rank 0 creates it; the caller removes it with shm_unlink) and runs
- * `rounds` exchanges of rank-stamped payloads of varying length, each rank
- * sleeping up to `jitterUs` microseconds before each, verifying every
- * contribution. Exercises the Simple path's per-call host exchange. */
-ncclResult_t nbxShmxSelfTest(const char* name, int rank, int nranks, int rounds, int jitterUs);
-
 /* NCCL_PROTO parsing (tuning.cc:254-259 list syntax: "LL,LL128", "^Simple",
  * case-insensitive; NULL or "" = all): bit 0 LL, bit 1 LL128, bit 2 Simple. */
 int nbxDebugProtoMask(const char* ncclProto);

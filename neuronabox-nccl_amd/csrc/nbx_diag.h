@@ -23,6 +23,10 @@ enum DiagSite : uint64_t {
   kDiagLL128AG = 5,      // LL128 two-shot: an all-gather sub-slot line
   kDiagRing = 6,         // pipelined ring: the left neighbour's progress word
   kDiagBarrier = 7,      // phase barrier: a peer's flag
+  kDiagSimpleRs = 8,     // Simple: a peer's RS-region slice (rsReady)
+  kDiagSimpleRsCredit = 9,   // Simple: a peer's credit for this rank's RS slot (rsCredit)
+  kDiagSimpleAg = 10,    // Simple: a peer's AG-region slice (agReady)
+  kDiagSimpleAgCredit = 11,  // Simple: a peer's credit for this rank's AG slot (agCredit)
 };
 constexpr int kDiagWords = 6;
 constexpr int kDiagByteOffset = 16;   // from the start of the host words
@@ -36,6 +40,10 @@ inline const char* diagSiteName(uint64_t s) {
     case kDiagLL128AG: return "LL128 two-shot all-gather line flag";
     case kDiagRing: return "ring progress word";
     case kDiagBarrier: return "phase barrier flag";
+    case kDiagSimpleRs: return "Simple reduce-scatter slice (peer's ready word)";
+    case kDiagSimpleRsCredit: return "Simple reduce-scatter slot credit";
+    case kDiagSimpleAg: return "Simple all-gather slice (peer's ready word)";
+    case kDiagSimpleAgCredit: return "Simple all-gather slot credit";
     default: return "unknown";
   }
 }

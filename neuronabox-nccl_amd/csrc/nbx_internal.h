@@ -26,8 +26,7 @@ class DynLaunch {
   uint64_t tiles_ = 0;
 };
 struct LLArgs;
-struct RingArgs;
-struct RingFifoArgs;
+struct SimpleArgs;
 // nbxReduceMulti with internal flags: kReduceAcquireSystem makes every
 // workgroup issue a system-scope acquire before its first load (sources in
 // peer GPU memory, written before the launch and ordered by a flag barrier).
@@ -43,12 +42,10 @@ ncclResult_t reduceMultiBatchEx(const nbxReduceTask* tasks, int nTasks, ncclData
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
 // The same for the LL128 kernel (args.nLines 64-byte lines).
 ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, hipStream_t stream);
-// Pipelined ring AllReduce (nbx_ring.h), `grid` workgroups = slices per chunk.
-ncclResult_t launchRingAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, RingArgs& args, unsigned grid,
-                                 hipStream_t stream);
-// Step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h kRingFifo).
-ncclResult_t launchRingFifo(ncclDataType_t dt, const nbxDevRedOpFull& op, RingFifoArgs& args, unsigned grid,
-                            hipStream_t stream);
+// Simple protocol collective (nbx_simple.h): the direct schedule, or the ring
+// schedule when `ring`; `grid` workgroups (<= args.gridMax).
+ncclResult_t launchSimple(ncclDataType_t dt, const nbxDevRedOpFull& op, SimpleArgs& args, unsigned grid, bool ring,
+                          hipStream_t stream);
 // LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
                                    hipStream_t stream);

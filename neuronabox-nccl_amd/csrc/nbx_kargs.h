@@ -116,8 +116,8 @@ struct KernelSet {
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)
-  const void* ring;                 // pipelined ring AllReduce (nbx_ring.h)
-  const void* ringFifo;             // step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h)
+  const void* simple;               // Simple protocol, direct schedule over init-mapped staging (nbx_simple.h)
+  const void* simpleRing;           // Simple protocol, ring schedule over init-mapped staging (nbx_simple.h)
   const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]
   const void* batchList[kMaxKSrcs]; // batched buckets from a work-list table (kReduceBatchList), [nSrcs-1]
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source

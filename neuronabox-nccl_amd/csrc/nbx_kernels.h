@@ -626,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void kReduceBatchList(BatchListArgs a) {
 
 }  // namespace nbx
 
-#include "nbx_ring.h"   // uses foldStore / ldPack above
+#include "nbx_simple.h"   // uses ldPack / stPack above
 
 namespace nbx {
 
@@ -673,8 +673,8 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.ll = (const void*)&kLLColl<Fn>;
   ks.ll128 = (const void*)&kLL128Coll<Fn>;
   ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;
-  ks.ring = (const void*)&kRingAllReduce<Fn>;
-  ks.ringFifo = (const void*)&kRingFifo<Fn>;
+  ks.simple = (const void*)&kSimpleColl<Fn>;
+  ks.simpleRing = (const void*)&kSimpleRing<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.bigBlocksPerCU = Fn::kBigBlocksPerCU;
   ks.valid = 1;

@@ -52,42 +52,44 @@ struct LLArgs {
   int32_t root;            // kLLReduce
 };
 
-constexpr int kRingMaxGrid = 256;   // slices per chunk = workgroups; one progress word each
+// ---------------------------------------------------------------------------
+// Simple protocol over init-mapped staging (nbx_simple.h). Peers never touch
+// the caller's buffers: each rank owns an uncached staging area and a set of
+// uncached flag words, allocated and IPC-mapped by every peer ONCE, at
+// ncclCommInitRank (the p2pMap / p2pSendConnect step of the reference,
+// transport/p2p.cc:290-330,450-520). A rank's kernels move data between its
+// own user buffers and staging; peer traffic is stores into the peer's
+// staging plus flag words (waitPeer / postPeer of prims_simple.h:129-185).
+//   staging  [region 2: RS | AG][slot][source rank n][workgroup gridMax][stageSlice bytes]
+//   flags    [kind 4][peer n][workgroup gridMax] u64      (written by the peer)
+//   counters [kind 4][peer n][workgroup gridMax] u64      (this rank's, device-resident)
+// Counter / flag kinds per (ordered pair, workgroup), monotonic over the
+// communicator's life, so producer and consumer agree without the host:
+//   rsSent  / flag rsReady  : RS-region slices this rank pushed to the peer / the peer pushed here
+//   rsRecv  / flag rsCredit : RS-region slices this rank consumed from the peer / the peer consumed from here
+//   agSent  / flag agReady  : the same for the AG region
+//   agRecv  / flag agCredit
+enum SimpleMode : int32_t { kSimpleAllReduce = 0, kSimpleReduceScatter = 1, kSimpleReduce = 2 };
+enum SimpleAlgo : int32_t { kSimpleAlgoDirect = 0, kSimpleAlgoRing = 1 };
+// flag words (written by the peer named by their index)
+enum SimpleFlag : int32_t { kFlRsReady = 0, kFlRsCredit = 1, kFlAgReady = 2, kFlAgCredit = 3 };
+// this rank's counters (per peer, per workgroup)
+enum SimpleCounter : int32_t { kCtRsSent = 0, kCtRsRecv = 1, kCtAgSent = 2, kCtAgRecv = 3 };
+constexpr int kSimpleMaxGrid = 256;
+constexpr int kSimpleMaxRanks = 64;
+constexpr int kSimpleMinSliceBytes = 4096;   // a call uses at most ceil(block / 4 KiB) workgroups
 
-// Pipelined ring AllReduce (nbx_ring.h kRingAllReduce): device-resident
-// sequencing, as LLState. The step-FIFO kernels (kRingFifo) keep, per
-// workgroup, how many FIFO entries this rank has produced and consumed over
-// all calls — every rank counts the same calls, so producer and consumer
-// agree without the host passing values (graph replays included).
-struct RingState {
-  uint64_t seq;      // completed ring calls
-  uint64_t arrive;   // workgroups of the running launch that have finished
-  uint64_t produced[kRingMaxGrid];   // kRingFifo: entries written into this rank's FIFO, per workgroup
-  uint64_t consumed[kRingMaxGrid];   // kRingFifo: entries of the left neighbour's FIFO read, per workgroup
-};
-
-// Step-FIFO ring ReduceScatter / chain Reduce (nbx_ring.h kRingFifo): NCCL's
-// Simple-protocol FIFO (prims_simple.h:129-185: the receiver waits on the
-// sender's tail, the sender on the receiver's head credit) with the FIFO in
-// the producer's HBM, read in place by the right neighbour over xGMI.
-enum RingFifoMode : int32_t { kRingFifoReduceScatter = 0, kRingFifoReduce = 1 };
-constexpr int kRingFifoSlots = 4;          // entries in flight per workgroup (NCCL_STEPS analogue)
-constexpr int kRingFifoEntryPacks = 2048;  // 16-B packs per entry: 32 KiB per workgroup per step
-constexpr uint64_t kRingFifoBytes = (uint64_t)kRingMaxGrid * kRingFifoSlots * kRingFifoEntryPacks * 16;
-
-struct RingFifoArgs {
-  const void* sendMe;     // this rank's input
-  const void* sendLeft;   // the left neighbour's input (peer mapping): the chain's first hop reads it raw
-  void* recv;             // RS: this rank's block; Reduce: the root's output (root only)
-  void* fifoMe;           // this rank's FIFO [kRingMaxGrid][kRingFifoSlots][kRingFifoEntryPacks] packs
-  const void* fifoLeft;   // the left neighbour's FIFO (peer mapping)
-  uint64_t* myTail;       // [kRingMaxGrid] entries the left neighbour has produced (it posts here; uncached)
-  uint64_t* rightTail;    // the right neighbour's tail words (peer mapping): this rank posts there
-  uint64_t* myHead;       // [kRingMaxGrid] entries of this rank's FIFO the right neighbour has consumed
-  uint64_t* leftHead;     // the left neighbour's head words (peer mapping): this rank posts there
-  RingState* state;
-  uint64_t blockElts;     // RS: recvcount (a whole number of 16-B packs); Reduce: count
-  uint64_t slicePacks;    // 16-B packs per workgroup slice of a block (Reduce: of the message)
+struct SimpleArgs {
+  const void* send;
+  void* recv;                  // nullptr on Reduce non-roots
+  char* const* peerStage;      // device table [n]: rank -> staging base (own entry: own staging)
+  uint64_t* const* peerFlags;  // device table [n]: rank -> flag words (own entry: own flags)
+  uint64_t* counters;          // this rank's [4][n][gridMax]
+  uint64_t total;              // elements of the message (ReduceScatter: recvcount * n)
+  uint64_t blockElts;          // elements per block: AllReduce/Reduce direct = blockRange, RS = recvcount, ring Reduce = count
+  uint64_t sliceBytes;         // bytes per (workgroup, block, round) of this call (multiple of 16)
+  uint64_t nRounds;
+  uint64_t stageSlice;         // staging bytes per (region, slot, source, workgroup)
   uint64_t arg;
   const void* argPtr;
   const volatile int* abortWord;
@@ -95,31 +97,10 @@ struct RingFifoArgs {
   uint64_t timeoutTicks;
   int32_t rank;
   int32_t nRanks;
-  int32_t root;           // Reduce
-  int32_t mode;           // RingFifoMode
-};
-
-struct RingArgs {
-  const void* sendMe;     // this rank's input
-  const void* sendLeft;   // the left neighbour's input (peer mapping): step 0 reads it raw
-  void* recvMe;           // this rank's output: partials of steps 0..n-3 live here
-  const void* recvLeft;   // the left neighbour's output (peer mapping): its partials
-  void* outs[8];          // last step: rank (me + k) % n's output for k < nOuts (push-gather)
-  uint64_t* myProgress;   // [kRingMaxGrid] words the LEFT neighbour posts (uncached, this rank's memory)
-  uint64_t* rightProgress;// the right neighbour's words (peer mapping): this rank posts there
-  RingState* state;
-  uint64_t total;         // elements of the message
-  uint64_t blockElts;     // direct-schedule block (multiple of 16 B / element)
-  uint64_t slicePacks;    // 16-B packs per slice (one slice per workgroup per chunk)
-  uint64_t arg;
-  const void* argPtr;
-  const volatile int* abortWord;
-  volatile int* errWord;
-  uint64_t timeoutTicks;
-  int32_t rank;
-  int32_t nRanks;
-  int32_t nOuts;          // 1: own output only (gather follows), n: push to every rank
-  int32_t pad;
+  int32_t mode;                // SimpleMode
+  int32_t root;
+  int32_t slots;               // staging slots per (region, source, workgroup), >= 2
+  int32_t gridMax;
 };
 
 }  // namespace nbx

@@ -68,13 +68,13 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugLL128TearTest(int 
   int rc = -1;
   if (hipExtMallocWithFlags((void**)&line, 64, hipDeviceMallocUncached) != hipSuccess) return -1;
   if (hipMalloc((void**)&pay, kL128DataBytes) == hipSuccess && hipMalloc((void**)&out, kL128DataBytes) == hipSuccess &&
-      hipMalloc((void**)&stamp, 16) == hipSuccess && hipMalloc((void**)&words, 8) == hipSuccess &&
+      hipMalloc((void**)&stamp, 16) == hipSuccess && hipMalloc((void**)&words, 64) == hipSuccess &&
       hipStreamCreateWithFlags(&sr, hipStreamNonBlocking) == hipSuccess &&
       hipStreamCreateWithFlags(&sw, hipStreamNonBlocking) == hipSuccess &&
       hipMemcpy(line, hLine, 64, hipMemcpyHostToDevice) == hipSuccess &&
       hipMemcpy(pay, hPay, kL128DataBytes, hipMemcpyHostToDevice) == hipSuccess &&
       hipMemset(out, 0, kL128DataBytes) == hipSuccess && hipMemset(stamp, 0, 16) == hipSuccess &&
-      hipMemset(words, 0, 8) == hipSuccess) {
+      hipMemset(words, 0, 64) == hipSuccess) {   // the host-words layout: a timeout's diag record lands at bytes 16-63
     LLArgs a{};
     a.myL128 = line;
     a.l128Bytes = 64;

@@ -468,28 +468,18 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   return ncclSuccess;
 }
 
-ncclResult_t launchRingAllReduce(ncclDataType_t dt, const nbxDevRedOpFull& op, RingArgs& a, unsigned grid,
-                                 hipStream_t stream) {
+ncclResult_t launchSimple(ncclDataType_t dt, const nbxDevRedOpFull& op, SimpleArgs& a, unsigned grid, bool ring,
+                          hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
-  if (!ks.valid || ks.ring == nullptr || grid < 1 || grid > (unsigned)kRingMaxGrid) return ncclInvalidArgument;
+  const void* k = ring ? ks.simpleRing : ks.simple;
+  if (!ks.valid || k == nullptr || grid < 1 || grid > (unsigned)a.gridMax || a.gridMax > kSimpleMaxGrid ||
+      a.nRanks < 2 || a.nRanks > kSimpleMaxRanks)
+    return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
   void* args[] = {&a};
-  hipError_t e = hipLaunchKernel(ks.ring, dim3(grid), dim3(kBlock), args, 0, stream);
-  if (e != hipSuccess) return ncclUnhandledCudaError;
-  return ncclSuccess;
-}
-
-ncclResult_t launchRingFifo(ncclDataType_t dt, const nbxDevRedOpFull& op, RingFifoArgs& a, unsigned grid,
-                            hipStream_t stream) {
-  if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
-  const KernelSet& ks = table()[(int)dt][op.op];
-  if (!ks.valid || ks.ringFifo == nullptr || grid < 1 || grid > (unsigned)kRingMaxGrid) return ncclInvalidArgument;
-  a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
-  a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
-  void* args[] = {&a};
-  hipError_t e = hipLaunchKernel(ks.ringFifo, dim3(grid), dim3(kBlock), args, 0, stream);
+  hipError_t e = hipLaunchKernel(k, dim3(grid), dim3(kBlock), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
   return ncclSuccess;
 }

@@ -1,0 +1,450 @@
+// nbx_simple.h — Simple protocol of the multi-process communicator: the
+// direct schedule (kSimpleColl) and the ring schedule (kSimpleRing), one
+// kernel per collective, flow control inside the kernel, peer data only
+// through staging that every peer mapped once at ncclCommInitRank.
+//
+// Reference: the Simple protocol's step FIFO (prims_simple.h:129-185:
+// waitPeer spins on the peer's tail / head, postPeer publishes after a
+// system fence), driven by runRing (all_reduce.h:13-95, reduce_scatter.h:13-66,
+// reduce.h:12-68) with connection buffers set up once (transport/p2p.cc:
+// 290-330 p2pMap, 450-520 p2pSendConnect / p2pRecvConnect). Peers see only
+// connection buffers; user pointers change every call (prims_simple.h:234-235).
+//
+// MI355X shape (layouts in nbx_ll_args.h SimpleArgs):
+//   * staging and flag words are uncached device memory (MTYPE UC): a peer's
+//     stores over xGMI land in HBM and no XCD L2 holds a stale copy. The
+//     caller's coarse-grained buffers are only ever touched by their own
+//     process's kernels, so dispatch-boundary coherence is all they need
+//     (round 2 read and wrote peers' user buffers through IPC mappings, and
+//     ranks sharing a GPU saw stale bytes and lost stores: tests/
+//     test_multiprocess_churn_gpu.py reproduces that deterministically);
+//   * the message is cut into n blocks (rank b owns block b); every block is
+//     cut into rounds of gridDim.x slices, workgroup g owns slice g of every
+//     block in every round, and waits only on workgroup g of its peers — no
+//     grid-wide barrier, skew between slices is absorbed by `slots` staging
+//     slots per (region, source, workgroup);
+//   * direct, per round (AllReduce): A. push slice g of block j into rank j's
+//     RS region (all n-1 peers, remote stores); B. fold block `me` from the
+//     local input and the n-1 RS slots in the order me+1, ..., me (PreOp on
+//     every source, PostOp at the end — the order NCCL's ring accumulates
+//     block me), store into the output and push it into every peer's AG
+//     region; C. copy the peers' AG slots into the output. Per rank 2(n-1)/n
+//     of the message crosses xGMI each way, like a ring, in three hops and on
+//     all n-1 links at once. ReduceScatter stops after B; Reduce pushes only
+//     to the root, which alone gathers; its fold order is root+1, ..., root;
+//   * ring, per round: the reference's ring schedule hop for hop through the
+//     right neighbour's staging (RS region: partials, AG region: finished
+//     chunks), each hop Fn(pre(local), received) (recvReduceSend's operand
+//     order; PreOp on the received raw input only at the first hop).
+// Every wait is bounded (timeout without progress, abort word) and records
+// what it waited for (nbx_diag.h).
+// Included by nbx_kernels.h after ldPack / stPack.
+#pragma once
+#include "nbx_diag.h"
+#include "nbx_functors.h"
+#include "nbx_kargs.h"
+#include "nbx_ll_args.h"
+
+namespace nbx {
+
+// Bounded spin until *w >= target (a peer's flag word); false on timeout
+// (timeoutTicks without the word reaching target) or abort.
+__device__ __forceinline__ bool simpleWait(const uint64_t* w, uint64_t target, const SimpleArgs& a, int peer,
+                                           uint64_t site) {
+  const uint64_t t0 = wall_clock64();
+  uint32_t spins = 0;
+  for (;;) {
+    const uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v >= target) return true;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255u) == 0u && (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks)) {
+      const bool aborted = *a.abortWord != 0;
+      if (!aborted) diagTimeout(a.errWord, site, peer, target, v, wall_clock64() - t0);
+      *a.errWord = aborted ? 2 : 1;
+      return false;
+    }
+  }
+}
+
+__device__ __forceinline__ void simplePost(uint64_t* w, uint64_t v) {
+  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// This workgroup's stores are complete and visible system-wide (peers' staging
+// included) before anyone of it posts a flag; its loads have returned too.
+__device__ __forceinline__ void simpleRelease() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  // the compiler may drop the wait after the L2 write-back (MI355X guide,
+  // "Compiler hazard"): wait explicitly before this wave joins the barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+__device__ __forceinline__ uint64_t* simpleFlag(uint64_t* base, int kind, int n, int who, int gm, int g) {
+  return base + ((uint64_t)kind * n + who) * gm + g;
+}
+
+// Slot `slot` of (region, source src, workgroup g) in rank `owner`'s staging.
+__device__ __forceinline__ char* simpleStage(const SimpleArgs& a, int owner, int region, uint64_t slot, int src,
+                                             int g) {
+  const uint64_t idx = (((uint64_t)region * a.slots + slot) * a.nRanks + src) * a.gridMax + g;
+  return a.peerStage[owner] + idx * a.stageSlice;
+}
+
+// Elements [*off, *off + *cnt) of block b that workgroup g moves in round k.
+template <class E>
+__device__ __forceinline__ void simpleSlice(const SimpleArgs& a, int b, uint64_t k, uint64_t* off, uint64_t* cnt) {
+  uint64_t lo = (uint64_t)b * a.blockElts;
+  if (lo > a.total) lo = a.total;
+  const uint64_t hi = a.total - lo < a.blockElts ? a.total : lo + a.blockElts;
+  const uint64_t sliceE = a.sliceBytes / sizeof(E);
+  const uint64_t s0 = (k * gridDim.x + blockIdx.x) * sliceE;
+  *off = lo + s0;
+  *cnt = s0 >= hi - lo ? 0 : (hi - lo - s0 < sliceE ? hi - lo - s0 : sliceE);
+}
+
+// Workgroup copy of nElts elements into up to two destinations (any alignment;
+// 16-B packs when every pointer is 16-B aligned).
+template <class E>
+__device__ __forceinline__ void simpleCopy(void* d0, void* d1, const void* src, uint64_t nElts) {
+  uint64_t done = 0;
+  if (((((uintptr_t)d0) | ((uintptr_t)src) | (d1 ? (uintptr_t)d1 : 0)) & 15u) == 0) {
+    const uint64_t nPk = nElts * sizeof(E) / 16;
+    const u32x4* s = (const u32x4*)src;
+    constexpr int U = 4;
+    for (uint64_t p = threadIdx.x; p < nPk; p += (uint64_t)U * kBlock) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (p + (uint64_t)u * kBlock < nPk) v[u] = ldPack(s + p + (uint64_t)u * kBlock);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (p + (uint64_t)u * kBlock < nPk) {
+          stPack((u32x4*)d0 + p + (uint64_t)u * kBlock, v[u]);
+          if (d1) stPack((u32x4*)d1 + p + (uint64_t)u * kBlock, v[u]);
+        }
+      }
+    }
+    done = nPk * 16 / sizeof(E);
+  }
+  for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
+    const E v = ((const E*)src)[e];
+    ((E*)d0)[e] = v;
+    if (d1) ((E*)d1)[e] = v;
+  }
+}
+
+// Workgroup fold of nElts elements: acc = pre?(src[0]); acc = Fn(acc, pre?(src[q]))
+// for q = 1 .. nSrcs-1 (pre on source q iff bit q of preMask), postOp, then
+// stored into every destination. Sources and destinations come from the LDS
+// tables (uniform pointers). 16-B packs when `aligned`, else element by element.
+template <class Fn>
+__device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t preMask,
+                                           bool doPost, char* const* dsts, int nDsts, uint64_t nElts, bool aligned) {
+  using E = typename Fn::Elt;
+  constexpr int EPP = 16 / (int)sizeof(E);
+  constexpr int U = 2;
+  constexpr int G = 8;   // sources whose loads are in flight together
+  uint64_t done = 0;
+  if (aligned) {
+    const uint64_t nPk = nElts / EPP;
+    for (uint64_t p = threadIdx.x; p < nPk; p += (uint64_t)U * kBlock) {
+      u32x4 acc[U];
+      for (int q0 = 0; q0 < nSrcs; q0 += G) {
+        u32x4 v[G][U];
+#pragma unroll
+        for (int s = 0; s < G; s++) {
+          if (q0 + s < nSrcs) {
+            const u32x4* sp = (const u32x4*)srcs[q0 + s];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+              if (p + (uint64_t)u * kBlock < nPk) v[s][u] = ldPack(sp + p + (uint64_t)u * kBlock);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < G; s++) {
+          if (q0 + s < nSrcs) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              u32x4 t = v[s][u];
+              if constexpr (Fn::kHasPre) if ((preMask >> (q0 + s)) & 1u) t = fn.prePack(t);
+              acc[u] = (q0 + s == 0) ? t : fn.redPack(acc[u], t);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (p + (uint64_t)u * kBlock < nPk) {
+          u32x4 r = acc[u];
+          if constexpr (Fn::kHasPost) if (doPost) r = fn.postPack(r);
+          for (int d = 0; d < nDsts; d++) stPack((u32x4*)dsts[d] + p + (uint64_t)u * kBlock, r);
+        }
+      }
+    }
+    done = nPk * EPP;
+  }
+  for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
+    E acc = ((const E*)srcs[0])[e];
+    if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.pre(acc);
+    for (int q = 1; q < nSrcs; q++) {
+      E x = ((const E*)srcs[q])[e];
+      if constexpr (Fn::kHasPre) if ((preMask >> q) & 1u) x = fn.pre(x);
+      acc = fn.red(acc, x);
+    }
+    if constexpr (Fn::kHasPost) if (doPost) acc = fn.post(acc);
+    for (int d = 0; d < nDsts; d++) ((E*)dsts[d])[e] = acc;
+  }
+}
+
+__device__ __forceinline__ bool simpleAligned(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
+
+// Per-workgroup state shared by both schedules.
+struct SimpleShared {
+  uint64_t cnt[4][kSimpleMaxRanks];   // SimpleCounter x peer
+  const char* src[kSimpleMaxRanks];
+  char* dst[kSimpleMaxRanks];
+  int fail;
+};
+
+__device__ __forceinline__ void simpleLoadCounters(const SimpleArgs& a, SimpleShared& sh) {
+  const int n = a.nRanks;
+  for (int i = (int)threadIdx.x; i < 4 * n; i += kBlock)
+    sh.cnt[i / n][i % n] = a.counters[(uint64_t)i * a.gridMax + blockIdx.x];
+  if (threadIdx.x == 0) sh.fail = 0;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void simpleStoreCounters(const SimpleArgs& a, SimpleShared& sh) {
+  __syncthreads();
+  const int n = a.nRanks;
+  for (int i = (int)threadIdx.x; i < 4 * n; i += kBlock)
+    a.counters[(uint64_t)i * a.gridMax + blockIdx.x] = sh.cnt[i / n][i % n];
+}
+
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
+  using E = typename Fn::Elt;
+  const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
+  const int n = a.nRanks, me = a.rank, g = (int)blockIdx.x, gm = a.gridMax, tid = (int)threadIdx.x;
+  const uint64_t slots = (uint64_t)a.slots;
+  __shared__ SimpleShared sh;
+  simpleLoadCounters(a, sh);
+  uint64_t* const myFlags = a.peerFlags[me];
+  const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
+  const bool storeLocal = !red || me == a.root;        // B writes this rank's output block
+  const bool gathers = ar || (red && me == a.root);    // C runs here
+  const int first = ((red ? a.root : me) + 1) % n;      // fold order of block `me`
+  auto pushTarget = [&](int p) { return p != me && (ar || (red && p == a.root)); };
+  const char* const send = (const char*)a.send;
+  char* const recv = (char*)a.recv;
+
+  for (uint64_t k = 0; k < a.nRounds; k++) {
+    // ---- A: slice g of block j into rank j's RS region, slot rsSent[j] % slots
+    if (tid < n && tid != me) {
+      const uint64_t sent = sh.cnt[kCtRsSent][tid];
+      if (sent + 1 > slots &&
+          !simpleWait(simpleFlag(myFlags, kFlRsCredit, n, tid, gm, g), sent + 1 - slots, a, tid, kDiagSimpleRsCredit))
+        sh.fail = 1;
+    }
+    __syncthreads();
+    if (sh.fail) return;
+    for (int q = 1; q < n; q++) {
+      const int j = (me + q) % n;
+      uint64_t off, cnt;
+      simpleSlice<E>(a, j, k, &off, &cnt);
+      if (cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), nullptr,
+                             send + off * sizeof(E), cnt);
+    }
+    simpleRelease();
+    if (tid < n && tid != me) simplePost(simpleFlag(a.peerFlags[tid], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][tid]);
+
+    // ---- B: fold block `me` (own input + the n-1 RS slots), store, push to the AG targets
+    if (tid < n && tid != me) {
+      if (!simpleWait(simpleFlag(myFlags, kFlRsReady, n, tid, gm, g), sh.cnt[kCtRsRecv][tid] + 1, a, tid,
+                      kDiagSimpleRs))
+        sh.fail = 1;
+      const uint64_t sent = sh.cnt[kCtAgSent][tid];
+      if (pushTarget(tid) && sent + 1 > slots &&
+          !simpleWait(simpleFlag(myFlags, kFlAgCredit, n, tid, gm, g), sent + 1 - slots, a, tid, kDiagSimpleAgCredit))
+        sh.fail = 1;
+    }
+    uint64_t off, cnt;
+    simpleSlice<E>(a, me, k, &off, &cnt);
+    if (tid < n) {
+      const int j = (first + tid) % n;
+      sh.src[tid] = j == me ? send + off * sizeof(E) : simpleStage(a, me, 0, sh.cnt[kCtRsRecv][j] % slots, j, g);
+      // destinations: [own output], then the push targets in the order me+1, ...
+      if (tid == 0 && storeLocal) sh.dst[0] = recv + off * sizeof(E);
+      if (tid > 0) {
+        const int p = (me + tid) % n;
+        if (ar) sh.dst[tid] = simpleStage(a, p, 1, sh.cnt[kCtAgSent][p] % slots, me, g);
+        else if (red && p == a.root) sh.dst[0] = simpleStage(a, p, 1, sh.cnt[kCtAgSent][p] % slots, me, g);
+      }
+    }
+    __syncthreads();
+    if (sh.fail) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const int nDsts = ar ? n : 1;
+    if (cnt) {
+      const bool aligned = simpleAligned(send + off * sizeof(E)) && (!storeLocal || simpleAligned(recv + off * sizeof(E)));
+      simpleFold<Fn>(fn, sh.src, n, ~0ull, true, sh.dst, nDsts, cnt, aligned);
+    }
+    simpleRelease();
+    if (tid < n && tid != me) {
+      simplePost(simpleFlag(a.peerFlags[tid], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][tid]);
+      if (pushTarget(tid)) simplePost(simpleFlag(a.peerFlags[tid], kFlAgReady, n, me, gm, g), ++sh.cnt[kCtAgSent][tid]);
+    }
+
+    // ---- C: the peers' finished blocks from the AG region into the output
+    if (gathers) {
+      if (tid < n && tid != me &&
+          !simpleWait(simpleFlag(myFlags, kFlAgReady, n, tid, gm, g), sh.cnt[kCtAgRecv][tid] + 1, a, tid,
+                      kDiagSimpleAg))
+        sh.fail = 1;
+      __syncthreads();
+      if (sh.fail) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      for (int q = 1; q < n; q++) {
+        const int j = (me + q) % n;
+        uint64_t o2, c2;
+        simpleSlice<E>(a, j, k, &o2, &c2);
+        if (c2) simpleCopy<E>(recv + o2 * sizeof(E), nullptr, simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), c2);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slots are read: they may be refilled
+      __syncthreads();
+      if (tid < n && tid != me)
+        simplePost(simpleFlag(a.peerFlags[tid], kFlAgCredit, n, me, gm, g), ++sh.cnt[kCtAgRecv][tid]);
+    }
+    __syncthreads();
+  }
+  simpleStoreCounters(a, sh);
+}
+
+// Ring schedule through the right neighbour's staging. AllReduce /
+// ReduceScatter: chunk c enters at rank c+1 (raw), is folded at c+2, ..., and
+// finished (PostOp) at c; AllReduce then forwards the finished chunk around
+// the ring (all_reduce.h:60-93). Reduce: the chain root+1 -> ... -> root over
+// the one block of the message (reduce.h:44-67).
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
+  using E = typename Fn::Elt;
+  const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
+  const int n = a.nRanks, me = a.rank, g = (int)blockIdx.x, gm = a.gridMax, tid = (int)threadIdx.x;
+  const int left = (me + n - 1) % n, right = (me + 1) % n;
+  const uint64_t slots = (uint64_t)a.slots;
+  __shared__ SimpleShared sh;
+  simpleLoadCounters(a, sh);
+  uint64_t* const myFlags = a.peerFlags[me];
+  const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
+  const char* const send = (const char*)a.send;
+  char* const recv = (char*)a.recv;
+  // thread 0 waits for what a hop needs: the left neighbour's slice (recvFrom)
+  // and free slots at the right neighbour (RS region: pushRs, AG region: pushAg)
+  auto hopWait = [&](int recvRegion, bool pushRs, bool pushAg) {
+    if (tid == 0) {
+      if (recvRegion >= 0) {
+        const int fl = recvRegion == 0 ? kFlRsReady : kFlAgReady;
+        const int ct = recvRegion == 0 ? kCtRsRecv : kCtAgRecv;
+        if (!simpleWait(simpleFlag(myFlags, fl, n, left, gm, g), sh.cnt[ct][left] + 1, a, left,
+                        recvRegion == 0 ? kDiagSimpleRs : kDiagSimpleAg))
+          sh.fail = 1;
+      }
+      const uint64_t rsS = sh.cnt[kCtRsSent][right], agS = sh.cnt[kCtAgSent][right];
+      if (pushRs && rsS + 1 > slots &&
+          !simpleWait(simpleFlag(myFlags, kFlRsCredit, n, right, gm, g), rsS + 1 - slots, a, right, kDiagSimpleRsCredit))
+        sh.fail = 1;
+      if (pushAg && agS + 1 > slots &&
+          !simpleWait(simpleFlag(myFlags, kFlAgCredit, n, right, gm, g), agS + 1 - slots, a, right, kDiagSimpleAgCredit))
+        sh.fail = 1;
+    }
+    __syncthreads();
+    if (!sh.fail && recvRegion >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    return sh.fail == 0;
+  };
+  auto hopPost = [&](int recvRegion, bool pushRs, bool pushAg) {
+    if (tid == 0) {
+      if (recvRegion == 0) simplePost(simpleFlag(a.peerFlags[left], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][left]);
+      if (recvRegion == 1) simplePost(simpleFlag(a.peerFlags[left], kFlAgCredit, n, me, gm, g), ++sh.cnt[kCtAgRecv][left]);
+      if (pushRs) simplePost(simpleFlag(a.peerFlags[right], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][right]);
+      if (pushAg) simplePost(simpleFlag(a.peerFlags[right], kFlAgReady, n, me, gm, g), ++sh.cnt[kCtAgSent][right]);
+    }
+    __syncthreads();
+  };
+
+  for (uint64_t k = 0; k < a.nRounds; k++) {
+    if (red) {
+      // chain position: 0 = root+1 (sends its raw input), n-1 = the root
+      const int pos = (me - a.root - 1 + 2 * n) % n;
+      uint64_t off, cnt;
+      simpleSlice<E>(a, 0, k, &off, &cnt);
+      const bool push = pos < n - 1;
+      if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
+      char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : recv + off * sizeof(E);
+      if (pos == 0) {
+        if (cnt) simpleCopy<E>(out, nullptr, send + off * sizeof(E), cnt);
+      } else if (cnt) {
+        if (tid == 0) {
+          sh.src[0] = send + off * sizeof(E);
+          sh.src[1] = simpleStage(a, me, 0, sh.cnt[kCtRsRecv][left] % slots, left, g);
+          sh.dst[0] = out;
+        }
+        __syncthreads();
+        const bool aligned = simpleAligned(send + off * sizeof(E)) && simpleAligned(out);
+        simpleFold<Fn>(fn, sh.src, 2, pos == 1 ? 3u : 1u, !push, sh.dst, 1, cnt, aligned);
+      }
+      simpleRelease();
+      hopPost(pos == 0 ? -1 : 0, push, false);
+      continue;
+    }
+    // send step: the raw chunk me-1 into the right neighbour's RS region
+    {
+      uint64_t off, cnt;
+      simpleSlice<E>(a, left, k, &off, &cnt);
+      if (!hopWait(-1, true, false)) return;
+      if (cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), nullptr,
+                             send + off * sizeof(E), cnt);
+      simpleRelease();
+      hopPost(-1, true, false);
+    }
+    // reduce-scatter hops: chunk me-2-st, Fn(pre(local), received)
+    for (int st = 0; st < n - 1; st++) {
+      const int c = (me + 2 * n - 2 - st) % n;
+      const bool last = st == n - 2;
+      uint64_t off, cnt;
+      simpleSlice<E>(a, c, k, &off, &cnt);
+      if (!hopWait(0, !last, last && ar)) return;
+      if (tid == 0) {
+        sh.src[0] = send + off * sizeof(E);
+        sh.src[1] = simpleStage(a, me, 0, sh.cnt[kCtRsRecv][left] % slots, left, g);
+        sh.dst[0] = last ? recv + off * sizeof(E) : simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g);
+        sh.dst[1] = simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g);
+      }
+      __syncthreads();
+      if (cnt) {
+        const bool aligned = simpleAligned(sh.src[0]) && simpleAligned(sh.dst[0]);
+        simpleFold<Fn>(fn, sh.src, 2, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, cnt, aligned);
+      }
+      simpleRelease();
+      hopPost(0, !last, last && ar);
+    }
+    if (!ar) continue;
+    // all-gather hops: the finished chunk me-1-st from the left, forwarded n-2 times
+    for (int st = 0; st < n - 1; st++) {
+      const int c = (me + 2 * n - 1 - st) % n;
+      const bool fwd = st < n - 2;
+      uint64_t off, cnt;
+      simpleSlice<E>(a, c, k, &off, &cnt);
+      if (!hopWait(1, false, fwd)) return;
+      if (cnt)
+        simpleCopy<E>(recv + off * sizeof(E), fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr,
+                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), cnt);
+      simpleRelease();
+      hopPost(1, false, fwd);
+    }
+  }
+  simpleStoreCounters(a, sh);
+}
+
+}  // namespace nbx

@@ -42,8 +42,6 @@
 #include "../../include/nbx_debug.h"
 #include "../../include/nbx_reduce.h"
 #include "nbx_bootstrap.h"
-#include "nbx_shmx.h"
-#include "nbx_sync.h"
 #include "nbx_internal.h"
 #include "nbx_ll_args.h"
 #include "nbx_diag.h"
@@ -641,15 +639,20 @@ ncclResult_t flushPendingImpl() {
 // ---------------------------------------------------------------------------
 // Multi-process communicator (ncclCommInitRank with nranks > 1, one process
 // per rank on one node). Replaces NCCL's bootstrap + P2P transport setup
-// (bootstrap.cc, transport/p2p.cc:190-381) with: a TCP bootstrap for the
-// allgathers, hipIpc handles of the caller's buffers exchanged per call
-// (NCCL calls "may perform inter-CPU synchronization", nccl.h.in:253-261)
-// and cached after the first map, and device flag barriers (nbx_sync.hip)
-// ordering the phases on the caller's stream. The data path is the same
-// one-shot direct exchange as the in-process clique.
+// (bootstrap.cc, transport/p2p.cc:190-381) with a TCP bootstrap for the
+// init-time allgathers and connection buffers that the library allocates and
+// every peer IPC-maps ONCE, at init (p2pMap / p2pSendConnect / p2pRecvConnect,
+// p2p.cc:290-330,450-520):
+//   * LL / LL128 line buffers (nbx_ll.h) for small and medium messages;
+//   * the Simple protocol's staging and flag words (nbx_simple.h) for the rest,
+//     direct or ring schedule (NCCL_ALGO=Ring).
+// Peers never touch the caller's buffers and no call exchanges anything on
+// the host: a collective is one kernel on the caller's stream whose flow
+// control (the reference's waitPeer / postPeer, prims_simple.h:129-185)
+// runs inside it. All sequencing state is device-resident, so graph capture
+// and replay need nothing special.
 
-enum { kSlotEnter = 0, kSlotReduced = 1, kSlotDone = 2, kSlotRing = 3, kNumSlots = 4 };
-constexpr int kMaxMpRanks = 64;
+constexpr int kMaxMpRanks = nbx::kSimpleMaxRanks;   // one staging source region per rank
 
 // One reducing collective as enqueued on a multi-process communicator (the
 // same record the in-process clique queues).
@@ -657,36 +660,21 @@ using MpCall = PendingColl;
 
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
-  nbx::ShmExchange* shmx = nullptr;     // per-call exchange through /dev/shm (nullptr: TCP bootstrap)
-  uint64_t* flags = nullptr;           // own phase flags (device memory, IPC-exported)
-  uint64_t** peerFlagsDev = nullptr;   // device table: rank -> flags (self = flags)
-  std::vector<void*> peerFlagMaps;     // IPC mappings to close
-  int* hostWords = nullptr;            // pinned: [0] abort, [1] error
+  int* hostWords = nullptr;            // pinned: [0] abort, [1] error, diag record at byte 16
   int* hostWordsDev = nullptr;
-  uint64_t seq = 0;
   double timeoutSec = 300.0;
-  struct Mapping {
-    void* base;
-    uint64_t lastUse;   // seq of the last collective that used it; kPinned: used by a captured graph
-  };
-  static constexpr uint64_t kPinned = ~0ull;
-  std::map<std::pair<int, std::string>, Mapping> maps;   // (peer, ipc handle) -> mapped base
-  size_t mapsMax = 512;   // NBX_IPC_CACHE_MAX: beyond this, unused mappings are closed
-  // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] lines + [n] done words +
-  // arrival counter; peers' buffers mapped
+  std::vector<void*> peerMaps;         // every IPC mapping this communicator opened (closed at destroy)
+  // LL protocol (nbx_ll.h): own buffer [2][n][slotLines] lines + [n] done words
   uint64_t* ll = nullptr;
   uint64_t** peerLLDev = nullptr;
-  std::vector<void*> peerLLMaps;
   uint64_t llMaxBytes = 0;
   uint64_t llSlotLines = 0;
   uint64_t llDoneOff = 0;
   nbx::LLState* llState = nullptr;  // device-resident LL-family sequencing (nbx_ll_args.h)
-  uint64_t* epochs = nullptr;       // device-resident barrier epochs, one per flag slot
   // LL128 protocol (nbx_ll.h kLL128Coll): own buffer [2][n][l128SlotLines] 64-B lines;
-  // shares the LL buffer's done words, arrival counter and parity credits
+  // shares the LL buffer's done words and parity credits
   uint64_t* l128 = nullptr;
   uint64_t** peerL128Dev = nullptr;
-  std::vector<void*> peerL128Maps;
   uint64_t l128MaxBytes = 0;        // 0: LL128 unavailable (n > 8)
   uint64_t l128OneShotMax = 0;      // AllReduce, n > 2: one-shot up to this, two-shot above
   uint64_t l128SlotLines = 0;
@@ -694,50 +682,57 @@ struct MpState {
   int protoMask = 0;                // NCCL_PROTO at init: kProtoLL | kProtoLL128 | kProtoSimple
   bool ring = false;                // NCCL_ALGO=Ring at init
   bool multiGpu = false;            // the ranks span more than one physical GPU (PCI key)
-  bool ringPipeline = true;         // ring as the pipelined kernel (nbx_ring.h); NBX_RING_PIPELINE=0: per-step kernels
-  bool groupBatch = true;           // NBX_GROUP_BATCH at init: groups run as batched exchanges
-  uint64_t* ringProg = nullptr;     // [kRingMaxGrid] progress words the left neighbour posts (uncached)
-  uint64_t* rightRingProg = nullptr;// the right neighbour's words (peer mapping)
-  nbx::RingState* ringState = nullptr;
-  unsigned ringMaxGrid = nbx::kRingMaxGrid;   // NBX_RING_MAX_GRID
-  // step FIFO of the ring ReduceScatter / chain Reduce (NCCL_ALGO=Ring only)
-  void* fifo = nullptr;             // own FIFO (device memory, IPC-exported)
-  uint64_t* fifoTail = nullptr;     // [kRingMaxGrid] entries the left neighbour produced (uncached)
-  uint64_t* fifoHead = nullptr;     // [kRingMaxGrid] entries of `fifo` the right neighbour consumed (uncached)
-  void* leftFifo = nullptr;         // peer mappings
-  uint64_t* rightFifoTail = nullptr;
-  uint64_t* leftFifoHead = nullptr;
+  // Simple protocol (nbx_simple.h): staging [2][slots][n][grid][slice] and flag
+  // words [4][n][grid] (uncached, IPC-mapped by every peer), counters [4][n][grid]
+  char* stage = nullptr;
+  uint64_t stageBytes = 0;
+  uint64_t* sflags = nullptr;
+  uint64_t* scounters = nullptr;
+  char** peerStageDev = nullptr;
+  uint64_t** peerSFlagsDev = nullptr;
+  uint64_t sliceBytes = 0;          // NBX_SIMPLE_SLICE_BYTES: staging bytes per (slot, source, workgroup)
+  int slots = 2;                    // NBX_SIMPLE_SLOTS
+  int simpleGrid = 0;               // workgroups of a full-size Simple call (NBX_SIMPLE_MAX_GRID, CU-capped)
+  // successive calls are ordered across streams, as NCCL serializes a
+  // communicator's work: a call on another stream waits for the previous one
+  hipEvent_t lastEvent = nullptr;
+  hipStream_t lastStream = nullptr;
+  bool haveLast = false;
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
+};
+
+// Exchanged before anything is allocated: where every rank runs.
+struct MpPreInfo {
+  uint64_t pciKey;   // (domain, bus, device) of this rank's GPU: identifies it across processes
+  int32_t device;
+  int32_t cus;
 };
 
 struct MpInitInfo {
   int32_t pid;
   int32_t device;
-  hipIpcMemHandle_t flagsHandle;
   hipIpcMemHandle_t llHandle;
   hipIpcMemHandle_t l128Handle;
-  hipIpcMemHandle_t ringHandle;
-  hipIpcMemHandle_t fifoHandle, fifoTailHandle, fifoHeadHandle;   // NCCL_ALGO=Ring only
-  uint64_t pciKey;   // (domain, bus, device) of this rank's GPU: identifies it across processes
+  hipIpcMemHandle_t stageHandle;
+  hipIpcMemHandle_t sflagsHandle;
+  uint64_t nonce;          // this communicator's mapping self-check pattern (mpVerifyMappings)
+  // settings every rank must share: every rank must pick the same protocol,
+  // grid and staging layout for the same call
   uint64_t llMaxBytes;
   uint64_t l128MaxBytes;
   uint64_t l128OneShotMax;
+  uint64_t sliceBytes;
   int32_t protoMask;
-  // schedule settings every rank must share: a workgroup of the pipelined ring
-  // waits on its left neighbour's progress word of the same slice, so a
-  // different grid (NBX_RING_MAX_GRID) or schedule would fold unfinished
-  // partials or drift the barrier epochs apart
-  int32_t ring;           // NCCL_ALGO=Ring
-  int32_t ringPipeline;   // NBX_RING_PIPELINE
-  int32_t ringMaxGrid;    // NBX_RING_MAX_GRID
-  int32_t groupBatch;     // NBX_GROUP_BATCH
+  int32_t ring;            // NCCL_ALGO=Ring
+  int32_t slots;
+  int32_t simpleGrid;
 };
 
 // NCCL_PROTO (tuning.cc:254-259, parseList): a comma-separated list of the
 // enabled protocols among LL, LL128, Simple, or "^list" for all but those.
 // Per message (per-rank block for ReduceScatter) the first enabled protocol
 // whose buffer holds it is used: LL up to NBX_LL_MAX_BYTES (64 KiB), LL128 up
-// to NBX_LL128_MAX_BYTES (1 MiB; n <= 8 ranks), else Simple (also the
+// to NBX_LL128_MAX_BYTES (4 MiB; n <= 8 ranks), else Simple (also the
 // fallback when Simple is disabled and nothing else fits).
 // Read when the communicator is created (as NCCL reads its tuning env at init).
 enum { kProtoLL = 1, kProtoLL128 = 2, kProtoSimple = 4, kProtoAll = 7 };
@@ -788,143 +783,25 @@ MpProto chooseProtoFor(int mask, bool twoShotKind, uint64_t slotBytes, uint64_t 
   return kMpSimple;
 }
 
-struct MpCallInfo {
-  uint64_t seq;
-  int32_t kind, dt, op, root;
-  uint64_t count;
-  int32_t flags;   // kMpContig
-  int32_t hasSend, hasRecv;
-  hipIpcMemHandle_t sendH, recvH;
-  uint64_t sendOff, recvOff;
-};
-
-// The Simple path's per-call allgather: shared memory when every rank could
-// attach the segment at init, the TCP bootstrap otherwise.
-ncclResult_t mpExchange(MpState* mp, uint64_t seq, const void* mine, size_t len, void* all) {
-  if (mp->shmx) return nbx::shmxAllGather(mp->shmx, seq, mine, len, all, mp->timeoutSec, mp->hostWords);
-  return nbx::bootstrapAllGather(mp->bs, mine, len, all);
-}
-
-// Name of the communicator's exchange segment, derived from its unique id.
-std::string shmxName(const ncclUniqueId& id) {
-  uint64_t h = 1469598103934665603ull;   // FNV-1a over the id bytes
-  for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; i++) h = (h ^ (uint8_t)id.internal[i]) * 1099511628211ull;
-  char buf[64];
-  std::snprintf(buf, sizeof(buf), "/nbx-shmx-%016llx", (unsigned long long)h);
-  return buf;
-}
-
-// Collective: rank 0 creates the segment, the others attach; used only if
-// every rank succeeded (NBX_HOST_EXCHANGE=tcp on any rank keeps TCP).
-ncclResult_t mpSetupShmx(ncclComm* c, const ncclUniqueId& id) {
-  MpState* mp = c->mp;
-  const char* env = std::getenv("NBX_HOST_EXCHANGE");
-  const bool want = !(env && strcasecmp(env, "tcp") == 0);
-  const std::string name = shmxName(id);
-  std::vector<int32_t> ok(c->nRanks);
-  int32_t mine = 0;
-  if (c->rank == 0 && want) {
-    nbx::shmxUnlink(name.c_str());   // a stale segment of a crashed run with the same id (practically never)
-    mp->shmx = nbx::shmxOpen(name.c_str(), 0, c->nRanks, sizeof(MpCallInfo), true);
-    mine = mp->shmx != nullptr;
-  }
-  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), ok.data()));   // created?
-  const bool created = ok[0] != 0;
-  if (c->rank != 0) {
-    if (created && want) mp->shmx = nbx::shmxOpen(name.c_str(), c->rank, c->nRanks, sizeof(MpCallInfo), false);
-    mine = mp->shmx != nullptr;
-  }
-  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), ok.data()));   // everyone attached?
-  if (c->rank == 0 && created) nbx::shmxUnlink(name.c_str());
-  bool all = true;
-  for (int32_t v : ok) all &= v != 0;
-  if (!all && mp->shmx) {
-    nbx::shmxClose(mp->shmx);
-    mp->shmx = nullptr;
-  }
-  info("comm %p rank %d: per-call exchange over %s", (void*)c, c->rank, mp->shmx ? "shared memory" : "TCP");
-  return ncclSuccess;
-}
-
-// Closing a peer-buffer mapping frees its virtual range, and the next import
-// in this process can land at the same address. A call through such a
-// reused address read zeros / garbage from the peer's buffer and its stores
-// to it vanished (bench N = 2 rehearsals: 8 of 22 runs, always the first call
-// through a new mapping whose address an earlier, closed mapping had used —
-// a stale translation for the old mapping). Retired mappings are
-// therefore kept open, up to NBX_IPC_RETIRED_MAX (4096) process-wide, oldest
-// closed first, so addresses are not reused while their translations may be live.
-void retirePeerMapping(void* base) {
-  static std::mutex mu;
-  static std::deque<void*> retired;
-  static const size_t maxRetired = [] {
-    const char* v = std::getenv("NBX_IPC_RETIRED_MAX");
-    return (v && *v) ? (size_t)std::strtoull(v, nullptr, 10) : (size_t)4096;
-  }();
-  std::lock_guard<std::mutex> g(mu);
-  retired.push_back(base);
-  while (retired.size() > maxRetired) {
-    (void)hipIpcCloseMemHandle(retired.front());
-    retired.pop_front();
-  }
-}
-
-ncclResult_t ipcHandleOf(const void* p, hipIpcMemHandle_t* h, uint64_t* off) {
-  hipDeviceptr_t base = nullptr;
-  size_t size = 0;
-  HIPCHECK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p));
-  HIPCHECK(hipIpcGetMemHandle(h, (void*)base));
-  *off = (uint64_t)((const char*)p - (const char*)base);
-  return ncclSuccess;
-}
-
-// `pin`: the call is being captured into a graph, whose replays keep using the
-// mapping — it is never evicted.
-ncclResult_t mapPeer(MpState* mp, int peer, const hipIpcMemHandle_t& h, void** base, bool pin) {
-  auto key = std::make_pair(peer, std::string((const char*)&h, sizeof(h)));
-  const uint64_t use = pin ? MpState::kPinned : mp->seq;
-  auto it = mp->maps.find(key);
-  if (it != mp->maps.end()) {
-    if (it->second.lastUse != MpState::kPinned) it->second.lastUse = use;
-    *base = it->second.base;
-    return ncclSuccess;
-  }
-  void* p = nullptr;
-  HIPCHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  mp->maps[key] = MpState::Mapping{p, use};
-  *base = p;
-  return ncclSuccess;
-}
-
-// Advance this rank's epoch of `slot`, post it, wait for the ranks in `mask`
-// to reach it (epochs live on the device: graph replays stay in step).
-ncclResult_t mpSignalWait(ncclComm* comm, int slot, uint64_t mask, hipStream_t stream) {
-  MpState* mp = comm->mp;
-  HIPCHECK(nbx::launchPeerBarrier(mp->flags, mp->peerFlagsDev, comm->nRanks, slot, mask, mp->epochs,
-                                  mp->hostWordsDev, mp->hostWordsDev + 1, mp->timeoutSec, stream));
-  return ncclSuccess;
-}
-
-ncclResult_t mpBarrier(ncclComm* comm, int slot, hipStream_t stream) {
-  const int n = comm->nRanks;
-  const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1ull);
-  return mpSignalWait(comm, slot, all, stream);
-}
-
-
-// NCCL_ALGO (tuning.cc:254-259): "Ring" selects the ring schedule for
-// AllReduce; anything else (default) the one-shot direct exchange.
+// NCCL_ALGO (tuning.cc:254-259): "Ring" selects the ring schedule for the
+// Simple protocol; anything else (default) the direct schedule.
 // Read when the communicator is created.
 bool algoRingFromEnv() {
   const char* v = std::getenv("NCCL_ALGO");
   return v && strcasecmp(v, "ring") == 0;
 }
 
-// Memory that other GPUs write and this GPU polls (barrier flags, LL lines).
-// Uncached (fine-grained, MTYPE UC) by default: a peer's system-scope store
-// over xGMI lands in HBM and no XCD L2 can hold a stale copy, which is what
-// RCCL uses for its flags too. NBX_SYNC_MEM=coarse selects plain hipMalloc
-// (A/B measurement only).
+long envLong(const char* name, long dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atol(v) : dflt;
+}
+
+// Memory that other GPUs write and this GPU reads (LL lines, Simple staging
+// and flag words). Uncached (MTYPE UC) by default: a peer's stores over xGMI
+// land in HBM and no XCD L2 can hold a stale copy, which is what RCCL uses
+// for its connection buffers too. NBX_SYNC_MEM=coarse selects plain hipMalloc
+// (A/B measurement only: coarse-grained memory shared between processes is
+// exactly what round 2's wrong results came from).
 hipError_t allocSyncMem(void** p, size_t bytes) {
   static const bool coarse = [] {
     const char* v = std::getenv("NBX_SYNC_MEM");
@@ -935,7 +812,6 @@ hipError_t allocSyncMem(void** p, size_t bytes) {
 }
 
 ncclResult_t mpLL128SelfTest(ncclComm* c);
-bool groupBatchEnabled();
 
 // A device spin gave up (host error word set): name the wait, the peer, the
 // value it waited for and the last one it saw (nbx_diag.h), once per record.
@@ -958,129 +834,199 @@ void mpReportDeviceError(ncclComm* c) {
        (unsigned long long)rec[4]);
 }
 
+ncclResult_t mpOpenPeer(MpState* mp, const hipIpcMemHandle_t& h, void** p) {
+  HIPCHECK(hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess));
+  mp->peerMaps.push_back(*p);
+  return ncclSuccess;
+}
+
+// The 16-byte mapping self-check word rank `from` leaves at slot `at`.
+void checkWord(uint64_t nonce, int from, int at, uint64_t out[2]) {
+  out[0] = nonce ^ (0x9e3779b97f4a7c15ull * (uint64_t)(from + 1));
+  out[1] = ~nonce ^ (0xc2b2ae3d27d4eb4full * (uint64_t)(at + 1));
+}
+
+// Every peer mapping is checked once, before first use, with this
+// communicator's random nonces: each rank stores a word through its mapping
+// of every peer's staging (slot = its rank) and its own word at slot n; after
+// a bootstrap barrier each rank checks the words peers stored into its own
+// staging and reads every peer's own word through its mapping. A mapping that
+// reaches other pages than the peer's allocation (the round-2 failure mode)
+// makes ncclCommInitRank fail loudly instead of a collective going silently
+// wrong. The words live in the AG region's last bytes, which a call rewrites
+// before reading.
+ncclResult_t mpVerifyMappings(ncclComm* c, const std::vector<MpInitInfo>& all, const std::vector<char*>& stages) {
+  MpState* mp = c->mp;
+  const int n = c->nRanks, me = c->rank;
+  const uint64_t base = mp->stageBytes - 16ull * (uint64_t)(n + 1);
+  uint64_t w[2];
+  for (int j = 0; j < n; j++) {
+    if (j == me) continue;
+    checkWord(all[me].nonce, me, j, w);
+    HIPCHECK(hipMemcpy(stages[j] + base + 16ull * (uint64_t)me, w, 16, hipMemcpyHostToDevice));
+  }
+  checkWord(all[me].nonce, me, n, w);
+  HIPCHECK(hipMemcpy(mp->stage + base + 16ull * (uint64_t)n, w, 16, hipMemcpyHostToDevice));
+  HIPCHECK(hipDeviceSynchronize());
+  int32_t bad = 0, dummy = 0;
+  std::vector<int32_t> gathered(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), gathered.data()));
+  std::vector<uint64_t> mine(2 * (size_t)(n + 1));
+  HIPCHECK(hipMemcpy(mine.data(), mp->stage + base, 16ull * (uint64_t)(n + 1), hipMemcpyDeviceToHost));
+  for (int j = 0; j < n; j++) {
+    if (j == me) continue;
+    checkWord(all[j].nonce, j, me, w);
+    if (mine[2 * j] != w[0] || mine[2 * j + 1] != w[1]) {
+      warn("ncclCommInitRank : rank %d's store through its mapping of rank %d's staging did not land", j, me);
+      bad = 1;
+    }
+    uint64_t got[2];
+    HIPCHECK(hipMemcpy(got, stages[j] + base + 16ull * (uint64_t)n, 16, hipMemcpyDeviceToHost));
+    checkWord(all[j].nonce, j, n, w);
+    if (got[0] != w[0] || got[1] != w[1]) {
+      warn("ncclCommInitRank : rank %d's mapping of rank %d's staging reads other bytes", me, j);
+      bad = 1;
+    }
+  }
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &bad, sizeof(bad), gathered.data()));
+  for (int32_t b : gathered)
+    if (b) return ncclSystemError;
+  return ncclSuccess;
+}
+
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   MpState* mp = new MpState();
   c->mp = mp;
+  const int n = c->nRanks, me = c->rank;
   const char* t = std::getenv("NBX_TIMEOUT_SEC");
   if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
-  const char* cm = std::getenv("NBX_IPC_CACHE_MAX");
-  if (cm && std::atol(cm) > 0) mp->mapsMax = (size_t)std::atol(cm);
   mp->protoMask = protoFromEnv();
   mp->ring = algoRingFromEnv();
+  NCCLCHECK(nbx::bootstrapConnect(id, me, n, &mp->bs));
+  // where every rank runs: decides LL128's self-test and the Simple grid
+  MpPreInfo pre{};
   {
-    const char* v = std::getenv("NBX_RING_PIPELINE");
-    mp->ringPipeline = !(v && std::strcmp(v, "0") == 0);
-    const char* gcap = std::getenv("NBX_RING_MAX_GRID");
-    const long gv = (gcap && *gcap) ? std::atol(gcap) : nbx::kRingMaxGrid;
-    mp->ringMaxGrid = (unsigned)(gv < 1 ? 1 : gv > nbx::kRingMaxGrid ? nbx::kRingMaxGrid : gv);
+    int dom = 0, bus = 0, dv = 0, cus = 0;
+    (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device);
+    (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device);
+    (void)hipDeviceGetAttribute(&dv, hipDeviceAttributePciDeviceId, c->device);
+    HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    pre.pciKey = ((uint64_t)(uint32_t)dom << 32) | ((uint64_t)(uint32_t)bus << 8) | (uint64_t)(uint32_t)dv;
+    pre.device = c->device;
+    pre.cus = cus;
   }
-  NCCLCHECK(nbx::bootstrapConnect(id, c->rank, c->nRanks, &mp->bs));
-  HIPCHECK(allocSyncMem((void**)&mp->flags, kNumSlots * sizeof(uint64_t)));
-  HIPCHECK(hipMemset(mp->flags, 0, kNumSlots * sizeof(uint64_t)));
-  HIPCHECK(hipMalloc((void**)&mp->epochs, kNumSlots * sizeof(uint64_t)));
-  HIPCHECK(hipMemset(mp->epochs, 0, kNumSlots * sizeof(uint64_t)));
+  std::vector<MpPreInfo> pres(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &pre, sizeof(pre), pres.data()));
+  int minCus = pre.cus, maxShare = 1;
+  for (int j = 0; j < n; j++) {
+    mp->multiGpu |= pres[j].pciKey != pre.pciKey;
+    minCus = std::min(minCus, (int)pres[j].cus);
+    int share = 0;
+    for (int q = 0; q < n; q++) share += pres[q].pciKey == pres[j].pciKey;
+    maxShare = std::max(maxShare, share);
+  }
+  // Simple grid: one workgroup per CU, all co-resident (workgroup g of a rank
+  // waits on workgroup g of its peers); ranks sharing a GPU split its CUs.
+  {
+    long g = envLong("NBX_SIMPLE_MAX_GRID", nbx::kSimpleMaxGrid);
+    g = std::min<long>(g, std::max(1, minCus / maxShare));
+    mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
+    long s = envLong("NBX_SIMPLE_SLICE_BYTES", 16 << 10);
+    s = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(s, 1 << 20));
+    mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
+    mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
+  }
+  HIPCHECK(hipEventCreateWithFlags(&mp->lastEvent, hipEventDisableTiming));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
   HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
-  HIPCHECK(allocSyncMem((void**)&mp->ringProg, nbx::kRingMaxGrid * sizeof(uint64_t)));
-  HIPCHECK(hipMemset(mp->ringProg, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
-  HIPCHECK(hipMalloc((void**)&mp->ringState, sizeof(nbx::RingState)));
-  HIPCHECK(hipMemset(mp->ringState, 0, sizeof(nbx::RingState)));
-  if (mp->ring) {
-    HIPCHECK(hipMalloc(&mp->fifo, nbx::kRingFifoBytes));
-    HIPCHECK(allocSyncMem((void**)&mp->fifoTail, nbx::kRingMaxGrid * sizeof(uint64_t)));
-    HIPCHECK(hipMemset(mp->fifoTail, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
-    HIPCHECK(allocSyncMem((void**)&mp->fifoHead, nbx::kRingMaxGrid * sizeof(uint64_t)));
-    HIPCHECK(hipMemset(mp->fifoHead, 0, nbx::kRingMaxGrid * sizeof(uint64_t)));
-  }
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(mp->hostWords, 0, 64);
   HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
   // LL buffer: 2 parities x n sources x 2 lines per 8-byte pack
   {
-    const char* v = std::getenv("NBX_LL_MAX_BYTES");
-    uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (64u << 10);
+    uint64_t mx = (uint64_t)envLong("NBX_LL_MAX_BYTES", 64 << 10);
     mx = (mx + 15) & ~(uint64_t)15;
     if (mx < 1024) mx = 1024;
     mp->llMaxBytes = mx;
     mp->llSlotLines = 2 * (mx / 8);
-    mp->llDoneOff = 2 * (uint64_t)c->nRanks * mp->llSlotLines;
-    const size_t llBytes = (mp->llDoneOff + (uint64_t)c->nRanks + 1) * sizeof(uint64_t);
+    mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
+    const size_t llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
     HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes));
     HIPCHECK(hipMemset(mp->ll, 0, llBytes));
   }
-  // LL128 buffer: 2 parities x n sources x 64-byte lines of 56 payload bytes (n <= 8)
-  if (c->nRanks <= nbx::kL128MaxRanksHost) {
-    const char* v = std::getenv("NBX_LL128_MAX_BYTES");
-    uint64_t mx = (v && *v) ? std::strtoull(v, nullptr, 10) : (4u << 20);
-    const char* o = std::getenv("NBX_LL128_ONESHOT_MAX");
-    mp->l128OneShotMax = (o && *o) ? std::strtoull(o, nullptr, 10) : (256u << 10);
+  // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
+  if (n <= nbx::kL128MaxRanksHost) {
+    uint64_t mx = (uint64_t)envLong("NBX_LL128_MAX_BYTES", 4 << 20);
+    mp->l128OneShotMax = (uint64_t)envLong("NBX_LL128_ONESHOT_MAX", 256 << 10);
     if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
     if (mx != 0) {
       mx = (mx + 15) & ~(uint64_t)15;
       mp->l128MaxBytes = mx;
       mp->l128SlotLines = l128SlotLinesFor(mx);
-      mp->l128Bytes = 2 * (uint64_t)c->nRanks * mp->l128SlotLines * nbx::kL128LineBytesHost;
+      mp->l128Bytes = 2 * (uint64_t)n * mp->l128SlotLines * nbx::kL128LineBytesHost;
       HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes));
       HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
     }
   }
+  // Simple staging, flag words and counters
+  const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
+  mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
+  HIPCHECK(allocSyncMem((void**)&mp->stage, mp->stageBytes));
+  HIPCHECK(hipMemset(mp->stage, 0, mp->stageBytes));
+  HIPCHECK(allocSyncMem((void**)&mp->sflags, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->sflags, 0, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(hipMalloc((void**)&mp->scounters, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->scounters, 0, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(hipDeviceSynchronize());   // zeroed before any peer can map and write them
+
   MpInitInfo mine{};
   mine.pid = (int32_t)getpid();
   mine.device = c->device;
   mine.llMaxBytes = mp->llMaxBytes;
   mine.l128MaxBytes = mp->l128MaxBytes;
   mine.l128OneShotMax = mp->l128OneShotMax;
+  mine.sliceBytes = mp->sliceBytes;
   mine.protoMask = mp->protoMask;
-  mp->groupBatch = groupBatchEnabled();
   mine.ring = mp->ring;
-  mine.ringPipeline = mp->ringPipeline;
-  mine.ringMaxGrid = (int32_t)mp->ringMaxGrid;
-  mine.groupBatch = mp->groupBatch;
-  HIPCHECK(hipIpcGetMemHandle(&mine.flagsHandle, mp->flags));
+  mine.slots = mp->slots;
+  mine.simpleGrid = mp->simpleGrid;
+  mine.nonce = std::random_device{}() * 0x100000001ull ^ (uint64_t)std::random_device{}() ^
+               ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)mp;
   HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
   if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
-  HIPCHECK(hipIpcGetMemHandle(&mine.ringHandle, mp->ringProg));
-  if (mp->ring) {
-    HIPCHECK(hipIpcGetMemHandle(&mine.fifoHandle, mp->fifo));
-    HIPCHECK(hipIpcGetMemHandle(&mine.fifoTailHandle, mp->fifoTail));
-    HIPCHECK(hipIpcGetMemHandle(&mine.fifoHeadHandle, mp->fifoHead));
-  }
-  {
-    int dom = 0, bus = 0, dv = 0;
-    (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device);
-    (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device);
-    (void)hipDeviceGetAttribute(&dv, hipDeviceAttributePciDeviceId, c->device);
-    mine.pciKey = ((uint64_t)(uint32_t)dom << 32) | ((uint64_t)(uint32_t)bus << 8) | (uint64_t)(uint32_t)dv;
-  }
-  std::vector<MpInitInfo> all(c->nRanks);
+  HIPCHECK(hipIpcGetMemHandle(&mine.stageHandle, mp->stage));
+  HIPCHECK(hipIpcGetMemHandle(&mine.sflagsHandle, mp->sflags));
+  std::vector<MpInitInfo> all(n);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
-  for (int j = 0; j < c->nRanks; j++) mp->multiGpu |= all[j].pciKey != mine.pciKey;
-  std::vector<uint64_t*> table(c->nRanks), llTable(c->nRanks), l128Table(c->nRanks, nullptr);
-  for (int j = 0; j < c->nRanks; j++) {
-    // every rank must pick the same protocol for the same call
+  std::vector<uint64_t*> llTable(n), l128Table(n, nullptr), flagTable(n);
+  std::vector<char*> stageTable(n);
+  for (int j = 0; j < n; j++) {
+    // every rank must pick the same protocol, grid and layout for the same call
     if (all[j].llMaxBytes != mp->llMaxBytes || all[j].l128MaxBytes != mp->l128MaxBytes ||
         all[j].l128OneShotMax != mp->l128OneShotMax || all[j].protoMask != mp->protoMask) {
       warn("ncclCommInitRank : NCCL_PROTO / NBX_LL_MAX_BYTES / NBX_LL128_MAX_BYTES / NBX_LL128_ONESHOT_MAX differ "
            "across ranks");
       return ncclInvalidUsage;
     }
-    if (all[j].ring != mine.ring || all[j].ringPipeline != mine.ringPipeline ||
-        all[j].ringMaxGrid != mine.ringMaxGrid || all[j].groupBatch != mine.groupBatch) {
-      warn("ncclCommInitRank : NCCL_ALGO / NBX_RING_PIPELINE / NBX_RING_MAX_GRID / NBX_GROUP_BATCH differ across ranks");
+    if (all[j].ring != mine.ring || all[j].sliceBytes != mine.sliceBytes || all[j].slots != mine.slots ||
+        all[j].simpleGrid != mine.simpleGrid) {
+      warn("ncclCommInitRank : NCCL_ALGO / NBX_SIMPLE_MAX_GRID / NBX_SIMPLE_SLICE_BYTES / NBX_SIMPLE_SLOTS differ "
+           "across ranks");
       return ncclInvalidUsage;
     }
-    if (j == c->rank) {
-      table[j] = mp->flags;
+    if (j == me) {
       llTable[j] = mp->ll;
       l128Table[j] = mp->l128;
+      stageTable[j] = mp->stage;
+      flagTable[j] = mp->sflags;
       continue;
     }
     if (all[j].device != c->device) {
       int can = 0;
       HIPCHECK(hipDeviceCanAccessPeer(&can, c->device, all[j].device));
       if (!can) {
-        // every data path here is a kernel load/store of peer memory; there is
-        // no host-staged transport, so fail cleanly instead of faulting later
+        // every data path here is a kernel store to peer memory; there is no
+        // host-staged transport, so fail cleanly instead of faulting later
         warn("ncclCommInitRank : device %d cannot access peer device %d (no P2P)", c->device, all[j].device);
         return ncclSystemError;
       }
@@ -1089,52 +1035,31 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
       (void)hipGetLastError();
     }
     void* p = nullptr;
-    HIPCHECK(hipIpcOpenMemHandle(&p, all[j].flagsHandle, hipIpcMemLazyEnablePeerAccess));
-    mp->peerFlagMaps.push_back(p);
-    table[j] = (uint64_t*)p;
-    void* q = nullptr;
-    HIPCHECK(hipIpcOpenMemHandle(&q, all[j].llHandle, hipIpcMemLazyEnablePeerAccess));
-    mp->peerLLMaps.push_back(q);
-    llTable[j] = (uint64_t*)q;
+    NCCLCHECK(mpOpenPeer(mp, all[j].llHandle, &p));
+    llTable[j] = (uint64_t*)p;
     if (mp->l128) {
-      void* w = nullptr;
-      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].l128Handle, hipIpcMemLazyEnablePeerAccess));
-      mp->peerL128Maps.push_back(w);
-      l128Table[j] = (uint64_t*)w;
+      NCCLCHECK(mpOpenPeer(mp, all[j].l128Handle, &p));
+      l128Table[j] = (uint64_t*)p;
     }
-    if (j == (c->rank + 1) % c->nRanks) {   // the ring's right neighbour: this rank posts its progress there
-      void* w = nullptr;
-      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].ringHandle, hipIpcMemLazyEnablePeerAccess));
-      mp->rightRingProg = (uint64_t*)w;
-      if (mp->ring) {   // ... and its FIFO tail words
-        HIPCHECK(hipIpcOpenMemHandle(&w, all[j].fifoTailHandle, hipIpcMemLazyEnablePeerAccess));
-        mp->rightFifoTail = (uint64_t*)w;
-      }
-    }
-    if (mp->ring && j == (c->rank + c->nRanks - 1) % c->nRanks) {   // the left neighbour: its FIFO and head words
-      void* w = nullptr;
-      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].fifoHandle, hipIpcMemLazyEnablePeerAccess));
-      mp->leftFifo = w;
-      HIPCHECK(hipIpcOpenMemHandle(&w, all[j].fifoHeadHandle, hipIpcMemLazyEnablePeerAccess));
-      mp->leftFifoHead = (uint64_t*)w;
-    }
+    NCCLCHECK(mpOpenPeer(mp, all[j].stageHandle, &p));
+    stageTable[j] = (char*)p;
+    NCCLCHECK(mpOpenPeer(mp, all[j].sflagsHandle, &p));
+    flagTable[j] = (uint64_t*)p;
   }
-  HIPCHECK(hipMalloc((void**)&mp->peerFlagsDev, c->nRanks * sizeof(uint64_t*)));
-  HIPCHECK(hipMemcpy(mp->peerFlagsDev, table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
-  HIPCHECK(hipMalloc((void**)&mp->peerLLDev, c->nRanks * sizeof(uint64_t*)));
-  HIPCHECK(hipMemcpy(mp->peerLLDev, llTable.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
-  if (mp->l128) {
-    HIPCHECK(hipMalloc((void**)&mp->peerL128Dev, c->nRanks * sizeof(uint64_t*)));
-    HIPCHECK(hipMemcpy(mp->peerL128Dev, l128Table.data(), c->nRanks * sizeof(uint64_t*), hipMemcpyHostToDevice));
-  }
-  // everyone has mapped everyone before the first collective
-  int dummy = 0;
-  std::vector<int> sink(c->nRanks);
-  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), sink.data()));
-  NCCLCHECK(mpSetupShmx(c, id));
+  auto upload = [](void** dev, const void* host, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(dev, bytes);
+    return e != hipSuccess ? e : hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice);
+  };
+  HIPCHECK(upload((void**)&mp->peerLLDev, llTable.data(), n * sizeof(uint64_t*)));
+  if (mp->l128) HIPCHECK(upload((void**)&mp->peerL128Dev, l128Table.data(), n * sizeof(uint64_t*)));
+  HIPCHECK(upload((void**)&mp->peerStageDev, stageTable.data(), n * sizeof(char*)));
+  HIPCHECK(upload((void**)&mp->peerSFlagsDev, flagTable.data(), n * sizeof(uint64_t*)));
+  // every mapping checked, and everyone has mapped everyone, before the first collective
+  NCCLCHECK(mpVerifyMappings(c, all, stageTable));
   NCCLCHECK(mpLL128SelfTest(c));
-  info("comm %p rank %d nranks %d device %d: multi-process communicator ready", (void*)c, c->rank, c->nRanks,
-       c->device);
+  info("comm %p rank %d nranks %d device %d: multi-process communicator ready (Simple grid %d, slice %llu B, "
+       "staging %llu MiB)", (void*)c, me, n, c->device, mp->simpleGrid, (unsigned long long)mp->sliceBytes,
+       (unsigned long long)(mp->stageBytes >> 20));
   return ncclSuccess;
 }
 
@@ -1143,29 +1068,13 @@ void mpFree(ncclComm* c) {
   if (!mp) return;
   DevGuard g(c->device);
   (void)hipDeviceSynchronize();
-  for (auto& kv : mp->maps) retirePeerMapping(kv.second.base);
-  for (void* p : mp->peerFlagMaps) (void)hipIpcCloseMemHandle(p);
-  for (void* p : mp->peerLLMaps) (void)hipIpcCloseMemHandle(p);
-  for (void* p : mp->peerL128Maps) (void)hipIpcCloseMemHandle(p);
-  if (mp->rightRingProg) (void)hipIpcCloseMemHandle(mp->rightRingProg);
-  if (mp->rightFifoTail) (void)hipIpcCloseMemHandle(mp->rightFifoTail);
-  if (mp->leftFifo) (void)hipIpcCloseMemHandle(mp->leftFifo);
-  if (mp->leftFifoHead) (void)hipIpcCloseMemHandle(mp->leftFifoHead);
-  if (mp->fifo) (void)hipFree(mp->fifo);
-  if (mp->fifoTail) (void)hipFree(mp->fifoTail);
-  if (mp->fifoHead) (void)hipFree(mp->fifoHead);
-  if (mp->ringProg) (void)hipFree(mp->ringProg);
-  if (mp->ringState) (void)hipFree(mp->ringState);
-  if (mp->peerL128Dev) (void)hipFree(mp->peerL128Dev);
-  if (mp->l128) (void)hipFree(mp->l128);
-  if (mp->peerFlagsDev) (void)hipFree(mp->peerFlagsDev);
-  if (mp->peerLLDev) (void)hipFree(mp->peerLLDev);
-  if (mp->ll) (void)hipFree(mp->ll);
-  if (mp->epochs) (void)hipFree(mp->epochs);
-  if (mp->llState) (void)hipFree(mp->llState);
-  if (mp->flags) (void)hipFree(mp->flags);
+  for (void* p : mp->peerMaps) (void)hipIpcCloseMemHandle(p);
+  for (void* p : {(void*)mp->peerStageDev, (void*)mp->peerSFlagsDev, (void*)mp->scounters, (void*)mp->sflags,
+                  (void*)mp->stage, (void*)mp->peerL128Dev, (void*)mp->l128, (void*)mp->peerLLDev, (void*)mp->ll,
+                  (void*)mp->llState})
+    if (p) (void)hipFree(p);
+  if (mp->lastEvent) (void)hipEventDestroy(mp->lastEvent);
   if (mp->hostWords) (void)hipHostFree(mp->hostWords);
-  nbx::shmxClose(mp->shmx);
   nbx::bootstrapClose(mp->bs);
   delete mp;
   c->mp = nullptr;
@@ -1185,8 +1094,7 @@ MpProto mpProtoOf(const ncclComm* comm, const MpCall& c) {
                         mp->llMaxBytes, mp->l128MaxBytes, mp->l128OneShotMax);
 }
 
-// LL / LL128 protocols: small and medium collectives in one kernel, no host
-// exchange (nbx_ll.h).
+// LL / LL128 protocols: small and medium collectives in one kernel (nbx_ll.h).
 ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
@@ -1194,11 +1102,6 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
   const uint64_t slotBytes = (uint64_t)c.count * (uint64_t)eb;
   size_t off0, per;
   blockRange(c.count, eb, n, 0, &off0, &per);
-  if (c.send == nullptr || (c.recv == nullptr && (c.kind != kReduce || me == c.root))) {
-    warn("rank %d passed a NULL buffer", me);
-    return ncclInvalidArgument;
-  }
-  ++mp->seq;
   nbx::LLArgs la{};
   la.send = c.send;
   la.recv = c.recv;
@@ -1237,298 +1140,79 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
   return nbx::launchLLColl(c.dt, c.op, la, c.stream);
 }
 
-// Simple path, step 0: allgather the call (kind, type, op, count) and the IPC
-// handles of every rank's buffers, and check that the ranks agree.
-// `flags` is this rank's kMpContig bit, exchanged so that group batching
-// decisions are identical on every rank.
-constexpr int32_t kMpContig = 1;   // same stream as the previous call of the group
-ncclResult_t mpExchangeCall(ncclComm* comm, const MpCall& c, int32_t flags, std::vector<MpCallInfo>* all) {
+// Simple protocol: one kernel (nbx_simple.h). Blocks: AllReduce / Reduce the
+// direct schedule's 16-B aligned blocks (blockRange; the ring's chunks are the
+// same blocks), ReduceScatter the API's recvcount blocks, ring Reduce the
+// whole message as one block (a chain). A call of B-byte blocks runs on
+// min(grid, B / 4 KiB) workgroups in rounds of one slice per workgroup and
+// block, the slice at most the staging slice — every rank derives the same
+// numbers from the same arguments.
+ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
-  const uint64_t seq = ++mp->seq;
-  MpCallInfo mine{};
-  mine.seq = seq;
-  mine.kind = (int32_t)c.kind;
-  mine.dt = (int32_t)c.dt;
-  mine.op = c.op.op;
-  mine.root = c.root;
-  mine.count = c.count;
-  mine.flags = flags;
-  mine.hasSend = c.count > 0 && c.send != nullptr;
-  mine.hasRecv = c.count > 0 && c.recv != nullptr;
-  if (mine.hasSend) NCCLCHECK(ipcHandleOf(c.send, &mine.sendH, &mine.sendOff));
-  if (mine.hasRecv) NCCLCHECK(ipcHandleOf(c.recv, &mine.recvH, &mine.recvOff));
-  all->assign(n, MpCallInfo{});
-  NCCLCHECK(mpExchange(mp, seq, &mine, sizeof(mine), all->data()));
-  for (int j = 0; j < n; j++) {
-    const MpCallInfo& a = (*all)[j];
-    if (a.seq != seq || a.kind != mine.kind || a.dt != mine.dt || a.op != mine.op || a.root != c.root ||
-        a.count != c.count) {
-      warn("collective mismatch across ranks (rank %d vs %d)", j, me);
-      return ncclInvalidUsage;
-    }
-  }
-  return ncclSuccess;
-}
-
-// Bound the mapping cache: a peer's freed-and-reallocated buffers come back
-// with new handles, and every open mapping pins the peer's old allocation.
-// Past the bound, wait for this device's work (no kernel in flight uses a
-// mapping), then close every mapping not used since the call before `seq`.
-ncclResult_t mpEvictMappings(MpState* mp, uint64_t seq, bool capturing) {
-  if (mp->maps.size() <= mp->mapsMax || capturing) return ncclSuccess;
-  HIPCHECK(hipDeviceSynchronize());
-  for (auto it = mp->maps.begin(); it != mp->maps.end();) {
-    if (it->second.lastUse != MpState::kPinned && it->second.lastUse + 1 < seq) {
-      retirePeerMapping(it->second.base);
-      it = mp->maps.erase(it);
-    } else {
-      ++it;
-    }
-  }
-  return ncclSuccess;
-}
-
-// Every rank's send / recv base for one call (own buffers as passed, peers'
-// through the IPC mapping cache).
-ncclResult_t mpMapCall(ncclComm* comm, const MpCall& c, const std::vector<MpCallInfo>& all, bool capturing,
-                       std::vector<const char*>* sendP, std::vector<char*>* recvP) {
-  MpState* mp = comm->mp;
-  const int n = comm->nRanks, me = comm->rank;
-  sendP->assign(n, nullptr);
-  recvP->assign(n, nullptr);
-  for (int j = 0; j < n; j++) {
-    if (j == me) {
-      (*sendP)[j] = (const char*)c.send;
-      (*recvP)[j] = (char*)c.recv;
-      continue;
-    }
-    void* b = nullptr;
-    if (all[j].hasSend) {
-      NCCLCHECK(mapPeer(mp, j, all[j].sendH, &b, capturing));
-      (*sendP)[j] = (const char*)b + all[j].sendOff;
-    }
-    if (all[j].hasRecv) {
-      NCCLCHECK(mapPeer(mp, j, all[j].recvH, &b, capturing));
-      (*recvP)[j] = (char*)b + all[j].recvOff;
-    }
-  }
-  for (int j = 0; j < n; j++)
-    if (!(*sendP)[j] || ((c.kind != kReduce || j == c.root) && !(*recvP)[j])) {
-      warn("rank %d passed a NULL buffer", j);
-      return ncclInvalidArgument;
-    }
-  return ncclSuccess;
-}
-
-// This rank's block of the direct schedule: block `me` of every rank's send
-// buffer in fold order, and where the folded block goes. AllReduce /
-// ReduceScatter fold in ring order me+1, ..., me; Reduce in chain order
-// root+1, ..., root for every block (reduce.h:44-67). AllReduce with
-// n <= NBX_MAX_DSTS pushes the block into every rank's output (push-gather,
-// all_reduce.h:343-360), so there is no separate gather phase.
-RankBlock mpDirectBlock(const MpCall& c, int n, int me, const std::vector<const char*>& sendP,
-                        const std::vector<char*>& recvP) {
-  const int eb = typeSize(c.dt);
-  const size_t total = c.kind == kReduceScatter ? c.count * (size_t)n : c.count;
-  RankBlock b;
-  size_t off;
+  const uint64_t eb = (uint64_t)typeSize(c.dt);
+  nbx::SimpleArgs sa{};
+  sa.send = c.send;
+  sa.recv = c.recv;
   if (c.kind == kReduceScatter) {
-    off = (size_t)me * c.count;
-    b.len = c.count;
+    sa.blockElts = c.count;
+    sa.total = (uint64_t)c.count * (uint64_t)n;
+  } else if (c.kind == kReduce && mp->ring) {
+    sa.blockElts = c.count;
+    sa.total = c.count;
   } else {
-    blockRange(total, eb, n, me, &off, &b.len);
+    size_t o0, per;
+    blockRange(c.count, (int)eb, n, 0, &o0, &per);
+    sa.blockElts = per;
+    sa.total = c.count;
   }
-  if (b.len == 0) return b;
-  const int first = (c.kind == kReduce ? c.root : me) + 1;
-  for (int k = 0; k < n; k++) b.srcs.push_back(sendP[(first + k) % n] + off * (size_t)eb);
-  if (c.kind == kReduceScatter) b.dsts.push_back(recvP[me]);
-  else if (c.kind == kReduce) b.dsts.push_back(recvP[c.root] + off * (size_t)eb);
-  else if (n > NBX_MAX_DSTS) b.dsts.push_back(recvP[me] + off * (size_t)eb);
-  else
-    for (int k = 0; k < n; k++) b.dsts.push_back(recvP[(me + k) % n] + off * (size_t)eb);
-  return b;
+  const uint64_t blockBytes = std::min<uint64_t>(sa.blockElts, sa.total) * eb;
+  if (blockBytes == 0) return ncclSuccess;
+  uint64_t grid = (blockBytes + nbx::kSimpleMinSliceBytes - 1) / nbx::kSimpleMinSliceBytes;
+  grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, (uint64_t)mp->simpleGrid));
+  uint64_t slice = ((blockBytes + grid - 1) / grid + 15) & ~(uint64_t)15;
+  slice = std::min<uint64_t>(slice, mp->sliceBytes);
+  sa.sliceBytes = slice;
+  sa.nRounds = (blockBytes + grid * slice - 1) / (grid * slice);
+  sa.peerStage = mp->peerStageDev;
+  sa.peerFlags = mp->peerSFlagsDev;
+  sa.counters = mp->scounters;
+  sa.stageSlice = mp->sliceBytes;
+  sa.abortWord = mp->hostWordsDev;
+  sa.errWord = mp->hostWordsDev + 1;
+  sa.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
+  sa.rank = me;
+  sa.nRanks = n;
+  sa.mode = c.kind == kAllReduce ? nbx::kSimpleAllReduce
+            : c.kind == kReduceScatter ? nbx::kSimpleReduceScatter
+                                       : nbx::kSimpleReduce;
+  sa.root = c.root;
+  sa.slots = mp->slots;
+  sa.gridMax = mp->simpleGrid;
+  return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
 }
 
-// NCCL_ALGO=Ring ReduceScatter / Reduce through the step FIFO (kRingFifo):
-// every rank's buffers 16-B aligned (decided from the exchanged offsets, so
-// every rank decides alike) and, for ReduceScatter, blocks of whole 16-B packs
-// (block c starts at c * recvcount elements). Otherwise the direct schedule.
-bool mpRingFifoEligible(const MpCall& c, int n, const std::vector<MpCallInfo>& all) {
-  if (c.kind != kReduceScatter && c.kind != kReduce) return false;
-  const int eb = typeSize(c.dt);
-  if (c.kind == kReduceScatter && ((uint64_t)c.count * (uint64_t)eb) % 16 != 0) return false;
-  for (int j = 0; j < n; j++) {
-    const MpCallInfo& ai = all[j];
-    if ((ai.sendOff & 15u) != 0) return false;
-    if (ai.hasRecv && (ai.recvOff & 15u) != 0) return false;
-  }
-  return true;
-}
-
-// Simple path, after the exchange: map, barriers, reduce (direct or ring), gather.
-ncclResult_t mpRunSimple(ncclComm* comm, const MpCall& c, const std::vector<MpCallInfo>& all) {
-  MpState* mp = comm->mp;
-  const int n = comm->nRanks, me = comm->rank;
-  const int eb = typeSize(c.dt);
-  hipStream_t stream = c.stream;
-  if (c.count == 0) return ncclSuccess;
-  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
-  HIPCHECK(hipStreamIsCapturing(stream, &capture));
-  const bool capturing = capture != hipStreamCaptureStatusNone;
-  NCCLCHECK(mpEvictMappings(mp, all[me].seq, capturing));
-  std::vector<const char*> sendP;
-  std::vector<char*> recvP;
-  const size_t mapsBefore = mp->maps.size();
-  NCCLCHECK(mpMapCall(comm, c, all, capturing, &sendP, &recvP));
-  if (traceOn()) {   // NBX_TRACE=1: every rank's send / recv as this rank sees them
-    auto hsh = [](const hipIpcMemHandle_t& h) {
-      uint64_t x = 1469598103934665603ull;
-      for (size_t i = 0; i < sizeof(h); i++) x = (x ^ (unsigned char)((const char*)&h)[i]) * 1099511628211ull;
-      return x;
-    };
-    for (int j = 0; j < n; j++)
-      NBX_TRACE("mp simple seq=%llu rank %d count=%zu: rank %d send %p (h %016llx off %llu) recv %p (h %016llx off %llu)%s",
-                (unsigned long long)all[me].seq, me, c.count, j, (const void*)sendP[j],
-                (unsigned long long)hsh(all[j].sendH), (unsigned long long)all[j].sendOff, (void*)recvP[j],
-                (unsigned long long)hsh(all[j].recvH), (unsigned long long)all[j].recvOff,
-                mp->maps.size() != mapsBefore ? " [new mapping]" : "");
-  }
-  // 1. every rank's stream has reached the collective (its inputs are written,
-  //    its output may be written by peers)
-  NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
-  const size_t total = c.kind == kReduceScatter ? c.count * (size_t)n : c.count;
-  const bool push = c.kind == kAllReduce && n <= NBX_MAX_DSTS;
-  if (c.kind == kAllReduce && n > 2 && mp->ring) {
-    // 2'. ring reduce-scatter (all_reduce.h:60-79): chunk c starts at rank c+1 and
-    // visits c+2, ..., c; at step s this rank folds chunk c = me-2-s as
-    // Fn(pre(local), received) — NCCL's operand order (recvReduceSend: srcs[0] is
-    // the local input, srcs[1] the received partial) — into its own recv buffer,
-    // where the right neighbour reads it at step s+1. Step 0 reads the left
-    // neighbour's raw input (its `send`, PreOp applies to both sources); the last
-    // step (c == me) applies postOp and, with push, stores into every output.
-    // Every rank works on a different chunk at each step, so all ring links
-    // carry 1/n of the data concurrently.
-    const int left = (me + n - 1) % n;
-    // pipelined: one kernel, slices flow through the ring on device progress
-    // words (nbx_ring.h). It needs 16-B aligned buffers, and every rank must
-    // choose it or none: decided from the exchanged offsets of all ranks
-    // (allocation bases are >= 256-B aligned, so an offset's alignment is the
-    // pointer's).
-    const int nOuts = push ? n : 1;
-    bool aligned = true;
-    for (const MpCallInfo& ai : all) aligned &= ((ai.sendOff | ai.recvOff) & 15u) == 0;
-    if (mp->ringPipeline && aligned) {
-      size_t o0, per;
-      blockRange(total, eb, n, 0, &o0, &per);
-      const uint64_t epp = (uint64_t)(16 / eb);
-      const uint64_t maxPacks = per / epp;
-      uint64_t grid = (maxPacks + 1023) / 1024;   // slices of >= 16 KiB
-      if (grid < 1) grid = 1;
-      if (grid > mp->ringMaxGrid) grid = mp->ringMaxGrid;
-      nbx::RingArgs ra{};
-      ra.sendMe = sendP[me];
-      ra.sendLeft = sendP[left];
-      ra.recvMe = recvP[me];
-      ra.recvLeft = recvP[left];
-      for (int k = 0; k < nOuts; k++) ra.outs[k] = recvP[(me + k) % n];
-      ra.myProgress = mp->ringProg;
-      ra.rightProgress = mp->rightRingProg;
-      ra.state = mp->ringState;
-      ra.total = total;
-      ra.blockElts = per;
-      ra.slicePacks = (maxPacks + grid - 1) / grid;
-      ra.abortWord = mp->hostWordsDev;
-      ra.errWord = mp->hostWordsDev + 1;
-      ra.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
-      ra.rank = me;
-      ra.nRanks = n;
-      ra.nOuts = nOuts;
-      NCCLCHECK(nbx::launchRingAllReduce(c.dt, c.op, ra, (unsigned)grid, stream));
-    } else {
-    std::vector<void*> pushDsts;
-    for (int st = 0; st < n - 1; st++) {
-      const int ch = ((me - 2 - st) % n + n) % n;
-      size_t off, len;
-      blockRange(total, eb, n, ch, &off, &len);
-      if (len > 0) {
-        const void* srcs[2] = {sendP[me] + off * (size_t)eb,
-                               st == 0 ? (const void*)(sendP[left] + off * (size_t)eb)
-                                       : (const void*)(recvP[left] + off * (size_t)eb)};
-        void* dsts[1] = {recvP[me] + off * (size_t)eb};
-        const bool last = st == n - 2;
-        pushDsts.clear();
-        for (int k = 0; k < n; k++) pushDsts.push_back(recvP[(me + k) % n] + off * (size_t)eb);
-        NCCLCHECK(nbx::reduceMultiEx(last && push ? pushDsts.data() : dsts, last && push ? n : 1, srcs, 2, len,
-                                     c.dt, c.op, st == 0 ? 2 : 1, last ? 1 : 0, (ncclStream_t)stream,
-                                     nbx::kReduceAcquireSystem));
-      }
-      if (st < n - 2) NCCLCHECK(mpSignalWait(comm, kSlotRing, 1ull << left, stream));
-    }
-    }
-  } else if (mp->ring && mp->ringPipeline && n > 1 && mpRingFifoEligible(c, n, all)) {
-    // 2''. ring ReduceScatter / chain Reduce through the step FIFO (nbx_ring.h
-    // kRingFifo; reduce_scatter.h:13-66, reduce.h:12-68)
-    const int left = (me + n - 1) % n;
-    const uint64_t epp = (uint64_t)(16 / eb);
-    const uint64_t blockPacks = ((uint64_t)c.count + epp - 1) / epp;   // RS: recvcount, Reduce: count
-    uint64_t grid = (blockPacks + 1023) / 1024;   // slices of >= 16 KiB
-    if (grid < 1) grid = 1;
-    if (grid > mp->ringMaxGrid) grid = mp->ringMaxGrid;
-    nbx::RingFifoArgs fa{};
-    fa.sendMe = sendP[me];
-    fa.sendLeft = sendP[left];
-    fa.recv = recvP[me];
-    fa.fifoMe = mp->fifo;
-    fa.fifoLeft = mp->leftFifo;
-    fa.myTail = mp->fifoTail;
-    fa.rightTail = mp->rightFifoTail;
-    fa.myHead = mp->fifoHead;
-    fa.leftHead = mp->leftFifoHead;
-    fa.state = mp->ringState;
-    fa.blockElts = c.count;
-    fa.slicePacks = (blockPacks + grid - 1) / grid;
-    fa.abortWord = mp->hostWordsDev;
-    fa.errWord = mp->hostWordsDev + 1;
-    fa.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
-    fa.rank = me;
-    fa.nRanks = n;
-    fa.root = c.root;
-    fa.mode = c.kind == kReduceScatter ? nbx::kRingFifoReduceScatter : nbx::kRingFifoReduce;
-    NCCLCHECK(nbx::launchRingFifo(c.dt, c.op, fa, (unsigned)grid, stream));
-  } else {
-    // 2. direct reduce of this rank's block
-    const RankBlock b = mpDirectBlock(c, n, me, sendP, recvP);
-    if (b.len > 0)
-      NCCLCHECK(nbx::reduceMultiEx(b.dsts.data(), (int)b.dsts.size(), b.srcs.data(), n, b.len, c.dt, c.op, n, 1,
-                                   (ncclStream_t)stream, nbx::kReduceAcquireSystem));
-  }
-  // 3. AllReduce with n > NBX_MAX_DSTS: gather the peers' reduced blocks
-  if (c.kind == kAllReduce && !push) {
-    NCCLCHECK(mpBarrier(comm, kSlotReduced, stream));
-    nbxDevRedOpFull copyOp{nbxDevSum, 0, 0};
-    for (int k = 1; k < n; k++) {
-      const int j = (me + k) % n;
-      size_t o, l;
-      blockRange(total, eb, n, j, &o, &l);
-      if (l == 0) continue;
-      void* d[1] = {recvP[me] + o * (size_t)eb};
-      const void* s1[1] = {recvP[j] + o * (size_t)eb};
-      NCCLCHECK(nbx::reduceMultiEx(d, 1, s1, 1, l * (size_t)eb, ncclUint8, copyOp, 0, 0, (ncclStream_t)stream,
-                                   nbx::kReduceAcquireSystem));
-    }
-  }
-  // 4. nobody reuses its buffers while a peer may still read them
-  NCCLCHECK(mpBarrier(comm, kSlotDone, stream));
-  return ncclSuccess;
-}
-
+// One call of a multi-process communicator, ordered after the previous one
+// (a call on another stream waits for it: the kernels share the
+// communicator's device-resident sequencing, as NCCL's calls on one
+// communicator never overlap). Inside a stream capture the graph's own edges
+// order the captured calls; nothing is recorded there.
 ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
+  MpState* mp = comm->mp;
+  if (c.count == 0) return ncclSuccess;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(c.stream, &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (!capturing && mp->haveLast && mp->lastStream != c.stream)
+    HIPCHECK(hipStreamWaitEvent(c.stream, mp->lastEvent, 0));
   const MpProto proto = mpProtoOf(comm, c);
-  if (proto != kMpSimple) return mpLaunchLL(comm, c, proto);
-  std::vector<MpCallInfo> all;
-  NCCLCHECK(mpExchangeCall(comm, c, 0, &all));
-  return mpRunSimple(comm, c, all);
+  NCCLCHECK(proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto));
+  if (!capturing) {
+    HIPCHECK(hipEventRecord(mp->lastEvent, c.stream));
+    mp->lastStream = c.stream;
+    mp->haveLast = true;
+  }
+  return ncclSuccess;
 }
 
 // LL128 correctness probe at communicator creation. LL128 relies on a 64-byte
@@ -1615,142 +1299,30 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
   return ncclSuccess;
 }
 
+
 // ---------------------------------------------------------------------------
-// Groups on a multi-process communicator. Inside ncclGroupStart/End the calls
-// are queued and run at the outermost ncclGroupEnd, in order: every
-// Simple-protocol call is exchanged first (one allgather each, flags
-// included), then maximal runs of direct-schedule calls that every rank issued
-// on one stream and that touch no buffer an earlier member of the run writes
-// (or write one it reads) run as ONE exchange — one enter barrier, one
-// nbxReduceMultiBatch per (datatype, op), one done barrier — the way NCCL packs
-// a group's collectives into one kernel's work list (enqueue.cc:67-91
-// appendWorkElemColl). Every decision uses only exchanged data, so all ranks
-// make the same one. LL / LL128 calls and the ring / gather schedules run
-// one by one, in order. NBX_GROUP_BATCH=0 runs every call at enqueue instead.
+// Groups on a multi-process communicator (group.cc:82-103 semantics): calls
+// inside ncclGroupStart/End are queued and launched, in order, at the
+// outermost ncclGroupEnd, each as its own kernel on its stream. No host
+// exchange keeps the ranks in step: every kernel's sequencing is per
+// workgroup and device-resident, so the ranks only have to issue the same
+// calls in the same order, as NCCL requires.
 thread_local std::vector<ncclComm*> t_groupMpComms;
-constexpr size_t kMaxMpBatch = 64;
-
-bool groupBatchEnabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("NBX_GROUP_BATCH");
-    return !(v && std::strcmp(v, "0") == 0);
-  }();
-  return on;
-}
-
-// Bytes of every rank's buffers a call reads (send) and writes (recv),
-// identified by (IPC handle of the allocation, offset range).
-struct HSpan {
-  hipIpcMemHandle_t h;
-  uint64_t lo, hi;
-  bool write;
-};
-
-void callSpans(const MpCall& c, int n, const std::vector<MpCallInfo>& all, std::vector<HSpan>* out) {
-  const uint64_t eb = (uint64_t)typeSize(c.dt);
-  const uint64_t sendBytes = (c.kind == kReduceScatter ? (uint64_t)c.count * (uint64_t)n : c.count) * eb;
-  const uint64_t recvBytes = (uint64_t)c.count * eb;
-  for (const MpCallInfo& a : all) {
-    if (a.hasSend) out->push_back({a.sendH, a.sendOff, a.sendOff + sendBytes, false});
-    if (a.hasRecv) out->push_back({a.recvH, a.recvOff, a.recvOff + recvBytes, true});
-  }
-}
-
-bool hspansConflict(const std::vector<HSpan>& a, const std::vector<HSpan>& b) {
-  for (const HSpan& x : a)
-    for (const HSpan& y : b)
-      if ((x.write || y.write) && x.lo < y.hi && y.lo < x.hi && std::memcmp(&x.h, &y.h, sizeof(x.h)) == 0)
-        return true;
-  return false;
-}
-
-// One batched exchange over calls[lo, hi) (all Simple, direct schedule, one stream).
-ncclResult_t mpRunBatch(ncclComm* comm, const std::vector<MpCall>& calls,
-                        const std::vector<std::vector<MpCallInfo>>& alls, size_t lo, size_t hi) {
-  MpState* mp = comm->mp;
-  const int n = comm->nRanks, me = comm->rank;
-  hipStream_t stream = calls[lo].stream;
-  hipStreamCaptureStatus capture = hipStreamCaptureStatusNone;
-  HIPCHECK(hipStreamIsCapturing(stream, &capture));
-  const bool capturing = capture != hipStreamCaptureStatusNone;
-  NCCLCHECK(mpEvictMappings(mp, alls[lo][me].seq, capturing));
-  std::vector<RankBlock> blocks;
-  std::vector<const PendingColl*> colls;
-  for (size_t k = lo; k < hi; k++) {
-    std::vector<const char*> sendP;
-    std::vector<char*> recvP;
-    NCCLCHECK(mpMapCall(comm, calls[k], alls[k], capturing, &sendP, &recvP));
-    blocks.push_back(mpDirectBlock(calls[k], n, me, sendP, recvP));
-    colls.push_back(&calls[k]);
-  }
-  NBX_TRACE("mp group batch of %zu collectives", hi - lo);
-  NCCLCHECK(mpBarrier(comm, kSlotEnter, stream));
-  NCCLCHECK(foldBlocksBatched(colls, blocks, n, stream));
-  NCCLCHECK(mpBarrier(comm, kSlotDone, stream));
-  return ncclSuccess;
-}
-
-ncclResult_t runMpGroupImpl(ncclComm* comm) {
-  MpState* mp = comm->mp;
-  const int n = comm->nRanks;
-  std::vector<MpCall> calls;
-  calls.swap(mp->group);
-  const size_t m = calls.size();
-  std::vector<MpProto> protos(m);
-  std::vector<std::vector<MpCallInfo>> alls(m);
-  for (size_t k = 0; k < m; k++) {
-    protos[k] = mpProtoOf(comm, calls[k]);
-    if (protos[k] != kMpSimple) continue;
-    const int32_t flags = (k > 0 && protos[k - 1] == kMpSimple && calls[k].stream == calls[k - 1].stream) ? kMpContig : 0;
-    NCCLCHECK(mpExchangeCall(comm, calls[k], flags, &alls[k]));
-  }
-  auto directSimple = [&](size_t k) {
-    const MpCall& c = calls[k];
-    return protos[k] == kMpSimple && c.count > 0 && !(c.kind == kAllReduce && n > NBX_MAX_DSTS) &&
-           !(c.kind == kAllReduce && n > 2 && mp->ring) &&
-           !(mp->ring && mp->ringPipeline && mpRingFifoEligible(c, n, alls[k]));   // ring RS / Reduce: alone
-  };
-  auto contigEverywhere = [&](size_t k) {
-    for (const MpCallInfo& a : alls[k])
-      if (!(a.flags & kMpContig)) return false;
-    return true;
-  };
-  size_t k = 0;
-  while (k < m) {
-    if (protos[k] != kMpSimple) {
-      NCCLCHECK(mpLaunchLL(comm, calls[k], protos[k]));
-      k++;
-      continue;
-    }
-    size_t j = k + 1;
-    if (directSimple(k)) {
-      std::vector<HSpan> spans;
-      callSpans(calls[k], n, alls[k], &spans);
-      for (; j < m && j - k < kMaxMpBatch; j++) {
-        if (!directSimple(j) || !contigEverywhere(j)) break;
-        std::vector<HSpan> sj;
-        callSpans(calls[j], n, alls[j], &sj);
-        if (hspansConflict(spans, sj)) break;
-        spans.insert(spans.end(), sj.begin(), sj.end());
-      }
-    }
-    if (j == k + 1) NCCLCHECK(mpRunSimple(comm, calls[k], alls[k]));
-    else NCCLCHECK(mpRunBatch(comm, calls, alls, k, j));
-    k = j;
-  }
-  return ncclSuccess;
-}
 
 ncclResult_t runMpGroup(ncclComm* comm) {
   DevGuard g(comm->device);
-  ncclResult_t r;
+  std::vector<MpCall> calls;
+  calls.swap(comm->mp->group);
+  ncclResult_t r = ncclSuccess;
   try {
-    r = runMpGroupImpl(comm);
+    for (const MpCall& c : calls) {
+      r = runMpColl(comm, c);
+      if (r != ncclSuccess) break;
+    }
   } catch (const std::exception& e) {
     warn("internal exception: %s", e.what());
     r = ncclInternalError;
   }
-  comm->mp->group.clear();
   if (r != ncclSuccess) comm->asyncError.store(r);
   return r;
 }
@@ -1786,7 +1358,7 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
   }
   if (comm->mp) {
     const MpCall call{kind, sendbuff, recvbuff, count, dt, opFull, root, stream};
-    if (t_groupDepth > 0 && comm->mp->groupBatch) {   // run at the outermost ncclGroupEnd
+    if (t_groupDepth > 0) {   // run at the outermost ncclGroupEnd
       if (comm->mp->group.empty()) t_groupMpComms.push_back(comm);
       comm->mp->group.push_back(call);
       return ncclSuccess;
@@ -2141,35 +1713,6 @@ NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slot
                                    uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax) {
   return (int)chooseProtoFor(protoMask, twoShotKind != 0, slotBytes, blockBytes, nRanks, llMaxBytes, ll128MaxBytes,
                              ll128OneShotMax);
-}
-
-NBX_EXPORT ncclResult_t nbxShmxSelfTest(const char* name, int rank, int nranks, int rounds, int jitterUs) {
-  if (name == nullptr || nranks < 1 || rank < 0 || rank >= nranks || rounds < 0) return ncclInvalidArgument;
-  constexpr size_t kMax = 256;
-  nbx::ShmExchange* x = nullptr;
-  if (rank == 0) {
-    x = nbx::shmxOpen(name, 0, nranks, kMax, true);
-  } else {
-    for (int i = 0; i < 20000 && x == nullptr; i++) {   // wait for rank 0's segment (<= ~20 s)
-      x = nbx::shmxOpen(name, rank, nranks, kMax, false);
-      if (!x) usleep(1000);
-    }
-  }
-  if (!x) return ncclSystemError;
-  std::mt19937 rng(1234u + (unsigned)rank);
-  std::vector<unsigned char> mine(kMax), all(kMax * (size_t)nranks);
-  ncclResult_t r = ncclSuccess;
-  for (int k = 1; k <= rounds && r == ncclSuccess; k++) {
-    const size_t len = 1 + (size_t)(k * 37) % kMax;
-    for (size_t i = 0; i < len; i++) mine[i] = (unsigned char)(rank * 31 + k * 7 + (int)i);
-    if (jitterUs > 0) usleep(rng() % (unsigned)jitterUs);
-    r = nbx::shmxAllGather(x, (uint64_t)(3 * k + (k % 2)), mine.data(), len, all.data(), 60.0, nullptr);
-    for (int j = 0; r == ncclSuccess && j < nranks; j++)
-      for (size_t i = 0; i < len; i++)
-        if (all[(size_t)j * len + i] != (unsigned char)(j * 31 + k * 7 + (int)i)) r = ncclInternalError;
-  }
-  nbx::shmxClose(x);
-  return r;
 }
 
 NBX_EXPORT ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds) {

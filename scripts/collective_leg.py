@@ -339,7 +339,7 @@ def main():
     if "NBX_BENCH_DEVICE" in os.environ:   # rehearsal: every rank on one GPU, keep LL/LL128 grids co-resident
         os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
         os.environ.setdefault("NBX_LL_MAX_GRID", "64")
-        os.environ.setdefault("NBX_RING_MAX_GRID", "64")
+        os.environ.setdefault("NBX_SIMPLE_MAX_GRID", "32")
     for line in sys.stdin:
         parts = line.split()
         if not parts:

@@ -39,36 +39,3 @@ def test_bootstrap_rejects_bad_args(nbx):
     assert lib.nbxBootstrapSelfTest(None, 0, 1, 1) == 4
     empty = nbx.ncclUniqueId()
     assert lib.nbxBootstrapSelfTest(ctypes.byref(empty), 0, 1, 1) == 4   # no root in the id
-
-
-def _shmx_rank(name, rank, n, rounds, jitter, q):
-    from tests.conftest import load_package
-    nbx = load_package()
-    lib = nbx.load_library()
-    lib.nbxShmxSelfTest.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    q.put((rank, lib.nbxShmxSelfTest(name.encode(), rank, n, rounds, jitter)))
-
-
-@pytest.mark.parametrize("n,rounds,jitter", [(1, 50, 0), (2, 400, 0), (5, 200, 200), (8, 100, 500)])
-def test_shm_exchange_rounds(nbx, n, rounds, jitter):
-    """The Simple path's per-call host exchange through /dev/shm: rank-stamped
-    payloads of varying length, exchange numbers with gaps (LL calls in
-    between skip numbers), random per-rank delays — every contribution
-    verified, no rank overwriting a payload a slower peer still reads."""
-    import os
-    name = f"/nbx-shmx-test-{os.getpid()}-{n}"
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=_shmx_rank, args=(name, r, n, rounds, jitter, q)) for r in range(n)]
-    for p in procs:
-        p.start()
-    try:
-        res = dict(q.get(timeout=180) for _ in range(n))
-        for p in procs:
-            p.join(timeout=60)
-    finally:
-        try:
-            os.unlink("/dev/shm" + name)
-        except OSError:
-            pass
-    assert res == {r: 0 for r in range(n)}

@@ -50,7 +50,8 @@ def test_all_kernels_present(kernels):
     assert len(packs) == 42 * 16           # 8 source counts x {small, big} tiles
     shifted = [n for n in names if "kReduceShifted" in n]
     assert len(shifted) == 42 * (1 + 8)    # realigning kernels: run-time count, and one per source count 1..8
-    assert any("kPeerBarrier" in n for n in names)
+    simple = [n for n in names if "kSimpleColl" in n or "kSimpleRing" in n]
+    assert len(simple) == 42 * 2           # Simple protocol: direct and ring schedule per functor
 
 
 def test_no_scratch_and_vgpr_budget(kernels):

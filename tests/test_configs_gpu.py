@@ -227,7 +227,7 @@ def test_configs_d_e_8_ranks_full_size(nbx, oracle, monkeypatch, algo):
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "300")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "240")
     monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
-    monkeypatch.setenv("NBX_RING_MAX_GRID", "64")    # 8 ranks' persistent ring grids co-resident on one GPU
+    monkeypatch.setenv("NBX_SIMPLE_MAX_GRID", "32")    # 8 ranks' Simple grids co-resident on one GPU
     monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
     n = N_RANKS
     uid = nbx.get_unique_id()

@@ -98,26 +98,26 @@ def _blocks(count, eb, n):
     return [(min(count, per * b), min(count, per * b + per)) for b in range(n)]
 
 
-@pytest.mark.parametrize("n,algo,proto,cache", [(2, "direct", "LL,Simple", ""), (3, "direct", "LL,Simple", ""),
-                                                (3, "ring", "LL,Simple", ""), (4, "ring", "LL,Simple", ""),
-                                                (5, "ring", "LL,Simple", ""), (4, "ring-steps", "LL,Simple", ""),
-                                                (3, "direct", "", ""), (3, "direct", "LL,Simple", "2")])
-def test_multiprocess_collectives(nbx, oracle, n, algo, proto, cache, monkeypatch):
+@pytest.mark.parametrize("n,algo,proto,slice_", [(2, "direct", "LL,Simple", ""), (3, "direct", "LL,Simple", ""),
+                                                 (3, "ring", "LL,Simple", ""), (4, "ring", "LL,Simple", ""),
+                                                 (5, "ring", "LL,Simple", ""), (4, "direct", "LL,Simple", "4096"),
+                                                 (3, "direct", "", ""), (9, "direct", "LL,Simple", "")])
+def test_multiprocess_collectives(nbx, oracle, n, algo, proto, slice_, monkeypatch):
     """NCCL_ALGO=Ring: NCCL's ring order (chunk c from rank c+1 to c, Fn(local,
     received)); for the commutative ops tested it is bit-identical to the
     oracle's left fold in the order c+1, ..., c. NCCL_PROTO=LL,Simple keeps the
     40009-element messages on the Simple (direct / ring) path; the default
-    sends most of them through LL128. NBX_IPC_CACHE_MAX=2 makes nearly every
-    Simple call close and re-open peer mappings (fresh buffers per case)."""
+    sends most of them through LL128. NBX_SIMPLE_SLICE_BYTES=4096 with a grid of
+    2 makes every call run many rounds through the 2 staging slots; 9 ranks:
+    more sources than the 8-source reduce kernels (the fold runs in groups)."""
     # bounded waits everywhere: a failing rank must not strand its peers
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
     monkeypatch.setenv("NCCL_PROTO", proto)
-    monkeypatch.setenv("NCCL_ALGO", "Ring" if algo.startswith("ring") else "")
-    # ring: the pipelined kernel (nbx_ring.h); ring-steps: one kernel + barrier per step
-    monkeypatch.setenv("NBX_RING_PIPELINE", "0" if algo == "ring-steps" else "1")
-    monkeypatch.setenv("NBX_IPC_CACHE_MAX", cache)
+    monkeypatch.setenv("NCCL_ALGO", "Ring" if algo == "ring" else "")
+    monkeypatch.setenv("NBX_SIMPLE_SLICE_BYTES", slice_)
+    monkeypatch.setenv("NBX_SIMPLE_MAX_GRID", "2" if slice_ else "")
     res = _run_ranks(nbx, n, _child)
     _check_cases(oracle, n, res)
 
@@ -275,14 +275,15 @@ def ring_chain(oracle, parts, dtype, devop, arg, n):
 def test_multiprocess_ring_fifo_reduce_scatter_and_reduce(nbx, oracle, n, grid, monkeypatch):
     """NCCL_ALGO=Ring: ReduceScatter block b folded along the ring b+1, ..., b
     and Reduce along the chain root+1, ..., root, through the step FIFO —
-    bitwise NCCL's operand order (ring_chain). NBX_RING_MAX_GRID=2/3 makes each
-    workgroup's slice span many FIFO entries, so the 4-slot FIFO wraps and the
-    head credits gate the producer."""
+    bitwise NCCL's operand order (ring_chain). NBX_SIMPLE_MAX_GRID=2/3 with
+    4 KiB staging slices makes every call run many rounds, so the 2 staging
+    slots wrap and the credits gate the producer."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     monkeypatch.setenv("NCCL_ALGO", "Ring")
     monkeypatch.setenv("NCCL_PROTO", "Simple")
-    monkeypatch.setenv("NBX_RING_MAX_GRID", grid or "32")
+    monkeypatch.setenv("NBX_SIMPLE_MAX_GRID", grid or "32")
+    monkeypatch.setenv("NBX_SIMPLE_SLICE_BYTES", "4096" if grid else "")
     res = _run_ranks(nbx, n, _child_ring_fifo)
     for i, (kind, dtype, op, count, root) in enumerate(RING_FIFO_CASES):
         root = root % n
@@ -567,10 +568,9 @@ def test_multiprocess_graph_capture(nbx, n, monkeypatch):
 
 
 def _child_failure(uid_bytes, rank, q, evq):
-    """Rank 0 meets an absent peer: the LL kernel's bounded spin times out
-    (ncclRemoteError via ncclCommGetAsyncError), the Simple path's host
-    exchange times out (the call returns ncclRemoteError), and ncclCommAbort
-    ends a spinning kernel at once. Rank 1 joins the communicator and then
+    """Rank 0 meets an absent peer: the LL kernel's and the Simple kernel's
+    bounded spins time out (ncclRemoteError via ncclCommGetAsyncError), and
+    ncclCommAbort ends a spinning kernel at once. Rank 1 joins the communicator and then
     issues nothing until rank 0 is done."""
     try:
         import time
@@ -595,14 +595,12 @@ def _child_failure(uid_bytes, rank, q, evq):
         torch.cuda.synchronize()
         out["ll_timeout_s"] = time.perf_counter() - t0
         out["ll_async_error"] = comm.async_error()
-        big = torch.ones(4 << 20, device="cuda")   # 16 MiB: Simple path, host exchange
+        big = torch.ones(4 << 20, device="cuda")   # 16 MiB: Simple protocol kernel
         t0 = time.perf_counter()
-        try:
-            comm.all_reduce(big.data_ptr(), big.data_ptr(), big.numel(), 7, 0, st)
-            out["simple_error"] = 0
-        except nbx.NcclError as e:
-            out["simple_error"] = int(e.code)
+        comm.all_reduce(big.data_ptr(), big.data_ptr(), big.numel(), 7, 0, st)
+        torch.cuda.synchronize()
         out["simple_timeout_s"] = time.perf_counter() - t0
+        out["simple_error"] = comm.async_error()
         comm.abort()
         # a fresh communicator whose peer never calls: abort ends the spinning kernel
         evq.put("next")
