@@ -15,7 +15,11 @@ Extra JSON fields:
   roofline     — the dominant kernel's algorithmic bytes per launch / its mean
                  launch duration (HIP events on the launch stream) vs the
                  8 TB/s HBM3E peak; `traffic` = HBM bytes per launch from the
-                 committed rocprofv3 PMC pass (profiles/), or null.
+                 committed rocprofv3 PMC pass (profiles/pmc_latest.json) — NOT
+                 measured in this run: `traffic_provenance` names its box/run;
+                 `ceiling_mixed` = the same tile's 8:1 read/write stream with
+                 no arithmetic, measured here, and frac_of_ceiling = achieved /
+                 ceiling_mixed.
   cpu_baseline — the oracle's C restatement (oracle/reduce_oracle.c, a port of
                  the reference semantics) timed on this box's host cores on a
                  bounded sample of the same workload (rank 0, N=1 only).
@@ -25,9 +29,14 @@ Extra JSON fields:
                  multi-process communicator across the N GPUs, checked exactly;
                  run in a child process per rank (scripts/collective_leg.py) so
                  a failure there is reported here instead of ending the bench.
+                 Then `collective.clique`: config D through the single-process
+                 communicator (ncclCommInitAll over the same N GPUs, no IPC;
+                 scripts/clique_leg.py, a child of rank 0), so a multi-process
+                 plumbing failure can be told from an xGMI data-path failure.
                  Then `collective.rccl`: RCCL (torch.distributed "nccl") on the
                  same shapes in the bench process, as the vendor reference.
-                 NBX_BENCH_COLLECTIVE=0 skips both, NBX_BENCH_RCCL=0 the RCCL part.
+                 NBX_BENCH_COLLECTIVE=0 skips all three, NBX_BENCH_CLIQUE=0 the
+                 clique part, NBX_BENCH_RCCL=0 the RCCL part.
 """
 from __future__ import annotations
 
@@ -97,18 +106,23 @@ def max_over_ranks(value: float, world: int) -> float:
 
 
 def _pmc_traffic():
-    """HBM bytes per launch of the f32 sum 8-src kernel from the committed PMC
-    summary (profiles/pmc_latest.json, written by scripts/pmc_traffic.py from
-    separate rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 note)."""
+    """(HBM bytes per launch, provenance) of the f32 sum 8-src kernel from the
+    committed PMC summary (profiles/pmc_latest.json, written by
+    scripts/pmc_traffic.py from separate rocprofv3 --pmc passes, FETCH_SIZE
+    doubled per the gfx950 note). Carried over from that run, not measured by
+    this bench invocation; the provenance string says so."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
         if d.get("workload") == "config_b_f32_sum_8x256MiB":
-            return d.get("hbm_bytes_per_launch")
+            src = d.get("source", "")
+            return d.get("hbm_bytes_per_launch"), (
+                f"carried over from profiles/pmc_latest.json ({src or 'committed rocprofv3 --pmc passes'}); "
+                "not measured in this run")
     except (OSError, ValueError):
         pass
-    return None
+    return None, None
 
 
 def host_e2e_leg(torch, nbx, srcs, out, stream, op, reps: int = 2):
@@ -198,13 +212,15 @@ def stream_ceilings(torch, nbx, srcs, out, stream, reps: int = 10):
             raise RuntimeError(f"stream ceiling launch failed: {rc}")
     rd = timed(lambda: chk(lib.nbxDebugStream(0, out.data_ptr(), s_arr, N_SRCS, COUNT * ELT, 0, sh)),
                N_SRCS * COUNT * ELT)
+    mx = timed(lambda: chk(lib.nbxDebugStream(2, b.data_ptr(), s_arr, N_SRCS, COUNT * ELT, 0, sh)), ALG_BYTES)
     wr = timed(lambda: chk(lib.nbxDebugStream(1, b.data_ptr(), None, 0, half, 0, sh)), half)
     cp = timed(lambda: chk(lib.nbxReduceMulti(b_arr, 1, a_arr, 1, half // 4, f32, op, 0, 0, sh)), 2 * half)
     del a, b
-    return {"read_GBs": rd, "write_GBs": wr, "copy_GBs": cp,
+    return {"read_GBs": rd, "write_GBs": wr, "copy_GBs": cp, "mixed_GBs": mx,
             "what": "same process, this box: read-only 8 x 256 MiB (hot kernel's nt loads, 8x4 packs/lane, "
                     "1 WG/CU, nothing stored); write-only 1.125 GiB (plain 16-B stores); 1:1 copy 1.125 GiB -> "
-                    "1.125 GiB (nbxReduceMulti, 1 source)"}
+                    "1.125 GiB (nbxReduceMulti, 1 source); mixed 8:1 = the hot kernel's tile and schedule reading "
+                    "8 x 256 MiB and storing 256 MiB with no arithmetic"}
 
 
 def cpu_baseline(seconds: float = 1.5):
@@ -263,6 +279,62 @@ def _spawn_collective_leg(world: int, script: str | None = None):
                              cwd=ROOT)
     child.nbx_log = log.name
     return child
+
+
+def _spawn_clique_leg(world: int, rank: int, script: str | None = None):
+    """Rank 0 only: start the single-process clique child before the parent
+    touches the GPU; it stays idle (no HIP call) until told to run."""
+    if (world <= 1 or rank != 0 or os.environ.get("NBX_BENCH_COLLECTIVE", "1") == "0"
+            or os.environ.get("NBX_BENCH_CLIQUE", "1") == "0"):
+        return None
+    return _spawn_collective_leg(world, script or os.path.join(ROOT, "scripts", "clique_leg.py"))
+
+
+def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 400.0):
+    """Config D through ncclCommInitAll over every rank's GPU, run by rank 0's
+    child while the other ranks wait on the host (the process group's store:
+    no RCCL kernel of theirs occupies a GPU meanwhile). Rank 0 gets the result."""
+    import datetime
+    import torch.distributed as dist
+    devs = [None] * world
+    dist.all_gather_object(devs, dev)
+    store = dist.distributed_c10d._get_default_store()
+    key = "nbx_clique_leg_done"
+    if rank != 0:
+        store.wait([key], datetime.timedelta(seconds=result_timeout + 120))
+        return None
+    res = None
+    if child is not None:
+        try:
+            child.stdin.write(f"RUN {world} {','.join(str(d) for d in devs)}\n")
+            child.stdin.flush()
+            line = _read_line(child, "RESULT", result_timeout)
+            res = json.loads(line) if line else None
+        except (OSError, ValueError):
+            res = None
+        try:
+            child.stdin.close()
+        except OSError:
+            pass
+        try:
+            child.wait(timeout=60 if res is not None else 1)
+        except subprocess.TimeoutExpired:
+            child.kill()   # rank 0's own child, by PID
+            child.wait()
+        if res is None:
+            res = {"ok": False, "errors": ["no result from the clique leg: " + _log_tail(child)]}
+    store.set(key, "1")
+    if res is None:
+        return None
+    S = COUNT_D * 4
+    for name, fac in (("allreduce", 2 * (world - 1) / world), ("reduce_scatter", (world - 1) / world)):
+        ms = res.get(name + "_ms")
+        if ms:
+            alg = S / (ms * 1e-3) / 1e9
+            res[name] = {"ms": round(ms, 4), "algbw_GBs": round(alg, 2), "busbw_GBs": round(alg * fac, 2)}
+    res["workload"] = ("config D through ncclCommInitAll (one process, every GPU of the run, no IPC), "
+                       "ncclSum fp32 1 GiB per rank, checked exactly")
+    return res
 
 
 def _read_line(child, prefix: str, timeout: float):
@@ -467,6 +539,7 @@ def main():
     args = ap.parse_args()
 
     child = _spawn_collective_leg(int(os.environ.get("WORLD_SIZE", "1")))
+    clique_child = _spawn_clique_leg(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
     import torch
     world, rank, local = _dist_init()
     if args.gpus != world and world > 1:
@@ -531,7 +604,7 @@ def main():
         assert torch.equal(out[idx], ref), "bench output differs from the left-fold reference"
 
     achieved = ALG_BYTES / (kern_avg_ms * 1e-3) / 1e9
-    traffic = _pmc_traffic()
+    traffic, traffic_src = _pmc_traffic()
     ceil = None
     if os.environ.get("NBX_BENCH_CEILING", "1") != "0":
         ceil = stream_ceilings(torch, nbx, srcs, out, stream)
@@ -555,6 +628,7 @@ def main():
         "pct_hbm_peak": round(100.0 * (ALG_BYTES / (wall / args.steps)) / (HBM_PEAK_GBS * 1e9), 2),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_provenance": traffic_src,
                      "kernel": "kReducePacks<FnSumF<TyF32>, NSRC=8, U=4>",
                      "tile_schedule": "static" if os.environ.get("NBX_DYNAMIC_TILES", "1") == "0"
                      else "dynamic (per-stream tile counter)",
@@ -566,14 +640,21 @@ def main():
     if ceil:
         rf = result["roofline"]
         rf["ceiling_read"], rf["ceiling_write"], rf["ceiling_copy"] = ceil["read_GBs"], ceil["write_GBs"], ceil["copy_GBs"]
-        rf["frac_of_ceiling"] = round(achieved / max(ceil["read_GBs"], ceil["copy_GBs"]), 4)
-        rf["ceiling_what"] = ceil["what"] + "; frac_of_ceiling = achieved / max(read, copy)"
+        rf["ceiling_mixed"] = ceil["mixed_GBs"]
+        rf["frac_of_ceiling"] = round(achieved / ceil["mixed_GBs"], 4)
+        rf["frac_of_read_ceiling"] = round(achieved / max(ceil["read_GBs"], ceil["copy_GBs"]), 4)
+        rf["ceiling_what"] = (ceil["what"] + "; frac_of_ceiling = achieved / mixed (the stream the fold faces), "
+                              "frac_of_read_ceiling = achieved / max(read, copy)")
     if world == 1 and os.environ.get("NBX_BENCH_E2E", "1") != "0" and not args.no_cpu_baseline:
         result["host_e2e"] = host_e2e_leg(torch, nbx, srcs, out, stream, op)
     if child is not None:
         del srcs, out
         torch.cuda.empty_cache()
         coll = collective_leg(child, world, rank)
+        if os.environ.get("NBX_BENCH_CLIQUE", "1") != "0":
+            cl = clique_leg(clique_child, world, rank, local)
+            if coll is not None:
+                coll["clique"] = cl
         if os.environ.get("NBX_BENCH_RCCL", "1") != "0":
             rccl = rccl_leg(world)
             if coll is not None:

@@ -39,7 +39,10 @@ int nbxDebugCommProtoMask(ncclComm_t comm);
  * ceiling"): kind 0 reads nSrcs == 8 buffers of `bytes` each with the hot
  * kernel's loads and tile (16-B nontemporal, 8 x 4 packs per lane, one
  * workgroup per CU) and stores nothing; kind 1 writes `bytes` to dst with its
- * stores (plain 16-B). Buffers 16-B aligned, bytes a multiple of 16;
+ * stores (plain 16-B); kind 2 is the 8:1 mixed stream: the read kernel's
+ * tile and the fold's schedule (dynamic tiles from 16 tiles per workgroup),
+ * every load kept live without arithmetic, source 0 stored to dst (bytes per
+ * source). Buffers 16-B aligned, bytes a multiple of 16;
  * blocksPerCU 0 = the production shape. Asynchronous on `stream` (a
  * hipStream_t). The 1:1 copy ceiling is nbxReduceMulti with one source. */
 ncclResult_t nbxDebugStream(int kind, void* dst, const void* const* srcs, int nSrcs, size_t bytes, int blocksPerCU,

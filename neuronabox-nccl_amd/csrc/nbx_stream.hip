@@ -5,12 +5,18 @@
 // kReducePacks' big tile: 8 sources x 4 packs per lane, one 256-thread
 // workgroup per CU) and stores (plain 16-B). The 1:1 copy ceiling is the
 // production kernel itself at one source (nbxReduceMulti, nSrcs = 1).
+// Kind 2 is the mixed stream the fold actually faces: the same 8-source big
+// tile, same schedule (dynamic tiles from 16 tiles per workgroup, as
+// nbxReduceMulti), every load kept live but no arithmetic, and source 0's
+// packs stored — 8 reads per write, so fold / mixed isolates what the fold's
+// own ALU work and dependency chain cost.
 // Diagnostics only: nothing in the collectives calls these.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/nbx_debug.h"
 #include "nbx_functors.h"
+#include "nbx_internal.h"
 #include "nbx_kargs.h"
 #include "nbx_tiles.h"
 
@@ -46,6 +52,32 @@ __global__ __launch_bounds__(kBlock) void kStreamRead(KArgs a) {
     ((u32x4*)a.dst[0])[blockIdx.x * kBlock + threadIdx.x] = acc;
 }
 
+// 8:1 mixed stream: the fold's loads and stores without its arithmetic
+template <int NSRC, int U>
+__global__ __launch_bounds__(kBlock) void kStreamMixed(KArgs a) {
+  const u32x4* src[NSRC];
+#pragma unroll
+  for (int s = 0; s < NSRC; s++) src[s] = (const u32x4*)a.src[s];
+  u32x4* dst = (u32x4*)a.dst[0];
+  const uint64_t n = a.nPacks;
+  constexpr uint64_t kTile = (uint64_t)U * kBlock;
+  forEachTile(a, n / kTile, [&](uint64_t t) {
+    const uint64_t p = t * kTile + threadIdx.x;
+    u32x4 v[NSRC][U];
+#pragma unroll
+    for (int s = 0; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) v[s][u] = ldStream(src[s] + p + u * kBlock);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 1; s < NSRC; s++)
+#pragma unroll
+      for (int u = 0; u < U; u++) asm volatile("" ::"v"(v[s][u]));   // live, not computed on
+#pragma unroll
+    for (int u = 0; u < U; u++) dst[p + u * kBlock] = v[0][u];
+  });
+}
+
 // plain 16-B stores of a constant: the store half of the fold
 template <int U>
 __global__ __launch_bounds__(kBlock) void kStreamWrite(KArgs a) {
@@ -69,14 +101,14 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t nbxDebugStream(in
                                                                              size_t bytes, int blocksPerCU,
                                                                              ncclStream_t stream) {
   using namespace nbx;
-  if (kind < 0 || kind > 1 || dst == nullptr || (bytes & 15u) != 0 || blocksPerCU < 0 || blocksPerCU > 16)
+  if (kind < 0 || kind > 2 || dst == nullptr || (bytes & 15u) != 0 || blocksPerCU < 0 || blocksPerCU > 16)
     return ncclInvalidArgument;
   if (((uintptr_t)dst & 15u) != 0) return ncclInvalidArgument;
   KArgs a{};
   a.dst[0] = dst;
   a.nPacks = bytes / 16;
   a.arg = 0x0123456789abcdefull;
-  if (kind == 0) {
+  if (kind == 0 || kind == 2) {
     if (nSrcs != kMaxKSrcs || srcs == nullptr) return ncclInvalidArgument;
     for (int s = 0; s < nSrcs; s++) {
       if (srcs[s] == nullptr || ((uintptr_t)srcs[s] & 15u) != 0) return ncclInvalidArgument;
@@ -88,12 +120,21 @@ extern "C" __attribute__((visibility("default"))) ncclResult_t nbxDebugStream(in
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   // read: the production 8-source big tile (one workgroup per CU); write: the
   // production 1-source small tile (5 workgroups per CU)
-  const int per = blocksPerCU > 0 ? blocksPerCU : (kind == 0 ? 1 : 5);
-  const uint64_t tile = (uint64_t)(kind == 0 ? 4 : 1) * kBlock;
+  const int per = blocksPerCU > 0 ? blocksPerCU : (kind == 1 ? 5 : 1);
+  const uint64_t tile = (uint64_t)(kind == 1 ? 1 : 4) * kBlock;
   uint64_t grid = (a.nPacks + tile - 1) / tile;
   if (grid > (uint64_t)cus * (uint64_t)per) grid = (uint64_t)cus * (uint64_t)per;
   if (grid == 0) return ncclSuccess;
   void* args[] = {&a};
+  if (kind == 2) {   // the production schedule: dynamic tiles when each workgroup runs >= 16 tiles
+    const uint64_t tiles = a.nPacks / tile;
+    DynLaunch dyn;
+    if (tiles >= 16 * grid) dyn.begin(dev, (hipStream_t)stream, tiles, a);
+    const hipError_t e = hipLaunchKernel((const void*)&kStreamMixed<kMaxKSrcs, 4>, dim3((unsigned)grid), dim3(kBlock),
+                                         args, 0, (hipStream_t)stream);
+    dyn.done(e == hipSuccess);
+    return e == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+  }
   const void* fn = kind == 0 ? (const void*)&kStreamRead<kMaxKSrcs, 4> : (const void*)&kStreamWrite<1>;
   // static tiles: for a read-only stream the grid stride is the faster
   // schedule (7.07-7.10 vs 6.61 TB/s with dynamic tiles, profiles/r2/bench_dyn_ab_r2u.jsonl),

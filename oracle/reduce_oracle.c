@@ -26,6 +26,16 @@
  * for min and (a > b) ? a : b for max, so an exact tie (including +0 vs -0)
  * returns the second operand — the same tie rule as the integer MinMax line
  * reduce_kernel.h:168 and glibc's x86-64 fminf/fmaxf (minss/maxss).
+ * UNPINNED against the reference: what NVIDIA's fminf / min.f32 returns for
+ * +0 vs -0 (IEEE 754-2008 leaves the sign of min(+0, -0) to the
+ * implementation) and which NaN payload survives were never observable here;
+ * only NaN-ness is compared. Because a tie returns the second operand, the
+ * OPERAND ORDER of each fold step is observable for ±0 ties: the direct
+ * schedules fold Fn(acc, next) (common_kernel.h:79-131 left fold), while each
+ * ring / chain hop folds Fn(local input, received partial) (recvReduceSend,
+ * prims_simple.h srcs[0] = own input; reduce_scatter.h:49-64, reduce.h:44-67)
+ * — tests/test_multiprocess_gpu.py::test_multiprocess_float_minmax_ties checks
+ * both orders against this oracle.
  *
  * fp8 (OCP e4m3fn, e5m2): NOT in the reference (NCCL 2.19 has no fp8 type) —
  * PARITY UNPINNED by the reference; this build's own definition, following the

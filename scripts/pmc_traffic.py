@@ -10,7 +10,7 @@ profiles/pmc_latest.json with the HBM bytes per launch of the config-B kernel:
 
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads exactly half
 of a wide coalesced streaming read (MI355X_MICROARCH.md §HBM), hence x2.
-usage: pmc_traffic.py <run_dir> <out_dir>
+usage: pmc_traffic.py <run_dir> <out_dir> [source label, e.g. "round 3 run r3c"]
 """
 import csv
 import json
@@ -55,6 +55,7 @@ def main():
         "traffic_over_alg": round(hbm / ALG, 4),
         "kernel_trace": stats,
         "kernel_trace_GBps": round(ALG / (stats["avg_ns"] * 1e-9) / 1e9, 1) if stats else None,
+        "source": sys.argv[3] if len(sys.argv) > 3 else run,
     }
     with open(os.path.join(out, "pmc_latest.json"), "w") as f:
         json.dump(d, f, indent=2)

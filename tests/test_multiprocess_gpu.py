@@ -748,3 +748,104 @@ def test_multiprocess_timeout_and_abort(nbx, monkeypatch):
             assert 2.5 < r0["simple_timeout_s"] < 30, r0
         else:
             assert r0["abort_s"] < 20, r0                 # not the 120 s timeout
+
+
+# Float min/max with ±0 ties and NaNs: a tie returns the
+# second operand (oracle/reduce_oracle.c header), so the operand order of every
+# fold step is observable. Direct schedules fold Fn(acc, next) in the order
+# b+1, ..., b; ring / chain hops fold Fn(local, received) (ring_chain above).
+TIE_BITS = {   # +0, -0, +1, -1, +inf, -inf, qNaN, 2.5 (zeros drawn most often)
+    7: (np.uint32, [0x0, 0x80000000, 0x3f800000, 0xbf800000, 0x7f800000, 0xff800000, 0x7fc00000, 0x40200000]),
+    8: (np.uint64, [0x0, 1 << 63, 0x3ff0000000000000, 0xbff0000000000000, 0x7ff0000000000000,
+                    0xfff0000000000000, 0x7ff8000000000000, 0x4004000000000000]),
+    6: (np.uint16, [0x0, 0x8000, 0x3c00, 0xbc00, 0x7c00, 0xfc00, 0x7e00, 0x4100]),
+    9: (np.uint16, [0x0, 0x8000, 0x3f80, 0xbf80, 0x7f80, 0xff80, 0x7fc0, 0x4020]),
+}
+TIE_CASES = [(kind, dt, op) for kind in ("ar", "rs", "red") for dt in (7, 8, 6, 9) for op in (2, 3)]
+TIE_COUNT = 6007
+
+
+def _tie_input(kind, dt, op, n, r):
+    st, bits = TIE_BITS[dt]
+    total = TIE_COUNT * n if kind == "rs" else TIE_COUNT
+    rng = np.random.default_rng(9000 + 100 * dt + 10 * op + r + (0 if kind == "ar" else 3 if kind == "rs" else 6))
+    pick = rng.choice(len(bits), size=total, p=[0.3, 0.3, 0.06, 0.06, 0.06, 0.06, 0.1, 0.06])
+    return np.array(bits, dtype=st)[pick]
+
+
+def _child_ties(uid_direct, rank, n, q, uid_ring):
+    try:
+        import os
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        os.environ["NCCL_PROTO"] = "Simple"
+        comms = {"direct": nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_direct), rank)}
+        os.environ["NCCL_ALGO"] = "Ring"
+        comms["ring"] = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_ring), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        for algo, comm in comms.items():
+            for i, (kind, dt, op) in enumerate(TIE_CASES):
+                x = _tie_input(kind, dt, op, n, rank)
+                tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+                nb = TIE_COUNT * x.itemsize
+                ty = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+                root = i % n
+                if kind == "ar":
+                    comm.all_reduce(tx.data_ptr(), ty.data_ptr(), TIE_COUNT, dt, op, st)
+                elif kind == "rs":
+                    comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), TIE_COUNT, dt, op, st)
+                else:
+                    comm.reduce(tx.data_ptr(), ty.data_ptr() if rank == root else 0, TIE_COUNT, dt, op, root, st)
+                torch.cuda.synchronize()
+                out[(algo, i)] = ty.cpu().numpy().copy()
+            assert comm.async_error() == 0
+        for comm in comms.values():
+            comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multiprocess_float_minmax_ties(nbx, oracle, n, monkeypatch):
+    """f32 / f64 / f16 / bf16 ncclMax and ncclMin over inputs that are mostly
+    ±0 with NaNs and infinities, AllReduce / ReduceScatter / Reduce, on the
+    direct and the ring schedule: bit-exact against the oracle folded in each
+    schedule's own operand order (direct: left fold b+1, ..., b; ring: NCCL's
+    hop order Fn(local, received) along the chain b+1 -> ... -> b)."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_SIMPLE_MAX_GRID", "8")
+    res = _run_ranks(nbx, n, _child_ties, bytes(nbx.get_unique_id()))
+    for i, (kind, dt, op) in enumerate(TIE_CASES):
+        xs = [_tie_input(kind, dt, op, n, r) for r in range(n)]
+        xs = [x.view(oracle.NP_STORAGE[dt]) for x in xs]
+        devop, arg = oracle.host_to_dev_redop(op, dt, n)
+        eb = xs[0].itemsize
+        root = i % n
+        for algo in ("direct", "ring"):
+            def fold(parts):
+                if algo == "direct":
+                    return oracle.reduce_multi(parts, dt, devop, arg, n_pre_op_srcs=n)[0]
+                return ring_chain(oracle, parts, dt, devop, arg, n)
+            exp = {}
+            if kind == "rs":
+                for b in range(n):
+                    exp[b] = fold([xs[(b + 1 + k) % n][b * TIE_COUNT:(b + 1) * TIE_COUNT] for k in range(n)])
+            elif kind == "ar":
+                full = np.empty(TIE_COUNT, dtype=xs[0].dtype)
+                for c, (lo, hi) in enumerate(_blocks(TIE_COUNT, eb, n)):
+                    if hi > lo:
+                        full[lo:hi] = fold([xs[(c + 1 + k) % n][lo:hi] for k in range(n)])
+                exp = {r: full for r in range(n)}
+            else:
+                exp[root] = fold([xs[(root + 1 + k) % n] for k in range(n)])
+            for r, e in exp.items():
+                got = res[r][(algo, i)]
+                assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (algo, kind, dt, op, r)

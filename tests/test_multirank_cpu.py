@@ -120,3 +120,61 @@ def test_collective_leg_protocol_gloo(tmp_path, mode):
         assert out["ok"] is False
         assert any(e.startswith("rank 1:") for e in out["errors"])
         assert out["allreduce_direct"] is None
+
+
+STUB_CLIQUE = r'''
+import json, os, sys
+mode = os.environ.get("STUB_MODE", "ok")
+for line in sys.stdin:
+    p = line.split()
+    if p and p[0] == "RUN":
+        n, devs = int(p[1]), [int(d) for d in p[2].split(",")]
+        if mode == "die":
+            sys.exit(3)
+        print("RESULT " + json.dumps({"ok": True, "errors": [], "n_ranks": n, "devices": devs,
+                                      "allreduce_ms": 8.0, "reduce_scatter_ms": 4.0}), flush=True)
+        break
+'''
+
+
+def _clique_worker(rank, world, port, script, mode, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      STUB_MODE=mode)
+    import bench
+    child = bench._spawn_clique_leg(world, rank, script)
+    assert (child is None) == (rank != 0)   # rank 0 alone runs the single-process clique
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = bench.clique_leg(child, world, rank, dev=3 + rank, result_timeout=10.0)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["ok", "die"])
+def test_clique_leg_protocol_gloo(tmp_path, mode):
+    """bench.py's single-process (ncclCommInitAll) config-D leg: rank 0's child
+    gets every rank's device, the other ranks wait on the host store and
+    return None, algbw / busbw are derived, and a dying child is reported."""
+    script = tmp_path / "stub_clique.py"
+    script.write_text(STUB_CLIQUE)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_clique_worker, args=(r, world, port, str(script), mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[1] is None
+    out = res[0]
+    if mode == "ok":
+        assert out["ok"] is True and out["devices"] == [3, 4]
+        S = (256 << 20) * 4
+        assert out["allreduce"]["ms"] == 8.0
+        assert abs(out["allreduce"]["busbw_GBs"] - round(S / 8e-3 / 1e9 * 2 * (world - 1) / world, 2)) < 1e-9
+        assert abs(out["reduce_scatter"]["busbw_GBs"] - round(S / 4e-3 / 1e9 * (world - 1) / world, 2)) < 1e-9
+    else:
+        assert out["ok"] is False and out["errors"][0].startswith("no result from the clique leg")
