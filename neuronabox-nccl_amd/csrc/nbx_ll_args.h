@@ -101,6 +101,8 @@ struct SimpleArgs {
   int32_t root;
   int32_t slots;               // staging slots per (region, source, workgroup), >= 2
   int32_t gridMax;
+  int32_t prefetch;            // direct: push round k+1 before folding round k (a rank-local choice)
+  int32_t pad;
 };
 
 }  // namespace nbx

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
   const char* const send = (const char*)a.send;
   char* const recv = (char*)a.recv;
 
-  for (uint64_t k = 0; k < a.nRounds; k++) {
+  auto phaseA = [&](uint64_t k) -> bool {
     // ---- A: slice g of block j into rank j's RS region, slot rsSent[j] % slots
     if (tid < n && tid != me) {
       const uint64_t sent = sh.cnt[kCtRsSent][tid];
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
         sh.fail = 1;
     }
     __syncthreads();
-    if (sh.fail) return;
+    if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
       uint64_t off, cnt;
@@ -259,7 +259,10 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     }
     simpleRelease();
     if (tid < n && tid != me) simplePost(simpleFlag(a.peerFlags[tid], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][tid]);
-
+    __syncthreads();
+    return true;
+  };
+  auto phaseB = [&](uint64_t k) -> bool {
     // ---- B: fold block `me` (own input + the n-1 RS slots), store, push to the AG targets
     if (tid < n && tid != me) {
       if (!simpleWait(simpleFlag(myFlags, kFlRsReady, n, tid, gm, g), sh.cnt[kCtRsRecv][tid] + 1, a, tid,
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
       }
     }
     __syncthreads();
-    if (sh.fail) return;
+    if (sh.fail) return false;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const int nDsts = ar ? n : 1;
     if (cnt) {
@@ -296,28 +299,44 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
       simplePost(simpleFlag(a.peerFlags[tid], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][tid]);
       if (pushTarget(tid)) simplePost(simpleFlag(a.peerFlags[tid], kFlAgReady, n, me, gm, g), ++sh.cnt[kCtAgSent][tid]);
     }
-
-    // ---- C: the peers' finished blocks from the AG region into the output
-    if (gathers) {
-      if (tid < n && tid != me &&
-          !simpleWait(simpleFlag(myFlags, kFlAgReady, n, tid, gm, g), sh.cnt[kCtAgRecv][tid] + 1, a, tid,
-                      kDiagSimpleAg))
-        sh.fail = 1;
-      __syncthreads();
-      if (sh.fail) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      for (int q = 1; q < n; q++) {
-        const int j = (me + q) % n;
-        uint64_t o2, c2;
-        simpleSlice<E>(a, j, k, &o2, &c2);
-        if (c2) simpleCopy<E>(recv + o2 * sizeof(E), nullptr, simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), c2);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slots are read: they may be refilled
-      __syncthreads();
-      if (tid < n && tid != me)
-        simplePost(simpleFlag(a.peerFlags[tid], kFlAgCredit, n, me, gm, g), ++sh.cnt[kCtAgRecv][tid]);
-    }
     __syncthreads();
+    return true;
+  };
+  auto phaseC = [&](uint64_t k) -> bool {
+    // ---- C: the peers' finished blocks from the AG region into the output
+    if (tid < n && tid != me &&
+        !simpleWait(simpleFlag(myFlags, kFlAgReady, n, tid, gm, g), sh.cnt[kCtAgRecv][tid] + 1, a, tid,
+                    kDiagSimpleAg))
+      sh.fail = 1;
+    __syncthreads();
+    if (sh.fail) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    for (int q = 1; q < n; q++) {
+      const int j = (me + q) % n;
+      uint64_t o2, c2;
+      simpleSlice<E>(a, j, k, &o2, &c2);
+      if (c2) simpleCopy<E>(recv + o2 * sizeof(E), nullptr, simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), c2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slots are read: they may be refilled
+    __syncthreads();
+    if (tid < n && tid != me)
+      simplePost(simpleFlag(a.peerFlags[tid], kFlAgCredit, n, me, gm, g), ++sh.cnt[kCtAgRecv][tid]);
+    __syncthreads();
+    return true;
+  };
+  // With NBX_SIMPLE_PREFETCH (default on) the next round's pushes go out
+  // before this round's fold waits for the peers' pushes, so the flag round
+  // trip of B hides behind A(k+1); the order is local to a rank (every
+  // counter sequence is unchanged), so ranks need not agree on it.
+  if (a.prefetch && a.nRounds > 0 && !phaseA(0)) return;
+  for (uint64_t k = 0; k < a.nRounds; k++) {
+    if (a.prefetch) {
+      if (k + 1 < a.nRounds && !phaseA(k + 1)) return;
+    } else if (!phaseA(k)) {
+      return;
+    }
+    if (!phaseB(k)) return;
+    if (gathers && !phaseC(k)) return;
   }
   simpleStoreCounters(a, sh);
 }

@@ -693,6 +693,7 @@ struct MpState {
   uint64_t sliceBytes = 0;          // NBX_SIMPLE_SLICE_BYTES: staging bytes per (slot, source, workgroup)
   int slots = 2;                    // NBX_SIMPLE_SLOTS
   int simpleGrid = 0;               // workgroups of a full-size Simple call (NBX_SIMPLE_MAX_GRID, CU-capped)
+  int simplePrefetch = 1;           // NBX_SIMPLE_PREFETCH: next round's pushes before this round's fold
   // successive calls are ordered across streams, as NCCL serializes a
   // communicator's work: a call on another stream waits for the previous one
   hipEvent_t lastEvent = nullptr;
@@ -935,6 +936,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     s = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(s, 1 << 20));
     mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
     mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
+    mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
   }
   HIPCHECK(hipEventCreateWithFlags(&mp->lastEvent, hipEventDisableTiming));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
@@ -1189,6 +1191,7 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
   sa.root = c.root;
   sa.slots = mp->slots;
   sa.gridMax = mp->simpleGrid;
+  sa.prefetch = mp->simplePrefetch;
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
 }
 
