@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
   __shared__ SimpleShared sh;
   simpleLoadCounters(a, sh);
   uint64_t* const myFlags = a.peerFlags[me];
-  const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
+  const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce, rs = a.mode == kSimpleReduceScatter;
   const bool storeLocal = !red || me == a.root;        // B writes this rank's output block
   const bool gathers = ar || (red && me == a.root);    // C runs here
   const int first = ((red ? a.root : me) + 1) % n;      // fold order of block `me`
@@ -275,11 +275,13 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     }
     uint64_t off, cnt;
     simpleSlice<E>(a, me, k, &off, &cnt);
+    // the output holds the whole message, except ReduceScatter's: block `me` only
+    const uint64_t outOff = rs ? off - (uint64_t)me * a.blockElts : off;
     if (tid < n) {
       const int j = (first + tid) % n;
       sh.src[tid] = j == me ? send + off * sizeof(E) : simpleStage(a, me, 0, sh.cnt[kCtRsRecv][j] % slots, j, g);
       // destinations: [own output], then the push targets in the order me+1, ...
-      if (tid == 0 && storeLocal) sh.dst[0] = recv + off * sizeof(E);
+      if (tid == 0 && storeLocal) sh.dst[0] = recv + outOff * sizeof(E);
       if (tid > 0) {
         const int p = (me + tid) % n;
         if (ar) sh.dst[tid] = simpleStage(a, p, 1, sh.cnt[kCtAgSent][p] % slots, me, g);
@@ -291,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const int nDsts = ar ? n : 1;
     if (cnt) {
-      const bool aligned = simpleAligned(send + off * sizeof(E)) && (!storeLocal || simpleAligned(recv + off * sizeof(E)));
+      const bool aligned = simpleAligned(send + off * sizeof(E)) && (!storeLocal || simpleAligned(recv + outOff * sizeof(E)));
       simpleFold<Fn>(fn, sh.src, n, ~0ull, true, sh.dst, nDsts, cnt, aligned);
     }
     simpleRelease();
@@ -437,7 +439,9 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
       if (tid == 0) {
         sh.src[0] = send + off * sizeof(E);
         sh.src[1] = simpleStage(a, me, 0, sh.cnt[kCtRsRecv][left] % slots, left, g);
-        sh.dst[0] = last ? recv + off * sizeof(E) : simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g);
+        // the last hop's chunk is `me`; ReduceScatter's output holds that block only
+        sh.dst[0] = last ? recv + (ar ? off : off - (uint64_t)me * a.blockElts) * sizeof(E)
+                         : simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g);
         sh.dst[1] = simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g);
       }
       __syncthreads();
