@@ -18,6 +18,20 @@ extern "C" {
  * that multi-process ncclCommInitRank uses (the role of src/bootstrap.cc). */
 ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds);
 
+/* The Simple protocol's kernels (direct schedule, or ring when `ring`) for n
+ * "ranks" driven from ONE process on the current device: staging, flag words and
+ * counters laid out as ncclCommInitRank lays them out, every rank's kernel on
+ * its own stream, all n launches of a call running together (n x gridMax
+ * workgroups must fit the GPU at once). kind 0 AllReduce, 1 ReduceScatter
+ * (count = recvcount), 2 Reduce (to `root`); sends[r] / recvs[r] are rank r's
+ * device buffers (recvs[r] may be NULL on Reduce non-roots). Runs one untimed
+ * and `iters` timed calls; *msPerCall = mean device time per call. Returns an
+ * ncclResult_t (ncclRemoteError if a device wait timed out). Tuning and tests
+ * only: the multi-process communicator's data path without its processes. */
+int nbxDebugSimpleRun(int n, int kind, int ring, size_t count, int datatype, int op, const void* const* sends,
+                      void* const* recvs, int root, int gridMax, size_t sliceBytes, int slots, int prefetch,
+                      int iters, float* msPerCall);
+
 /* NCCL_PROTO parsing (tuning.cc:254-259 list syntax: "LL,LL128", "^Simple",
  * case-insensitive; NULL or "" = all): bit 0 LL, bit 1 LL128, bit 2 Simple. */
 int nbxDebugProtoMask(const char* ncclProto);

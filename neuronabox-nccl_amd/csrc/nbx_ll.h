@@ -236,14 +236,14 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
 // 16-byte granularity: a reader accepts a line only when all four chunks show
 // the flag, so a line torn at any 16-byte boundary is waited on, never folded
 // (tests/test_multiprocess_gpu.py::test_ll128_torn_line_is_waited_on). The
-// remaining assumption is that one 16-byte aligned global_store_dwordx4 lands
+// remaining assumption is that one 16-byte aligned buffer_store_dwordx4 lands
 // whole.
 // Line: 64 bytes = 4 lanes x {12 payload bytes, flag}; 48 payload bytes as two
 // pairs of lanes, each pair 24 bytes = 8-byte words W0, W1, W2:
 //   lane A (even) {W0.lo, W0.hi, W1.lo, flag}   lane B (odd) {W2.lo, W2.hi, W1.hi, flag}
 // so every 8-byte word is folded whole by one lane (A: W0 and W1, taking
 // W1.hi from B by a lane shuffle; B: W2) in its own direct-schedule order.
-// Writer: global_store_dwordx4 sc0 sc1 (system scope); reader:
+// Writer: buffer_store_dwordx4 sc0 sc1 (system scope); reader:
 // buffer_load_dwordx4 sc0 sc1 (volatile) and a wave ballot per 4-lane line.
 // Payload efficiency 75 % (LL: 50 %). Buffers, parities, done words and
 // credits are the LL protocol's (above). Restricted to n <= 8 ranks (one
@@ -257,8 +257,15 @@ constexpr int kL128LoadAux = 1 | 16 | (int)(1u << 31);   // sc0 sc1 (system scop
 static_assert(kL128LineBytes == kL128LineBytesHost && kL128DataBytes == kL128DataBytesHost &&
                   kL128Lanes == kL128LanesHost, "host/device layout");
 
-__device__ __forceinline__ void l128StoreLine16(uint64_t* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+// One 16-byte chunk of a line into a peer's LL128 buffer (`base`, uniform;
+// `word`: 8-byte word index of the chunk) by ONE buffer_store_dwordx4 sc0 sc1
+// (system scope, write-through). A buffer store rather than inline asm: the
+// compiler's hazard recognizer cannot see an asm dwordx4 store, so a VALU write
+// to its data registers right behind it could change what is stored.
+typedef unsigned int l128V4U __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void l128StoreLine16(uint64_t* base, uint32_t bytes, uint64_t word, u32x4 v) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(l128V4U, v), rs, (int)(word * 8u), 0, 1 | 16);
 }
 
 // byte offset (in the message) of lane t's pair in line i, and of its first whole word
@@ -412,9 +419,8 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
         const u32x4 v = a.mode == kLLReduceScatter
                             ? l128Chunk((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, call.flag)
                             : whole;
-        uint64_t* line = a.peerL128[j] + ((uint64_t)(call.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) +
-                         2 * t;
-        l128StoreLine16(line, v);
+        l128StoreLine16(a.peerL128[j], a.l128Bytes,
+                        ((uint64_t)(call.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) + 2 * t, v);
       }
     }
   }
@@ -511,7 +517,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
     const uint64_t lines = (len + kL128DataBytes - 1) / kL128DataBytes;
     for (uint64_t i = g0; i < lines; i += groups) {
       const u32x4 v = l128Chunk(send + off, len, i, t, call.flag);
-      l128StoreLine16(a.peerL128[j] + (subSlot(0, me) + i) * (kL128LineBytes / 8) + 2 * t, v);
+      l128StoreLine16(a.peerL128[j], a.l128Bytes, (subSlot(0, me) + i) * (kL128LineBytes / 8) + 2 * t, v);
     }
   }
   // B. own block: fold, store, all-gather pushes
@@ -544,7 +550,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
       const u32x4 line = {(uint32_t)w[0], (uint32_t)(w[0] >> 32), (t & 1) ? w1hi : (uint32_t)w[1], call.flag};
       for (int j = 0; j < n; j++) {
         if (j == me || failed || (reduce && j != a.root)) continue;
-        l128StoreLine16(a.peerL128[j] + (subSlot(1, me) + i) * (kL128LineBytes / 8) + 2 * t, line);
+        l128StoreLine16(a.peerL128[j], a.l128Bytes, (subSlot(1, me) + i) * (kL128LineBytes / 8) + 2 * t, line);
       }
     }
   }

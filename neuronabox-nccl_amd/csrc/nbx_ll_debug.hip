@@ -22,7 +22,7 @@ __global__ __launch_bounds__(64) void kL128TearWriter(uint64_t* line, const unsi
   const int t = (int)threadIdx.x;
   if (t >= kL128Lanes) return;
   const u32x4 v = l128Chunk(payload, kL128DataBytes, 0, t, flag);
-  if (t >= 2) l128StoreLine16(line + 2 * t, v);
+  if (t >= 2) l128StoreLine16(line, 64, 2 * t, v);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (t == 0) {
     const uint64_t t0 = wall_clock64();
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(64) void kL128TearWriter(uint64_t* line, const unsi
     stamp[0] = wall_clock64();
   }
   __builtin_amdgcn_wave_barrier();
-  if (t < 2) l128StoreLine16(line + 2 * t, v);
+  if (t < 2) l128StoreLine16(line, 64, 2 * t, v);
 }
 
 // the production poll + fold for a 2-rank line whose own contribution is zero:

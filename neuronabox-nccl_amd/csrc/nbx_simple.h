@@ -70,12 +70,47 @@ __device__ __forceinline__ void simplePost(uint64_t* w, uint64_t v) {
   __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// This workgroup's stores are complete and visible system-wide (peers' staging
-// included) before anyone of it posts a flag; its loads have returned too.
-__device__ __forceinline__ void simpleRelease() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  // the compiler may drop the wait after the L2 write-back (MI355X guide,
-  // "Compiler hazard"): wait explicitly before this wave joins the barrier
+// Staging is uncached (MTYPE UC) and written with system-scope write-through
+// stores (`sc0 sc1`, as the LL128 lines): once a wave's vmcnt has drained, its
+// stores are performed at the memory, so a flag stored after every wave's
+// drain (workgroup barrier) publishes them without an L2 write-back fence —
+// the guide's write-through hand-off (MI355X_MICROARCH.md, "Valid forms": sc0
+// sc1 stores and loads both sides). Readers load staging with `sc0 sc1`
+// loads too (buffer loads with the system-scope cache policy): a first
+// version read it with nontemporal loads (L1 bypass only) and a chain Reduce
+// folded zeros for ~1 % of a slot's elements. Round 3's
+// first version used system-scope release / acquire fences per phase instead
+// (buffer_wbl2 / buffer_inv of the whole XCD L2, several per round per
+// workgroup): 25x slower on 1 GiB.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sysRsrc(const void* p, uint64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)((bytes + 15) & ~15ull), 0x00020000);
+}
+// (A buffer store, not inline asm: the compiler's hazard recognizer does not
+// see an asm dwordx4 store, and a VALU write to its data registers right after
+// it corrupted the first dword of ~6 % of the packs.)
+constexpr int kSysStoreAux = 1 | 16;  // sc0 sc1: system scope, write-through
+typedef unsigned int nbxV4U __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void stSys(__amdgpu_buffer_rsrc_t rs, uint64_t pack, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nbxV4U, v), rs, (int)(pack * 16u), 0, kSysStoreAux);
+}
+template <class E>
+__device__ __forceinline__ void stSysElt(E* p, E v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <class E>
+__device__ __forceinline__ E ldElt(const E* p) { return __builtin_nontemporal_load(p); }
+template <class E>
+__device__ __forceinline__ E ldSysElt(const E* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+constexpr int kSysLoadAux = 1 | 16;   // buffer-load cache policy sc0 sc1: system scope
+__device__ __forceinline__ u32x4 ldSys(__amdgpu_buffer_rsrc_t rs, uint64_t pack) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(pack * 16u), 0, kSysLoadAux));
+}
+
+// Every wave's stores (and loads) of this phase have completed, then the
+// workgroup meets: a flag posted after this publishes them.
+__device__ __forceinline__ void simpleDrain() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 }
@@ -104,47 +139,66 @@ __device__ __forceinline__ void simpleSlice(const SimpleArgs& a, int b, uint64_t
 }
 
 // Workgroup copy of nElts elements into up to two destinations (any alignment;
-// 16-B packs when every pointer is 16-B aligned).
+// 16-B packs when every pointer is 16-B aligned). sys0 / sys1: the
+// destination is staging (write-through stores), else a caller buffer; sysSrc:
+// the source is staging (system-scope loads).
 template <class E>
-__device__ __forceinline__ void simpleCopy(void* d0, void* d1, const void* src, uint64_t nElts) {
+__device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool sys1, const void* src, bool sysSrc,
+                                           uint64_t nElts) {
   uint64_t done = 0;
   if (((((uintptr_t)d0) | ((uintptr_t)src) | (d1 ? (uintptr_t)d1 : 0)) & 15u) == 0) {
     const uint64_t nPk = nElts * sizeof(E) / 16;
     const u32x4* s = (const u32x4*)src;
-    constexpr int U = 4;
+    const __amdgpu_buffer_rsrc_t rs = sysRsrc(src, nElts * sizeof(E));
+    const __amdgpu_buffer_rsrc_t rd0 = sysRsrc(d0, nElts * sizeof(E));
+    const __amdgpu_buffer_rsrc_t rd1 = sysRsrc(d1 ? d1 : d0, nElts * sizeof(E));
+    constexpr int U = 16;   // 256 B per lane in flight (a 64 KiB slice in one batch): a staging round trip is long
     for (uint64_t p = threadIdx.x; p < nPk; p += (uint64_t)U * kBlock) {
       u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (p + (uint64_t)u * kBlock < nPk) v[u] = ldPack(s + p + (uint64_t)u * kBlock);
+        if (p + (uint64_t)u * kBlock < nPk) v[u] = sysSrc ? ldSys(rs, p + (uint64_t)u * kBlock) : ldPack(s + p + (uint64_t)u * kBlock);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         if (p + (uint64_t)u * kBlock < nPk) {
-          stPack((u32x4*)d0 + p + (uint64_t)u * kBlock, v[u]);
-          if (d1) stPack((u32x4*)d1 + p + (uint64_t)u * kBlock, v[u]);
+          const uint64_t q = p + (uint64_t)u * kBlock;
+          if (sys0) stSys(rd0, q, v[u]);
+          else stPack((u32x4*)d0 + q, v[u]);
+          if (d1) {
+            if (sys1) stSys(rd1, q, v[u]);
+            else stPack((u32x4*)d1 + q, v[u]);
+          }
         }
       }
     }
     done = nPk * 16 / sizeof(E);
   }
   for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
-    const E v = ((const E*)src)[e];
-    ((E*)d0)[e] = v;
-    if (d1) ((E*)d1)[e] = v;
+    const E v = sysSrc ? ldSysElt((const E*)src + e) : ldElt((const E*)src + e);
+    if (sys0) stSysElt((E*)d0 + e, v);
+    else ((E*)d0)[e] = v;
+    if (d1) {
+      if (sys1) stSysElt((E*)d1 + e, v);
+      else ((E*)d1)[e] = v;
+    }
   }
 }
 
 // Workgroup fold of nElts elements: acc = pre?(src[0]); acc = Fn(acc, pre?(src[q]))
 // for q = 1 .. nSrcs-1 (pre on source q iff bit q of preMask), postOp, then
-// stored into every destination. Sources and destinations come from the LDS
-// tables (uniform pointers). 16-B packs when `aligned`, else element by element.
-template <class Fn>
-__device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t preMask,
-                                           bool doPost, char* const* dsts, int nDsts, uint64_t nElts, bool aligned) {
+// stored into every destination (bit d of sysMask: destination d is staging,
+// written through). Sources and destinations come from the LDS tables
+// (uniform pointers). 16-B packs when `aligned`, else element by element.
+// U packs per lane per source, G = 32 / U sources' loads in flight together
+// (32 packs = 512 B per lane, as the 8-source big tile): deep unrolling for
+// the 2-source ring hops and small rank counts, source groups for many ranks.
+template <class Fn, int U>
+__device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t sysSrcMask,
+                                            uint64_t preMask, bool doPost, char* const* dsts, int nDsts,
+                                            uint64_t sysMask, uint64_t nElts, bool aligned) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
-  constexpr int U = 2;
-  constexpr int G = 8;   // sources whose loads are in flight together
+  constexpr int G = 32 / U;
   uint64_t done = 0;
   if (aligned) {
     const uint64_t nPk = nElts / EPP;
@@ -156,9 +210,12 @@ __device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs
         for (int s = 0; s < G; s++) {
           if (q0 + s < nSrcs) {
             const u32x4* sp = (const u32x4*)srcs[q0 + s];
+            const bool sys = (sysSrcMask >> (q0 + s)) & 1u;
+            const __amdgpu_buffer_rsrc_t rs = sysRsrc(sp, nElts * sizeof(E));
 #pragma unroll
             for (int u = 0; u < U; u++)
-              if (p + (uint64_t)u * kBlock < nPk) v[s][u] = ldPack(sp + p + (uint64_t)u * kBlock);
+              if (p + (uint64_t)u * kBlock < nPk)
+                v[s][u] = sys ? ldSys(rs, p + (uint64_t)u * kBlock) : ldPack(sp + p + (uint64_t)u * kBlock);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -179,23 +236,39 @@ __device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs
         if (p + (uint64_t)u * kBlock < nPk) {
           u32x4 r = acc[u];
           if constexpr (Fn::kHasPost) if (doPost) r = fn.postPack(r);
-          for (int d = 0; d < nDsts; d++) stPack((u32x4*)dsts[d] + p + (uint64_t)u * kBlock, r);
+          for (int d = 0; d < nDsts; d++) {
+            const uint64_t q = p + (uint64_t)u * kBlock;
+            if ((sysMask >> d) & 1u) stSys(sysRsrc(dsts[d], nElts * sizeof(E)), q, r);
+            else stPack((u32x4*)dsts[d] + q, r);
+          }
         }
       }
     }
     done = nPk * EPP;
   }
   for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
-    E acc = ((const E*)srcs[0])[e];
+    E acc = (sysSrcMask & 1u) ? ldSysElt((const E*)srcs[0] + e) : ldElt((const E*)srcs[0] + e);
     if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.pre(acc);
     for (int q = 1; q < nSrcs; q++) {
-      E x = ((const E*)srcs[q])[e];
+      E x = ((sysSrcMask >> q) & 1u) ? ldSysElt((const E*)srcs[q] + e) : ldElt((const E*)srcs[q] + e);
       if constexpr (Fn::kHasPre) if ((preMask >> q) & 1u) x = fn.pre(x);
       acc = fn.red(acc, x);
     }
     if constexpr (Fn::kHasPost) if (doPost) acc = fn.post(acc);
-    for (int d = 0; d < nDsts; d++) ((E*)dsts[d])[e] = acc;
+    for (int d = 0; d < nDsts; d++) {
+      if ((sysMask >> d) & 1u) stSysElt((E*)dsts[d] + e, acc);
+      else ((E*)dsts[d])[e] = acc;
+    }
   }
+}
+
+template <class Fn>
+__device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t sysSrcMask,
+                                           uint64_t preMask, bool doPost, char* const* dsts, int nDsts,
+                                           uint64_t sysMask, uint64_t nElts, bool aligned) {
+  if (nSrcs <= 2) simpleFoldU<Fn, 16>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned);
+  else if (nSrcs <= 4) simpleFoldU<Fn, 8>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned);
+  else simpleFoldU<Fn, 4>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned);
 }
 
 __device__ __forceinline__ bool simpleAligned(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
@@ -254,10 +327,10 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
       const int j = (me + q) % n;
       uint64_t off, cnt;
       simpleSlice<E>(a, j, k, &off, &cnt);
-      if (cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), nullptr,
-                             send + off * sizeof(E), cnt);
+      if (cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
+                             send + off * sizeof(E), false, cnt);
     }
-    simpleRelease();
+    simpleDrain();
     if (tid < n && tid != me) simplePost(simpleFlag(a.peerFlags[tid], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][tid]);
     __syncthreads();
     return true;
@@ -290,13 +363,16 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     }
     __syncthreads();
     if (sh.fail) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     const int nDsts = ar ? n : 1;
     if (cnt) {
       const bool aligned = simpleAligned(send + off * sizeof(E)) && (!storeLocal || simpleAligned(recv + outOff * sizeof(E)));
-      simpleFold<Fn>(fn, sh.src, n, ~0ull, true, sh.dst, nDsts, cnt, aligned);
+      // destination 0 is the caller's output unless a Reduce non-root pushes to the root
+      const uint64_t sysMask = storeLocal ? ~1ull : ~0ull;
+      // every source but the own input (at fold position (me - first) mod n) is staging
+      const uint64_t sysSrc = ~(1ull << ((me - first + n) % n));
+      simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
     }
-    simpleRelease();
+    simpleDrain();
     if (tid < n && tid != me) {
       simplePost(simpleFlag(a.peerFlags[tid], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][tid]);
       if (pushTarget(tid)) simplePost(simpleFlag(a.peerFlags[tid], kFlAgReady, n, me, gm, g), ++sh.cnt[kCtAgSent][tid]);
@@ -312,12 +388,12 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
       sh.fail = 1;
     __syncthreads();
     if (sh.fail) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
       uint64_t o2, c2;
       simpleSlice<E>(a, j, k, &o2, &c2);
-      if (c2) simpleCopy<E>(recv + o2 * sizeof(E), nullptr, simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), c2);
+      if (c2) simpleCopy<E>(recv + o2 * sizeof(E), false, nullptr, false,
+                            simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, c2);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slots are read: they may be refilled
     __syncthreads();
@@ -381,7 +457,6 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
         sh.fail = 1;
     }
     __syncthreads();
-    if (!sh.fail && recvRegion >= 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     return sh.fail == 0;
   };
   auto hopPost = [&](int recvRegion, bool pushRs, bool pushAg) {
@@ -404,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
       if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
       char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : recv + off * sizeof(E);
       if (pos == 0) {
-        if (cnt) simpleCopy<E>(out, nullptr, send + off * sizeof(E), cnt);
+        if (cnt) simpleCopy<E>(out, push, nullptr, false, send + off * sizeof(E), false, cnt);
       } else if (cnt) {
         if (tid == 0) {
           sh.src[0] = send + off * sizeof(E);
@@ -413,9 +488,9 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
         }
         __syncthreads();
         const bool aligned = simpleAligned(send + off * sizeof(E)) && simpleAligned(out);
-        simpleFold<Fn>(fn, sh.src, 2, pos == 1 ? 3u : 1u, !push, sh.dst, 1, cnt, aligned);
+        simpleFold<Fn>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned);
       }
-      simpleRelease();
+      simpleDrain();
       hopPost(pos == 0 ? -1 : 0, push, false);
       continue;
     }
@@ -424,9 +499,9 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
       uint64_t off, cnt;
       simpleSlice<E>(a, left, k, &off, &cnt);
       if (!hopWait(-1, true, false)) return;
-      if (cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), nullptr,
-                             send + off * sizeof(E), cnt);
-      simpleRelease();
+      if (cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr, false,
+                             send + off * sizeof(E), false, cnt);
+      simpleDrain();
       hopPost(-1, true, false);
     }
     // reduce-scatter hops: chunk me-2-st, Fn(pre(local), received)
@@ -447,9 +522,11 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
       __syncthreads();
       if (cnt) {
         const bool aligned = simpleAligned(sh.src[0]) && simpleAligned(sh.dst[0]);
-        simpleFold<Fn>(fn, sh.src, 2, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, cnt, aligned);
+        // the last hop stores the caller's output (and pushes the AG start); others push the partial
+        simpleFold<Fn>(fn, sh.src, 2, 2ull, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, last ? 2ull : 1ull,
+                       cnt, aligned);
       }
-      simpleRelease();
+      simpleDrain();
       hopPost(0, !last, last && ar);
     }
     if (!ar) continue;
@@ -461,9 +538,10 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
       simpleSlice<E>(a, c, k, &off, &cnt);
       if (!hopWait(1, false, fwd)) return;
       if (cnt)
-        simpleCopy<E>(recv + off * sizeof(E), fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr,
-                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), cnt);
-      simpleRelease();
+        simpleCopy<E>(recv + off * sizeof(E), false,
+                      fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr, true,
+                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, cnt);
+      simpleDrain();
       hopPost(1, false, fwd);
     }
   }

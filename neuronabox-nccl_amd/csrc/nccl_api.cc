@@ -929,10 +929,10 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   // Simple grid: one workgroup per CU, all co-resident (workgroup g of a rank
   // waits on workgroup g of its peers); ranks sharing a GPU split its CUs.
   {
-    long g = envLong("NBX_SIMPLE_MAX_GRID", nbx::kSimpleMaxGrid);
+    long g = envLong("NBX_SIMPLE_MAX_GRID", 128);
     g = std::min<long>(g, std::max(1, minCus / maxShare));
     mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
-    long s = envLong("NBX_SIMPLE_SLICE_BYTES", 16 << 10);
+    long s = envLong("NBX_SIMPLE_SLICE_BYTES", 64 << 10);
     s = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(s, 1 << 20));
     mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
     mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
@@ -1195,19 +1195,20 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
 }
 
-// One call of a multi-process communicator, ordered after the previous one
-// (a call on another stream waits for it: the kernels share the
-// communicator's device-resident sequencing, as NCCL's calls on one
-// communicator never overlap). Inside a stream capture the graph's own edges
-// order the captured calls; nothing is recorded there.
+// One call of a multi-process communicator, ordered after the previous one:
+// the kernels share the communicator's device-resident sequencing, and NCCL's
+// calls on one communicator never overlap. An event is recorded behind every
+// call; a call on another stream than the previous one waits for it first
+// (recording on the previous stream only at the switch would touch a stream
+// the caller may have destroyed meanwhile). Inside a stream capture the
+// graph's own edges order the captured calls; nothing is recorded there.
 ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
   MpState* mp = comm->mp;
   if (c.count == 0) return ncclSuccess;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIPCHECK(hipStreamIsCapturing(c.stream, &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (!capturing && mp->haveLast && mp->lastStream != c.stream)
-    HIPCHECK(hipStreamWaitEvent(c.stream, mp->lastEvent, 0));
+  if (!capturing && mp->haveLast && mp->lastStream != c.stream) HIPCHECK(hipStreamWaitEvent(c.stream, mp->lastEvent, 0));
   const MpProto proto = mpProtoOf(comm, c);
   NCCLCHECK(proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto));
   if (!capturing) {
@@ -1289,6 +1290,7 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
   (void)hipFree(dSend);
   (void)hipFree(dRecv);
   (void)hipStreamDestroy(st);
+  mp->haveLast = false;   // the probe's work is complete; its stream is gone
   if (r != ncclSuccess) return r;
   std::vector<int32_t> all(n);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &bad, sizeof(bad), all.data()));

@@ -18,6 +18,9 @@ finished and device-synchronised before the next one starts:
   4. rank 1 stores PEER (333.0) into the mapping with a kernel; rank 0 then
      reads its buffer with a kernel: counts of PEER / NEW values seen.
 Any OLD read in 3 or NEW seen in 4 is a stale copy. Prints one JSON line per mode.
+Modes torch / uncached synchronise the device (hipDeviceSynchronize) after
+every step; torch_nosync / uncached_nosync wait for each kernel with an event
+query instead (no device-wide synchronisation, as round 2's flag barriers).
 usage: probe_ipc_coherence.py [iters] [MiB list]
 """
 from __future__ import annotations
@@ -57,20 +60,31 @@ def _setup():
     return torch, nbx, lib, hip
 
 
-def _copy(nbx, torch, dst, src, n):
+def _wait(torch, sync):
+    if sync:
+        torch.cuda.synchronize()
+        return
+    e = torch.cuda.Event()   # completion of the work so far, without a device-wide synchronisation
+    e.record()
+    while not e.query():
+        pass
+
+
+def _copy(nbx, torch, dst, src, n, sync=True):
     op = nbx.host_to_dev_redop(0, 7, 1)
     nbx.reduce_multi([dst], [src], n, 7, op, 0, False, torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    _wait(torch, sync)
 
 
 def rank0(conn, mode, iters, sizes):
     torch, nbx, lib, hip = _setup()
+    sync = not mode.endswith("_nosync")
     for it in range(iters):
         for mib in sizes:
             conn.recv()   # rank 1 has used and freed its pages
             n = (mib << 20) // 4
             raw = None
-            if mode == "torch":
+            if mode.startswith("torch"):
                 buf = torch.full((n,), NEW, device="cuda")
                 base, size = ctypes.c_void_p(), ctypes.c_size_t()
                 hip.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(buf.data_ptr()))
@@ -80,16 +94,16 @@ def rank0(conn, mode, iters, sizes):
                 assert hip.hipExtMallocWithFlags(ctypes.byref(raw), n * 4, 0x3) == 0   # hipDeviceMallocUncached
                 ptr, off = raw.value, 0
                 src = torch.full((n,), NEW, device="cuda")
-                _copy(nbx, torch, ptr, src.data_ptr(), n)
+                _copy(nbx, torch, ptr, src.data_ptr(), n, sync)
                 del src
                 base = raw
-            torch.cuda.synchronize()
+            _wait(torch, sync)
             h = ctypes.create_string_buffer(64)
             assert hip.hipIpcGetMemHandle(h, base) == 0
             conn.send((h.raw, off, n))
             conn.recv()   # rank 1 has read and written through its mapping
             chk = torch.empty(n, device="cuda")
-            _copy(nbx, torch, chk.data_ptr(), ptr, n)
+            _copy(nbx, torch, chk.data_ptr(), ptr, n, sync)
             seen = {"peer": int((chk == PEER).sum()), "new": int((chk == NEW).sum())}
             conn.send(seen)
             del chk
@@ -103,6 +117,7 @@ def rank0(conn, mode, iters, sizes):
 
 def rank1(conn, mode, iters, sizes, q):
     torch, nbx, lib, hip = _setup()
+    sync = not mode.endswith("_nosync")
     rows = []
     for it in range(iters):
         for mib in sizes:
@@ -111,18 +126,18 @@ def rank1(conn, mode, iters, sizes, q):
             float(old.sum())          # reads through the caches
             del old
             torch.cuda.empty_cache()  # pages back to the driver
-            torch.cuda.synchronize()
+            _wait(torch, sync)
             conn.send("freed")
             hraw, off, n = conn.recv()
             p = ctypes.c_void_p()
             assert hip.hipIpcOpenMemHandle(ctypes.byref(p), _Handle.from_buffer_copy(hraw), 1) == 0
             mapped = p.value + off
             loc = torch.empty(n, device="cuda")
-            _copy(nbx, torch, loc.data_ptr(), mapped, n)
+            _copy(nbx, torch, loc.data_ptr(), mapped, n, sync)
             read = {"new": int((loc == NEW).sum()), "old": int((loc == OLD).sum())}
             read["other"] = n - read["new"] - read["old"]
             loc.fill_(PEER)
-            _copy(nbx, torch, mapped, loc.data_ptr(), n)
+            _copy(nbx, torch, mapped, loc.data_ptr(), n, sync)
             conn.send("written")
             seen = conn.recv()
             rows.append({"iter": it, "MiB": mib, "elements": n, "read_through_mapping": read,
@@ -142,7 +157,8 @@ def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 4, 20, 64]
     ctx = mp.get_context("spawn")
-    for mode in ("torch", "uncached"):
+    modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["torch", "uncached", "torch_nosync", "uncached_nosync"]
+    for mode in modes:
         a, b = ctx.Pipe()
         q = ctx.Queue()
         p0 = ctx.Process(target=rank0, args=(a, mode, iters, sizes), daemon=True)

@@ -849,3 +849,53 @@ def test_multiprocess_float_minmax_ties(nbx, oracle, n, monkeypatch):
             for r, e in exp.items():
                 got = res[r][(algo, i)]
                 assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (algo, kind, dt, op, r)
+
+
+def _child_streams(uid_bytes, rank, n, q):
+    """Successive calls of one communicator alternate between two streams with
+    no ordering by the caller: the library orders them (the Simple /
+    ring kernels share the communicator's device-resident counters)."""
+    try:
+        import os
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        os.environ["NCCL_PROTO"] = "Simple"
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = []
+        for it in range(8):
+            s = streams[it % 2]
+            cnt = 300001 + 4096 * it
+            with torch.cuda.stream(s):
+                idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+                x = torch.remainder(idx * 3 + 11 * rank + it, 257)
+                y = torch.full((cnt,), -1.0, device="cuda")
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, s.cuda_stream)
+            outs.append((it, cnt, x, y))
+        torch.cuda.synchronize()
+        bad = []
+        for it, cnt, x, y in outs:
+            idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+            want = sum(torch.remainder(idx * 3 + 11 * r + it, 257) for r in range(n))
+            if not torch.equal(y, want):
+                bad.append((it, int((y != want).sum())))
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", bad))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multiprocess_calls_alternate_streams(nbx, n, monkeypatch):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_SIMPLE_MAX_GRID", "8")
+    res = _run_ranks(nbx, n, _child_streams)
+    for r in range(n):
+        assert res[r] == [], (r, res[r])
