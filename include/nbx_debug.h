@@ -93,6 +93,11 @@ int nbxDebugBatchListSlots(int device, int state);
  * only query. Returns the threshold in force before the call. */
 int nbxDebugSetDynMinTiles(int tilesPerWorkgroup);
 
+/* Per-stream counters allocated so far on `device` by the dynamic schedules
+ * (which: 0 = big-tile reduce's tile counters, 1 = realigning kernel's class
+ * counters); keyed by stream handle (nbx_reduce.cc). -1 bad device. */
+int nbxDebugDynStreamSlots(int device, int which);
+
 #ifdef __cplusplus
 }
 #endif

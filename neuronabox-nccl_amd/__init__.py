@@ -307,6 +307,23 @@ def reduce_multi_host(dsts: Sequence[int], srcs: Sequence[int], count: int, dtyp
            "nbxReduceMultiHost")
 
 
+class ncclConfig(ctypes.Structure):
+    """ncclConfig_t (include/nccl.h; nccl.h.in:53-79), NCCL_CONFIG_INITIALIZER defaults."""
+    _fields_ = [("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+                ("blocking", ctypes.c_int), ("cgaClusterSize", ctypes.c_int), ("minCTAs", ctypes.c_int),
+                ("maxCTAs", ctypes.c_int), ("netName", ctypes.c_char_p), ("splitShare", ctypes.c_int)]
+
+    UNDEF_INT = -(2 ** 31)
+
+    @classmethod
+    def initializer(cls, blocking: int | None = None) -> "ncclConfig":
+        c = cls(ctypes.sizeof(cls), 0xcafebeef, 21904, cls.UNDEF_INT, cls.UNDEF_INT, cls.UNDEF_INT, cls.UNDEF_INT,
+                None, cls.UNDEF_INT)
+        if blocking is not None:
+            c.blocking = int(blocking)
+        return c
+
+
 class Communicator:
     """ncclComm_t wrapper (lifecycle + reducing collectives)."""
 
@@ -318,6 +335,18 @@ class Communicator:
         h = ctypes.c_void_p()
         _check(load_library().ncclCommInitRank(ctypes.byref(h), int(nranks), uid, int(rank)), "ncclCommInitRank")
         return cls(h.value)
+
+    @classmethod
+    def init_rank_config(cls, nranks: int, uid: ncclUniqueId, rank: int, blocking: int | None = None):
+        """ncclCommInitRankConfig; returns (communicator, result code). A
+        non-blocking communicator (blocking=0) comes back at once with
+        ncclInProgress; poll async_error() until it is no longer ncclInProgress."""
+        h = ctypes.c_void_p()
+        cfg = ncclConfig.initializer(blocking)
+        rc = load_library().ncclCommInitRankConfig(ctypes.byref(h), int(nranks), uid, int(rank), ctypes.byref(cfg))
+        if rc not in (ncclResult.ncclSuccess, ncclResult.ncclInProgress):
+            _check(rc, "ncclCommInitRankConfig")
+        return cls(h.value), int(rc)
 
     @classmethod
     def init_all(cls, devices: Iterable[int]) -> list:

@@ -181,6 +181,16 @@ bool overlaps(const void* a, const void* b, size_t bytes) {
 // still enqueue in base order. Not used while the stream is being captured
 // (a replay would reuse a stale base), for hipStreamPerThread (one handle,
 // many streams), or with NBX_DYNAMIC_TILES=0.
+// Keyed by the stream handle. HIP hands a destroyed stream's handle to the
+// next stream created (63 of 64 create / destroy cycles), but hipStreamDestroy
+// returns only once the stream's work has completed (20 ms of pending kernels:
+// destroy took 21.4 ms on the ROCm 7.2 runtime, 39 ms on torch's 7.0 runtime,
+// nothing left running after it; scripts/probe_stream_id.hip,
+// scripts/probe_stream_destroy.py, profiles/r3/probe_stream_*_r3f.log). So a
+// new stream that inherits a handle inherits an idle counter whose value is
+// the base the host tracks, and streams created per iteration keep reusing
+// the same few counters (tests/test_reduce_gpu.py::
+// test_dynamic_counters_with_stream_churn).
 constexpr int kDynCounters = 4096;
 
 struct DynTiles {
@@ -1141,6 +1151,16 @@ __attribute__((visibility("default"))) int nbxDebugSetBatchMode(int mode) {
 
 __attribute__((visibility("default"))) int nbxDebugBatchListSlots(int device, int state) {
   return listSlotCount(device, state);
+}
+
+__attribute__((visibility("default"))) int nbxDebugDynStreamSlots(int device, int which) {
+  if (device < 0 || device >= kMaxDevices) return -1;
+  if (which == 0) {
+    std::lock_guard<std::mutex> lk(g_dyn[device].mu);
+    return g_dyn[device].used;
+  }
+  std::lock_guard<std::mutex> lk(g_shiftDyn[device].mu);
+  return g_shiftDyn[device].used;
 }
 
 __attribute__((visibility("default"))) int nbxDebugSetDynMinTiles(int tilesPerWorkgroup) {

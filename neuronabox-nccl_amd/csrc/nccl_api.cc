@@ -37,6 +37,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "../../include/nbx_debug.h"
@@ -164,6 +165,7 @@ struct ncclComm {
   int freeHead = 0;
   std::shared_ptr<Clique> clique;  // nRanks > 1 (single process)
   MpState* mp = nullptr;           // nRanks > 1 (one process per rank)
+  std::thread initThread;          // non-blocking ncclCommInitRankConfig: mpInit in the background
 };
 
 namespace {
@@ -208,6 +210,18 @@ ncclResult_t commCheck(ncclComm* comm, const char* opName) {
     return ncclInvalidArgument;
   }
   return ncclSuccess;
+}
+
+// ncclCommEnsureReady (init.cc:287-305): an operation on a communicator needs
+// its (non-blocking) initialisation finished and no asynchronous error; an
+// initialisation still running is ncclInvalidArgument, any other error is
+// returned as it is. A finished background initialisation is joined here.
+ncclResult_t commEnsureReady(ncclComm* comm) {
+  const ncclResult_t r = (ncclResult_t)comm->asyncError.load();
+  if (r != ncclInProgress && comm->initThread.joinable()) comm->initThread.join();
+  if (r == ncclSuccess) return ncclSuccess;
+  warn("Attempt to use communicator before the previous operation returned ncclSuccess");
+  return r == ncclInProgress ? ncclInvalidArgument : r;
 }
 
 // comm.h:456-467
@@ -699,6 +713,7 @@ struct MpState {
   hipEvent_t lastEvent = nullptr;
   hipStream_t lastStream = nullptr;
   bool haveLast = false;
+  bool streamOrder = true;          // NBX_MP_STREAM_ORDER=0: calls on different streams are not ordered (A/B only)
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
 };
 
@@ -937,6 +952,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
     mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
     mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
+    mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
   }
   HIPCHECK(hipEventCreateWithFlags(&mp->lastEvent, hipEventDisableTiming));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
@@ -1197,22 +1213,30 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
 
 // One call of a multi-process communicator, ordered after the previous one:
 // the kernels share the communicator's device-resident sequencing, and NCCL's
-// calls on one communicator never overlap. An event is recorded behind every
-// call; a call on another stream than the previous one waits for it first
-// (recording on the previous stream only at the switch would touch a stream
-// the caller may have destroyed meanwhile). Inside a stream capture the
-// graph's own edges order the captured calls; nothing is recorded there.
+// calls on one communicator never overlap. A call on another stream than the
+// previous call's waits for that stream's work so far: an event is recorded
+// on the previous stream at the switch, not behind every call (an event per
+// call cost 4.6 us of host time per call: nbx_perf 4 KiB LL AllReduce 9.7 vs
+// 5.1 us, profiles/r3/nbx_perf_stream_order_r3f.txt). If the previous stream
+// has been destroyed meanwhile, the record fails and nothing is waited for:
+// hipStreamDestroy returns only after the stream's work completed
+// (scripts/probe_stream_destroy.py). Inside a stream capture the graph's own
+// edges order the captured calls; nothing is recorded there.
 ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
   MpState* mp = comm->mp;
   if (c.count == 0) return ncclSuccess;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIPCHECK(hipStreamIsCapturing(c.stream, &cap));
-  const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (!capturing && mp->haveLast && mp->lastStream != c.stream) HIPCHECK(hipStreamWaitEvent(c.stream, mp->lastEvent, 0));
+  const bool order = cap == hipStreamCaptureStatusNone && mp->streamOrder;
+  if (order && mp->haveLast && mp->lastStream != c.stream) {
+    if (hipEventRecord(mp->lastEvent, mp->lastStream) == hipSuccess)
+      HIPCHECK(hipStreamWaitEvent(c.stream, mp->lastEvent, 0));
+    else
+      (void)hipGetLastError();   // the previous stream is gone, and so is its work
+  }
   const MpProto proto = mpProtoOf(comm, c);
   NCCLCHECK(proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto));
-  if (!capturing) {
-    HIPCHECK(hipEventRecord(mp->lastEvent, c.stream));
+  if (order) {
     mp->lastStream = c.stream;
     mp->haveLast = true;
   }
@@ -1350,6 +1374,7 @@ ncclResult_t flushMpGroups() {
 ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff, void* recvbuff, size_t count,
                          ncclDataType_t dt, ncclRedOp_t op, int root, ncclComm* comm, hipStream_t stream) {
   NCCLCHECK(commCheck(comm, opName));
+  NCCLCHECK(commEnsureReady(comm));
   NCCLCHECK(argsCheck(comm, opName, sendbuff, recvbuff, count, dt, op, root, kind == kReduce));
   info("%s: sendbuff %p recvbuff %p count %zu datatype %d op %d root %d comm %p [nranks=%d] stream %p", opName,
        sendbuff, (void*)recvbuff, count, (int)dt, (int)op, root, (void*)comm, comm->nRanks, (void*)stream);
@@ -1396,6 +1421,8 @@ ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclCo
   const char* cp = std::getenv("NCCL_CHECK_POINTERS");
   c->checkPointers = cp && std::atoi(cp) != 0;
   if (config && config->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = config->blocking;
+  const char* be = std::getenv("NCCL_COMM_BLOCKING");   // init.cc:1444-1446: the env overrides the config
+  if (be && (std::atoi(be) == 0 || std::atoi(be) == 1) && *be != '\0') c->blocking = std::atoi(be);
   *out = c;
   return ncclSuccess;
 }
@@ -1436,24 +1463,53 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
          kMaxMpRanks);
     return ncclInvalidArgument;
   }
+  if (config && config->blocking != NCCL_CONFIG_UNDEF_INT && config->blocking != 0 && config->blocking != 1) {
+    warn("Invalid config blocking attribute value %d", config->blocking);   // init.cc:1544-1547
+    return ncclInvalidArgument;
+  }
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
-  if (nranks == 1) return newComm(newcomm, 1, 0, dev, config);
+  if (nranks == 1) {
+    NCCLCHECK(newComm(newcomm, 1, 0, dev, config));
+    return (*newcomm)->blocking ? ncclSuccess : ncclInProgress;   // nothing to wait for: already ready
+  }
   if (!nbx::bootstrapIdHasRoot(commId)) {
     warn("ncclCommInitRank : unique id carries no bootstrap root");
     return ncclInvalidArgument;
   }
   ncclComm* c = nullptr;
   NCCLCHECK(newComm(&c, nranks, myrank, dev, config));
-  ncclResult_t r;
-  try {
-    r = mpInit(c, commId);
-  } catch (const std::exception& e) {
-    warn("internal exception: %s", e.what());
-    r = ncclInternalError;
+  auto init = [](ncclComm* cm, ncclUniqueId id) -> ncclResult_t {
+    ncclResult_t r;
+    try {
+      r = mpInit(cm, id);
+    } catch (const std::exception& e) {
+      warn("internal exception: %s", e.what());
+      r = ncclInternalError;
+    }
+    if (r != ncclSuccess) mpFree(cm);
+    return r;
+  };
+  if (!c->blocking) {
+    // non-blocking (init.cc:1757-1771, group.cc:390-415): the communicator is
+    // handed out at once and initialised by a background thread;
+    // ncclCommGetAsyncError reports ncclInProgress until it is done
+    c->asyncError.store(ncclInProgress);
+    *newcomm = c;
+    try {
+      c->initThread = std::thread([c, commId, dev, init] {
+        (void)hipSetDevice(dev);
+        c->asyncError.store(init(c, commId));
+      });
+    } catch (const std::exception& e) {
+      warn("ncclCommInitRankConfig : cannot start the initialisation thread: %s", e.what());
+      c->asyncError.store(ncclSystemError);
+      return ncclSystemError;
+    }
+    return ncclInProgress;
   }
+  const ncclResult_t r = init(c, commId);
   if (r != ncclSuccess) {
-    mpFree(c);
     delete c;
     return r;
   }
@@ -1524,6 +1580,7 @@ NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* d
 
 NBX_API(ncclResult_t, ncclCommFinalize, ncclComm_t comm) {
   NCCLCHECK(commCheck(comm, "ncclCommFinalize"));
+  NCCLCHECK(commEnsureReady(comm));
   return flushPending();
 }
 
@@ -1553,12 +1610,14 @@ static ncclResult_t commFree(ncclComm* comm) {
 NBX_API(ncclResult_t, ncclCommDestroy, ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;   // init.cc: NULL comm is a no-op
   NCCLCHECK(commCheck(comm, "ncclCommDestroy"));
+  NCCLCHECK(commEnsureReady(comm));   // init.cc:1986-1987: the init thread must have finished
   return commFree(comm);
 }
 
 NBX_API(ncclResult_t, ncclCommAbort, ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
   NCCLCHECK(commCheck(comm, "ncclCommAbort"));
+  if (comm->initThread.joinable()) comm->initThread.join();   // a failing bootstrap ends by its timeout
   if (comm->mp && comm->mp->hostWords) comm->mp->hostWords[0] = 1;   // ends every spinning barrier
   return commFree(comm);
 }
@@ -1595,6 +1654,7 @@ NBX_API(ncclResult_t, ncclCommGetAsyncError, ncclComm_t comm, ncclResult_t* asyn
 
 NBX_API(ncclResult_t, ncclCommCount, const ncclComm_t comm, int* count) {
   NCCLCHECK(commCheck(comm, "CommCount"));
+  NCCLCHECK(commEnsureReady(comm));
   if (count == nullptr) return ncclInvalidArgument;
   *count = comm->nRanks;
   return ncclSuccess;
@@ -1602,6 +1662,7 @@ NBX_API(ncclResult_t, ncclCommCount, const ncclComm_t comm, int* count) {
 
 NBX_API(ncclResult_t, ncclCommCuDevice, const ncclComm_t comm, int* devid) {
   NCCLCHECK(commCheck(comm, "CommCuDevice"));
+  NCCLCHECK(commEnsureReady(comm));
   if (devid == nullptr) return ncclInvalidArgument;
   *devid = comm->device;
   return ncclSuccess;
@@ -1609,6 +1670,7 @@ NBX_API(ncclResult_t, ncclCommCuDevice, const ncclComm_t comm, int* devid) {
 
 NBX_API(ncclResult_t, ncclCommUserRank, const ncclComm_t comm, int* rank) {
   NCCLCHECK(commCheck(comm, "CommUserRank"));
+  NCCLCHECK(commEnsureReady(comm));
   if (rank == nullptr) return ncclInvalidArgument;
   *rank = comm->rank;
   return ncclSuccess;
@@ -1618,6 +1680,7 @@ NBX_API(ncclResult_t, ncclRedOpCreatePreMulSum, ncclRedOp_t* op, void* scalar, n
         ncclScalarResidence_t residence, ncclComm_t comm) {
   // enqueue.cc:1648-1685
   NCCLCHECK(commCheck(comm, "ncclRedOpCreatePreMulSum"));
+  NCCLCHECK(commEnsureReady(comm));
   if (op == nullptr || scalar == nullptr) return ncclInvalidArgument;
   const int sz = typeSize(datatype);
   if (sz < 0) return ncclInvalidArgument;

@@ -4,6 +4,7 @@
 // handle and hipStreamGetId of each; reports reuse of either.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <set>
 
@@ -30,6 +31,39 @@ int main() {
     if (i % 4 == 0) kSpin<<<1, 64, 0, s>>>(100000ull);   // 1 ms pending at destroy
     if (i < 8) std::printf("stream %d handle %p id %llu\n", i, (void*)s, id);
     (void)hipStreamDestroy(s);
+  }
+  // does hipStreamDestroy wait for pending work? a 20 ms kernel, then destroy
+  double destroyMs = -1.0, kernelLeftMs = -1.0;
+  {
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 2;
+    hipEvent_t done;
+    (void)hipEventCreate(&done);
+    kSpin<<<1, 64, 0, s>>>(2000000ull);   // 20 ms at 100 MHz
+    (void)hipEventRecord(done, s);
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipStreamDestroy(s);
+    const auto t1 = std::chrono::steady_clock::now();
+    destroyMs = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    const bool pending = hipEventQuery(done) == hipErrorNotReady;
+    (void)hipEventSynchronize(done);
+    kernelLeftMs = pending ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count() : 0.0;
+    (void)hipEventDestroy(done);
+  }
+  std::printf("{\"destroy_with_20ms_pending_ms\": %.3f, \"kernel_still_running_after_destroy_ms\": %.3f}\n", destroyMs,
+              kernelLeftMs);
+  // API calls on a destroyed (not reused) stream handle: the library's
+  // switch-time event record relies on an error here
+  {
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 2;
+    (void)hipStreamDestroy(s);
+    hipEvent_t ev;
+    (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    const hipError_t er = hipEventRecord(ev, s);
+    (void)hipGetLastError();
+    std::printf("{\"event_record_on_destroyed_stream_rc\": %d, \"name\": \"%s\"}\n", (int)er, hipGetErrorName(er));
+    (void)hipEventDestroy(ev);
   }
   unsigned long long nullId = 0;
   const hipError_t en = hipStreamGetId(nullptr, &nullId);

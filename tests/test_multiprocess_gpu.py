@@ -876,6 +876,29 @@ def _child_streams(uid_bytes, rank, n, q):
                 y = torch.full((cnt,), -1.0, device="cuda")
                 comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, s.cuda_stream)
             outs.append((it, cnt, x, y))
+        # a call on a raw stream destroyed right after it (its work still
+        # queued), then calls on another stream: the library's switch-time event
+        # record on the destroyed stream fails and is skipped (hipStreamDestroy
+        # waited for that work)
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        torch.cuda.synchronize()
+        for it in range(8, 11):
+            cnt = 300001 + 4096 * it
+            idx = torch.arange(cnt, device="cuda", dtype=torch.float32)
+            x = torch.remainder(idx * 3 + 11 * rank + it, 257)
+            y = torch.full((cnt,), -1.0, device="cuda")
+            torch.cuda.synchronize()
+            if it == 9:
+                raw = ctypes.c_void_p()
+                assert hip.hipStreamCreateWithFlags(ctypes.byref(raw), 1) == 0
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, raw.value)
+                assert hip.hipStreamDestroy(raw) == 0
+            else:
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, streams[0].cuda_stream)
+            outs.append((it, cnt, x, y))
         torch.cuda.synchronize()
         bad = []
         for it, cnt, x, y in outs:
@@ -899,3 +922,61 @@ def test_multiprocess_calls_alternate_streams(nbx, n, monkeypatch):
     res = _run_ranks(nbx, n, _child_streams)
     for r in range(n):
         assert res[r] == [], (r, res[r])
+
+
+def _child_nonblocking(uid_bytes, rank, n, q):
+    """Non-blocking communicator (config.blocking = 0): ncclCommInitRankConfig
+    returns ncclInProgress at once, operations before the initialisation has
+    finished fail with ncclInvalidArgument (ncclCommEnsureReady,
+    init.cc:287-305), ncclCommGetAsyncError turns ncclSuccess, then the
+    communicator works like a blocking one."""
+    try:
+        import time
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        if rank != 0:
+            time.sleep(1.5)   # rank 0's initialisation cannot finish before this
+        uid = nbx.ncclUniqueId.from_buffer_copy(uid_bytes)
+        comm, rc = nbx.Communicator.init_rank_config(n, uid, rank, blocking=0)
+        early = []
+        assert rc == int(nbx.ncclResult.ncclInProgress), rc
+        if rank == 0:
+            for name, fn in (("count", lambda: comm.count()),
+                             ("all_reduce", lambda: comm.all_reduce(0, 0, 16, 7, 0, 0))):
+                try:
+                    fn()
+                    early.append((name, "succeeded"))
+                except nbx.NcclError as e:
+                    early.append((name, int(e.code)))
+        t0 = time.monotonic()
+        while comm.async_error() == int(nbx.ncclResult.ncclInProgress):
+            assert time.monotonic() - t0 < 120, "initialisation did not finish"
+            time.sleep(0.01)
+        final = comm.async_error()
+        cnt = 100003
+        x = torch.remainder(torch.arange(cnt, device="cuda", dtype=torch.float32) * 5 + rank, 97)
+        y = torch.full((cnt,), -1.0, device="cuda")
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want = sum(torch.remainder(torch.arange(cnt, device="cuda", dtype=torch.float32) * 5 + r, 97) for r in range(n))
+        ok = bool(torch.equal(y, want))
+        comm.destroy()
+        q.put((rank, "ok", {"early": early, "final": final, "exact": ok, "count_after": n}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multiprocess_nonblocking_init(nbx, n, monkeypatch):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    res = _run_ranks(nbx, n, _child_nonblocking)
+    inval = int(nbx.ncclResult.ncclInvalidArgument)
+    assert res[0]["early"] == [("count", inval), ("all_reduce", inval)], res[0]
+    for r in range(n):
+        assert res[r]["final"] == 0 and res[r]["exact"], (r, res[r])

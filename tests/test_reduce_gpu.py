@@ -940,3 +940,49 @@ def test_dynamic_tiles_threads_sharing_a_stream(nbx, oracle, torch_gpu, dynamic_
     assert not errs, errs
     for o in outs:
         assert_same(o.cpu().numpy(), exp, dtype)
+
+
+def test_dynamic_counters_with_stream_churn(nbx, oracle, torch_gpu, dynamic_tiles_always):
+    """Per-stream counters are keyed by the stream handle, and HIP hands a
+    destroyed stream's handle to the next stream created. That is safe because
+    hipStreamDestroy returns only after the stream's work completed
+    (scripts/probe_stream_destroy.py): streams are created, given dynamic
+    launches (big-tile tile counters and the realigning kernel's class
+    counters) and destroyed with that work still queued, one after another;
+    every output stays bit-exact and the counters in use stay few."""
+    torch = torch_gpu
+    lib = nbx.load_library()
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    lib.nbxDebugDynStreamSlots.argtypes = [ctypes.c_int, ctypes.c_int]
+    dtype = 7
+    n = (1 << 20) + 37
+    srcs = oracle.random_inputs(dtype, 8, n + 1, seed=991)
+    exp_big = oracle.reduce_multi([x[:n] for x in srcs], dtype, 0, threads=8)[0]
+    exp_shift = oracle.reduce_multi([x[1:n + 1] if i % 2 else x[:n] for i, x in enumerate(srcs[:4])], dtype, 0,
+                                    threads=8)[0]
+    ts = [torch.from_numpy(x).cuda() for x in srcs]
+    big_src = [t.data_ptr() for t in ts]
+    shift_src = [t.data_ptr() + (4 if i % 2 else 0) for i, t in enumerate(ts[:4])]   # mixed alignment
+    iters = 16
+    outs = [(torch.zeros(n, dtype=torch.float32, device="cuda"), torch.zeros(n, dtype=torch.float32, device="cuda"))
+            for _ in range(iters)]
+    op = nbx.DevRedOpFull()
+    dev = torch.cuda.current_device()
+    torch.cuda.synchronize()
+    used0 = [lib.nbxDebugDynStreamSlots(dev, w) for w in (0, 1)]
+    for k in range(iters):
+        st = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(st), 1) == 0
+        ob, osh = outs[k]
+        for _ in range(2):
+            nbx.reduce_multi([ob.data_ptr()], big_src, n, dtype, op, 0, False, st.value)
+            nbx.reduce_multi([osh.data_ptr()], shift_src, n, dtype, op, 0, False, st.value)
+        assert hip.hipStreamDestroy(st) == 0   # with its launches still queued
+    torch.cuda.synchronize()
+    for ob, osh in outs:
+        assert_same(ob.cpu().numpy(), exp_big, dtype)
+        assert_same(osh.cpu().numpy(), exp_shift, dtype)
+    used1 = [lib.nbxDebugDynStreamSlots(dev, w) for w in (0, 1)]
+    assert all(u1 - u0 <= 2 for u0, u1 in zip(used0, used1)), (used0, used1)
