@@ -27,6 +27,7 @@ enum DiagSite : uint64_t {
   kDiagSimpleRsCredit = 9,   // Simple: a peer's credit for this rank's RS slot (rsCredit)
   kDiagSimpleAg = 10,    // Simple: a peer's AG-region slice (agReady)
   kDiagSimpleAgCredit = 11,  // Simple: a peer's credit for this rank's AG slot (agCredit)
+  kDiagOrder = 12,       // a call on another stream: the previous call's done word (kMpWaitDone)
 };
 constexpr int kDiagWords = 6;
 constexpr int kDiagByteOffset = 16;   // from the start of the host words
@@ -44,6 +45,7 @@ inline const char* diagSiteName(uint64_t s) {
     case kDiagSimpleRsCredit: return "Simple reduce-scatter slot credit";
     case kDiagSimpleAg: return "Simple all-gather slice (peer's ready word)";
     case kDiagSimpleAgCredit: return "Simple all-gather slot credit";
+    case kDiagOrder: return "previous call's completion (stream switch)";
     default: return "unknown";
   }
 }

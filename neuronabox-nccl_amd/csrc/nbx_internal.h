@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime_api.h>
 
+#include <cstdint>
 #include <mutex>
 #include <utility>
 
@@ -46,6 +47,9 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
 // schedule when `ring`; `grid` workgroups (<= args.gridMax).
 ncclResult_t launchSimple(ncclDataType_t dt, const nbxDevRedOpFull& op, SimpleArgs& args, unsigned grid, bool ring,
                           hipStream_t stream);
+// kMpWaitDone on `stream` (nbx_order.hip): the stream waits until *done >= target.
+ncclResult_t launchMpWaitDone(const uint64_t* done, uint64_t target, const volatile int* abortWord,
+                              volatile int* errWord, uint64_t timeoutTicks, hipStream_t stream);
 // LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
                                    hipStream_t stream);

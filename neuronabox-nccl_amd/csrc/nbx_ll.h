@@ -33,6 +33,7 @@
 //      done word (= seq) into every peer's buffer and advances the state.
 #pragma once
 #include "nbx_diag.h"
+#include "nbx_order.h"
 #include "nbx_functors.h"
 #include "nbx_ll_args.h"
 
@@ -220,6 +221,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   // done word: after every block of this launch has consumed its lines
   __syncthreads();
   if (threadIdx.x == 0) llEnd(a, call);
+  mpArrive(a.order);
 }
 
 
@@ -453,6 +455,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   // done word (as kLLColl)
   __syncthreads();
   if (threadIdx.x == 0) llEnd(a, call);
+  mpArrive(a.order);
 }
 
 
@@ -573,6 +576,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) llEnd(a, call);
+  mpArrive(a.order);
 }
 
 }  // namespace nbx

@@ -23,6 +23,22 @@ struct LLState {
   uint64_t arrive;      // blocks of the running launch that have finished
 };
 
+// Cross-stream order of one communicator's calls (nccl_api.cc runMpColl):
+// every eager call carries its sequence number; the launch's last block, once
+// every block's memory operations have completed, publishes it in `done`
+// (device memory). A call on another stream than the previous one is preceded
+// by kMpWaitDone on its stream, spinning until `done` reaches the previous
+// call's number — no event behind every call (an event marker cost ~5 us of
+// device time per call, scripts/probe_order_cost.hip). seq = 0 (captured
+// calls): nothing is published. `arrive`: 8 per-XCD arrival counters and one
+// top counter, each on its own 64-byte line, zero between launches.
+constexpr int kMpArriveStride = 16;   // u32 words between arrival counters (64 B)
+struct MpDone {
+  uint64_t* done;
+  uint32_t* arrive;   // [9 * kMpArriveStride]
+  uint64_t seq;
+};
+
 struct LLArgs {
   const void* send;
   void* recv;
@@ -50,6 +66,7 @@ struct LLArgs {
   int32_t postOp;
   int32_t mode;            // LLMode
   int32_t root;            // kLLReduce
+  MpDone order;
 };
 
 // ---------------------------------------------------------------------------
@@ -103,6 +120,7 @@ struct SimpleArgs {
   int32_t gridMax;
   int32_t prefetch;            // direct: push round k+1 before folding round k (a rank-local choice)
   int32_t pad;
+  MpDone order;
 };
 
 }  // namespace nbx

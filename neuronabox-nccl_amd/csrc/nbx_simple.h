@@ -41,6 +41,7 @@
 // Included by nbx_kernels.h after ldPack / stPack.
 #pragma once
 #include "nbx_diag.h"
+#include "nbx_order.h"
 #include "nbx_functors.h"
 #include "nbx_kargs.h"
 #include "nbx_ll_args.h"
@@ -417,6 +418,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     if (gathers && !phaseC(k)) return;
   }
   simpleStoreCounters(a, sh);
+  mpArrive(a.order);
 }
 
 // Ring schedule through the right neighbour's staging. AllReduce /
@@ -546,6 +548,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
     }
   }
   simpleStoreCounters(a, sh);
+  mpArrive(a.order);
 }
 
 }  // namespace nbx

@@ -710,10 +710,15 @@ struct MpState {
   int simplePrefetch = 1;           // NBX_SIMPLE_PREFETCH: next round's pushes before this round's fold
   // successive calls are ordered across streams, as NCCL serializes a
   // communicator's work: a call on another stream waits for the previous one
-  hipEvent_t lastEvent = nullptr;
   hipStream_t lastStream = nullptr;
-  bool haveLast = false;
   bool streamOrder = true;          // NBX_MP_STREAM_ORDER=0: calls on different streams are not ordered (A/B only)
+  // completion word of the communicator's kernels (MpDone, nbx_ll_args.h):
+  // [0, 8) done (last completed eager call), [64, 64 + 9 * 64) arrival counters
+  char* orderMem = nullptr;
+  uint64_t callSeq = 0;             // eager calls numbered from 1
+  uint64_t lastSeq = 0;             // number of the previous eager call that launched a kernel
+  uint64_t curSeq = 0;              // number of the call being launched (0: captured)
+  bool launched = false;            // the call being launched put a kernel on its stream
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
 };
 
@@ -954,7 +959,8 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
     mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
   }
-  HIPCHECK(hipEventCreateWithFlags(&mp->lastEvent, hipEventDisableTiming));
+  HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
+  HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
   HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
   HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1089,9 +1095,8 @@ void mpFree(ncclComm* c) {
   for (void* p : mp->peerMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : {(void*)mp->peerStageDev, (void*)mp->peerSFlagsDev, (void*)mp->scounters, (void*)mp->sflags,
                   (void*)mp->stage, (void*)mp->peerL128Dev, (void*)mp->l128, (void*)mp->peerLLDev, (void*)mp->ll,
-                  (void*)mp->llState})
+                  (void*)mp->llState, (void*)mp->orderMem})
     if (p) (void)hipFree(p);
-  if (mp->lastEvent) (void)hipEventDestroy(mp->lastEvent);
   if (mp->hostWords) (void)hipHostFree(mp->hostWords);
   nbx::bootstrapClose(mp->bs);
   delete mp;
@@ -1110,6 +1115,12 @@ MpProto mpProtoOf(const ncclComm* comm, const MpCall& c) {
   blockRange(c.count, eb, n, 0, &off0, &per);   // the direct schedule's AllReduce block
   return chooseProtoFor(mp->protoMask, c.kind != kReduceScatter, slotBytes, (uint64_t)per * (uint64_t)eb, n,
                         mp->llMaxBytes, mp->l128MaxBytes, mp->l128OneShotMax);
+}
+
+// The completion word this launch publishes (runMpColl numbers the call).
+nbx::MpDone mpOrderArgs(MpState* mp) {
+  mp->launched = true;
+  return nbx::MpDone{(uint64_t*)mp->orderMem, (uint32_t*)(mp->orderMem + 64), mp->curSeq};
 }
 
 // LL / LL128 protocols: small and medium collectives in one kernel (nbx_ll.h).
@@ -1141,6 +1152,7 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
             : c.kind == kReduceScatter ? nbx::kLLReduceScatter
                                        : nbx::kLLReduce;
   la.root = c.root;
+  la.order = mpOrderArgs(mp);
   if (proto == kMpLL128 || proto == kMpLL128x2) {
     la.peerL128 = mp->peerL128Dev;
     la.myL128 = mp->l128;
@@ -1208,37 +1220,42 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
   sa.slots = mp->slots;
   sa.gridMax = mp->simpleGrid;
   sa.prefetch = mp->simplePrefetch;
+  sa.order = mpOrderArgs(mp);
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
 }
 
 // One call of a multi-process communicator, ordered after the previous one:
 // the kernels share the communicator's device-resident sequencing, and NCCL's
-// calls on one communicator never overlap. A call on another stream than the
-// previous call's waits for that stream's work so far: an event is recorded
-// on the previous stream at the switch, not behind every call (an event per
-// call cost 4.6 us of host time per call: nbx_perf 4 KiB LL AllReduce 9.7 vs
-// 5.1 us, profiles/r3/nbx_perf_stream_order_r3f.txt). If the previous stream
-// has been destroyed meanwhile, the record fails and nothing is waited for:
-// hipStreamDestroy returns only after the stream's work completed
-// (scripts/probe_stream_destroy.py). Inside a stream capture the graph's own
-// edges order the captured calls; nothing is recorded there.
+// calls on one communicator never overlap. Every eager call is numbered and
+// its kernel's last block publishes the number in the communicator's done
+// word (MpDone, nbx_order.h); a call on another stream than the previous
+// one's is preceded on its stream by kMpWaitDone for the previous number. So
+// the common one-stream path adds nothing to a call, where an event recorded
+// behind every call cost ~5 us of device time per call
+// (scripts/probe_order_cost.hip: 2.9 -> 7.9 us per back-to-back tiny
+// kernel; nbx_perf 4 KiB LL AllReduce 9.7 vs 5.1 us,
+// profiles/r3/nbx_perf_stream_order_r3f.txt), and nothing ever touches a
+// stream other than the one the caller just passed (hipEventRecord on a
+// destroyed stream's handle crashes the process: scripts/probe_stream_id.hip,
+// r3g). Inside a stream capture the graph's own edges order the captured
+// calls; they are numbered 0 and publish nothing.
 ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
   MpState* mp = comm->mp;
   if (c.count == 0) return ncclSuccess;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIPCHECK(hipStreamIsCapturing(c.stream, &cap));
   const bool order = cap == hipStreamCaptureStatusNone && mp->streamOrder;
-  if (order && mp->haveLast && mp->lastStream != c.stream) {
-    if (hipEventRecord(mp->lastEvent, mp->lastStream) == hipSuccess)
-      HIPCHECK(hipStreamWaitEvent(c.stream, mp->lastEvent, 0));
-    else
-      (void)hipGetLastError();   // the previous stream is gone, and so is its work
-  }
+  if (order && mp->lastSeq != 0 && mp->lastStream != c.stream)
+    NCCLCHECK(nbx::launchMpWaitDone((const uint64_t*)mp->orderMem, mp->lastSeq, mp->hostWordsDev, mp->hostWordsDev + 1,
+                                    (uint64_t)(mp->timeoutSec * 1.0e8), c.stream));
+  mp->curSeq = order ? mp->callSeq + 1 : 0;
+  mp->launched = false;
   const MpProto proto = mpProtoOf(comm, c);
   NCCLCHECK(proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto));
-  if (order) {
+  if (order && mp->launched) {
+    mp->callSeq++;
+    mp->lastSeq = mp->callSeq;
     mp->lastStream = c.stream;
-    mp->haveLast = true;
   }
   return ncclSuccess;
 }
@@ -1314,7 +1331,7 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
   (void)hipFree(dSend);
   (void)hipFree(dRecv);
   (void)hipStreamDestroy(st);
-  mp->haveLast = false;   // the probe's work is complete; its stream is gone
+  mp->lastSeq = 0;   // the probe's work is complete; its stream is gone
   if (r != ncclSuccess) return r;
   std::vector<int32_t> all(n);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &bad, sizeof(bad), all.data()));

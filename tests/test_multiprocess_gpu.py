@@ -877,9 +877,9 @@ def _child_streams(uid_bytes, rank, n, q):
                 comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, s.cuda_stream)
             outs.append((it, cnt, x, y))
         # a call on a raw stream destroyed right after it (its work still
-        # queued), then calls on another stream: the library's switch-time event
-        # record on the destroyed stream fails and is skipped (hipStreamDestroy
-        # waited for that work)
+        # queued), then calls on another stream: the next call waits on the
+        # event recorded behind the destroyed stream's call (hipStreamDestroy
+        # waited for that work), never touching the dead stream itself
         import ctypes
         hip = ctypes.CDLL("libamdhip64.so.7")
         hip.hipStreamCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
