@@ -110,19 +110,21 @@ __device__ __forceinline__ LLCall llBegin(const LLArgs& a) {
   return c;
 }
 
-// Thread 0 of every block, after the block's reads of its own slots: the last
-// block to arrive publishes this rank's done word (= seq) in every peer's
-// buffer and advances the state for the next launch.
+// Every thread of every block, as the launch's last statement: the block's
+// memory operations complete, thread 0 arrives (nbx_order.h, per-XCD
+// counters), and the launch's last block publishes this rank's done word
+// (= seq) in every peer's buffer, advances the state for the next launch and
+// publishes the call's completion number (MpDone).
 __device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c) {
-  const uint64_t prev = __hip_atomic_fetch_add(&a.state->arrive, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev + 1 != (uint64_t)gridDim.x) return;
+  mpDrain();
+  if (threadIdx.x != 0 || !mpLastBlock(a.order.arrive)) return;
   for (int j = 0; j < a.nRanks; j++) {
     if (j == a.rank) continue;
     __hip_atomic_store(a.peerLL[j] + a.doneOff + a.rank, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __hip_atomic_store(&a.state->lastSeq[c.parity], c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&a.state->arrive, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&a.state->seq, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  mpPublish(a.order);
 }
 
 template <class Fn>
@@ -219,9 +221,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   }
 
   // done word: after every block of this launch has consumed its lines
-  __syncthreads();
-  if (threadIdx.x == 0) llEnd(a, call);
-  mpArrive(a.order);
+  llEnd(a, call);
 }
 
 
@@ -453,9 +453,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   }
 
   // done word (as kLLColl)
-  __syncthreads();
-  if (threadIdx.x == 0) llEnd(a, call);
-  mpArrive(a.order);
+  llEnd(a, call);
 }
 
 
@@ -574,9 +572,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
       if (!(t & 1)) llStoreBytes(recv + off, l128PairOff(i, t) + 8, len, ((uint64_t)pz << 32) | v[0].z);
     }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) llEnd(a, call);
-  mpArrive(a.order);
+  llEnd(a, call);
 }
 
 }  // namespace nbx

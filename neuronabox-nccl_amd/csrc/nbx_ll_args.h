@@ -15,12 +15,12 @@ constexpr int kL128LanesHost = 4;       // lanes (16 bytes each) per LL128 line
 // (plain device memory of this rank, zero at init). Kept on the device, not
 // passed by the host, so a captured graph replays with fresh sequence numbers:
 // every block of a launch reads seq at its start; the launch's last block
-// (the one whose arrival completes `arrive`) publishes the done words, then
-// advances seq / lastSeq and resets `arrive` for the next launch.
+// (found by the MpDone arrival counters, nbx_order.h) publishes the done
+// words, then advances seq / lastSeq for the next launch.
 struct LLState {
   uint64_t seq;         // last completed LL-family call (the pending one is seq + 1)
   uint64_t lastSeq[2];  // last call that used each parity's slots (credit target)
-  uint64_t arrive;      // blocks of the running launch that have finished
+  uint64_t unused;
 };
 
 // Cross-stream order of one communicator's calls (nccl_api.cc runMpColl):

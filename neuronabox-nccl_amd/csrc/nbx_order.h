@@ -10,29 +10,47 @@
 
 namespace nbx {
 
-// Called by EVERY thread of every block as the launch's last statement (the
-// early-return paths of a failed wait skip it: the communicator is broken then
-// and the waiter times out). Every thread's memory operations complete, the
-// block meets, thread 0 arrives at its XCD's counter (blockIdx.x % 8: the
-// round-robin dispatch puts such blocks on one XCD, so the 8 counters are
-// served by 8 L2s and each sees <= 32 arrivals instead of 256 on one address,
-// MI355X_MICROARCH.md 'fanin'); the last block of an XCD group arrives at the
-// top counter, and the last of those publishes the call's number.
-__device__ __forceinline__ void mpArrive(const MpDone& d) {
-  if (d.seq == 0) return;   // uniform: captured calls publish nothing
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x != 0) return;
+// Thread 0 of a block, after the whole block's memory operations completed
+// (mpDrain): arrive at this block's XCD counter (blockIdx.x % 8: round-robin
+// dispatch puts such blocks on one XCD, so the 8 counters sit in 8 L2s and
+// each sees <= 32 arrivals instead of 256 on one address, MI355X_MICROARCH.md
+// 'fanin'); the last block of an XCD group arrives at the top counter. True
+// for the launch's last block, which has reset every counter for the next
+// launch. Each arrival is a release: the block's stores are written back from
+// its XCD's L2 before the count can complete.
+__device__ __forceinline__ bool mpLastBlock(uint32_t* arrive) {
   const unsigned g = gridDim.x, x = blockIdx.x & 7u;
   const unsigned inGroup = (g - x + 7u) >> 3;   // blocks b < g with b % 8 == x
   const unsigned groups = g < 8u ? g : 8u;
-  uint32_t* const mine = d.arrive + (size_t)x * kMpArriveStride;
-  uint32_t* const top = d.arrive + (size_t)8 * kMpArriveStride;
-  if (__hip_atomic_fetch_add(mine, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u != inGroup) return;
+  uint32_t* const mine = arrive + (size_t)x * kMpArriveStride;
+  uint32_t* const top = arrive + (size_t)8 * kMpArriveStride;
+  if (__hip_atomic_fetch_add(mine, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u != inGroup) return false;
   __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups) return;
+  if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups) return false;
   __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(d.done, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// Every thread of the block: its memory operations complete, then the block meets.
+__device__ __forceinline__ void mpDrain() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+// The launch's last block publishes the call's number (a release after every
+// block's arrival) — the completion word a call on another stream waits for.
+__device__ __forceinline__ void mpPublish(const MpDone& d) {
+  if (d.seq != 0) __hip_atomic_store(d.done, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The Simple kernels' end, called by EVERY thread of every block as the
+// launch's last statement (the early-return paths of a failed wait skip it:
+// the communicator is broken then and a waiter times out). Captured calls
+// (seq 0) skip it.
+__device__ __forceinline__ void mpArrive(const MpDone& d) {
+  if (d.seq == 0) return;   // uniform
+  mpDrain();
+  if (threadIdx.x == 0 && mpLastBlock(d.arrive)) mpPublish(d);
 }
 
 }  // namespace nbx
