@@ -127,13 +127,33 @@ __device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c) {
   mpPublish(a.order);
 }
 
+// The message that pack k of the launch belongs to (a group launch's segment,
+// or the launch's single message) and k's pack index inside it.
+struct LLMsg {
+  const unsigned char* send;
+  unsigned char* recv;
+  uint64_t bytes;       // bytes per slot of this message
+  uint64_t k;           // pack index inside the message
+  uint64_t blockElts;
+};
+
+template <class E>
+__device__ __forceinline__ LLMsg llMsg(const LLArgs& a, uint64_t k) {
+  if (a.nSegs == 0)
+    return LLMsg{(const unsigned char*)a.send, (unsigned char*)a.recv, a.count * sizeof(E), k, a.blockElts};
+  int s = 0;
+  for (int q = 1; q < a.nSegs; q++)
+    if (k >= a.seg[q].packOff) s = q;
+  const LLSeg& g = a.seg[s];
+  return LLMsg{(const unsigned char*)g.send, (unsigned char*)g.recv, g.count * sizeof(E), k - g.packOff, g.blockElts};
+}
+
 template <class Fn>
 __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPK = 8 / (int)sizeof(E);   // elements per 8-byte pack
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
-  const uint64_t bytes = a.count * sizeof(E);   // bytes per slot
   const LLCall call = llBegin(a);
   const uint64_t flagHi = (uint64_t)call.flag << 32;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -152,13 +172,13 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   // 1. push two {data, flag} lines per pack into each target's slot [parity][me]
   if (!failed) {
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nPacks; k += stride) {
+      const LLMsg m = llMsg<E>(a, k);
       uint64_t whole = 0;
-      if (a.mode != kLLReduceScatter) whole = llLoadBytes((const unsigned char*)a.send, k * 8, bytes);
+      if (a.mode != kLLReduceScatter) whole = llLoadBytes(m.send, m.k * 8, m.bytes);
       for (int j = 0; j < n; j++) {
         if (!llIsTarget(a, j)) continue;
-        const uint64_t v = a.mode == kLLReduceScatter
-                               ? llLoadBytes((const unsigned char*)a.send + (uint64_t)j * bytes, k * 8, bytes)
-                               : whole;
+        const uint64_t v = a.mode == kLLReduceScatter ? llLoadBytes(m.send + (uint64_t)j * m.bytes, m.k * 8, m.bytes)
+                                                      : whole;
         const uint64_t l0 = (v & 0xffffffffull) | flagHi, l1 = (v >> 32) | flagHi;
         uint64_t* line = a.peerLL[j] + ((uint64_t)(call.parity * n + me) * a.slotLines + 2 * k);
         __hip_atomic_store(line, l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -169,15 +189,16 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
 
   // 2.+3. poll own slots, fold in the direct order, store the result
   const bool receives = a.mode != kLLReduce || me == a.root;
-  const unsigned char* own = (const unsigned char*)a.send + (a.mode == kLLReduceScatter ? (uint64_t)me * bytes : 0);
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; receives && k < a.nPacks; k += stride) {
     union Pk {
       uint64_t u;
       E e[EPK];
     };
+    const LLMsg m = llMsg<E>(a, k);
+    const unsigned char* own = m.send + (a.mode == kLLReduceScatter ? (uint64_t)me * m.bytes : 0);
     int first;
     if (a.mode == kLLAllReduce) {
-      const int c = (int)((k * EPK) / a.blockElts);   // packs never straddle 16-B-aligned blocks
+      const int c = (int)((m.k * EPK) / m.blockElts);   // packs never straddle 16-B-aligned blocks
       first = (c + 1) % n;
     } else {
       first = ((a.mode == kLLReduce ? a.root : me) + 1) % n;
@@ -188,7 +209,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
       const int j = (first + q) % n;
       Pk x;
       if (j == me) {
-        x.u = llLoadBytes(own, k * 8, bytes);
+        x.u = llLoadBytes(own, m.k * 8, m.bytes);
       } else {
         const uint64_t* line = a.myLL + ((uint64_t)(call.parity * n + j) * a.slotLines + 2 * k);
         uint64_t l0 = 0, l1 = 0;
@@ -217,7 +238,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
         for (int e = 0; e < EPK; e++) acc.e[e] = fn.post(acc.e[e]);
       }
     }
-    llStoreBytes((unsigned char*)a.recv, k * 8, bytes, acc.u);
+    llStoreBytes(m.recv, m.k * 8, m.bytes, acc.u);
   }
 
   // done word: after every block of this launch has consumed its lines

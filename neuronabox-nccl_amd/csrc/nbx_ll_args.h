@@ -39,6 +39,21 @@ struct MpDone {
   uint64_t seq;
 };
 
+// A group of small collectives as ONE LL launch (nccl_api.cc runMpGroup; NCCL
+// packs a group's collectives into one kernel's work, enqueue.cc:67-91): the
+// messages' slots are concatenated, 8-byte packs [packOff, packOff + packs of
+// this message) of the launch belong to segment s. Every segment has the
+// launch's kind, datatype, op (and root). nSegs = 0: the single message of
+// send / recv / count / blockElts.
+constexpr int kLLMaxSegs = 16;
+struct LLSeg {
+  const void* send;
+  void* recv;
+  uint64_t count;       // elements per slot (ReduceScatter: recvcount)
+  uint64_t packOff;     // first pack of this message in the launch's slot
+  uint64_t blockElts;   // AllReduce: the message's direct-schedule block (fold order)
+};
+
 struct LLArgs {
   const void* send;
   void* recv;
@@ -67,6 +82,9 @@ struct LLArgs {
   int32_t mode;            // LLMode
   int32_t root;            // kLLReduce
   MpDone order;
+  int32_t nSegs;           // kLLColl group launch: segments in seg[] (0: one message)
+  int32_t pad2;
+  LLSeg seg[kLLMaxSegs];
 };
 
 // ---------------------------------------------------------------------------

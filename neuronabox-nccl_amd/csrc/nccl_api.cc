@@ -720,6 +720,8 @@ struct MpState {
   uint64_t curSeq = 0;              // number of the call being launched (0: captured)
   bool launched = false;            // the call being launched put a kernel on its stream
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
+  bool groupBatch = true;           // NBX_GROUP_BATCH=0: every grouped call its own kernel
+  std::vector<hipEvent_t> groupEvents;   // fan-in / fan-out of a group launch over several streams
 };
 
 // Exchanged before anything is allocated: where every rank runs.
@@ -958,6 +960,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
     mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
     mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
+    mp->groupBatch = envLong("NBX_GROUP_BATCH", 1) != 0;
   }
   HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
   HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
@@ -1098,6 +1101,7 @@ void mpFree(ncclComm* c) {
                   (void*)mp->llState, (void*)mp->orderMem})
     if (p) (void)hipFree(p);
   if (mp->hostWords) (void)hipHostFree(mp->hostWords);
+  for (hipEvent_t e : mp->groupEvents) (void)hipEventDestroy(e);
   nbx::bootstrapClose(mp->bs);
   delete mp;
   c->mp = nullptr;
@@ -1124,7 +1128,8 @@ nbx::MpDone mpOrderArgs(MpState* mp) {
 }
 
 // LL / LL128 protocols: small and medium collectives in one kernel (nbx_ll.h).
-ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
+ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const MpCall* segs = nullptr,
+                        int nSegs = 0) {
   MpState* mp = comm->mp;
   const int n = comm->nRanks, me = comm->rank;
   const int eb = typeSize(c.dt);
@@ -1166,6 +1171,18 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto) {
     }
     la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
     return nbx::launchLL128Coll(c.dt, c.op, la, c.stream);
+  }
+  if (nSegs > 1) {   // a group's calls as one launch (runMpLLGroup): their slots concatenated
+    uint64_t packs = 0;
+    for (int s = 0; s < nSegs; s++) {
+      const MpCall& g = segs[s];
+      size_t o, p;
+      blockRange(g.count, eb, n, 0, &o, &p);
+      la.seg[s] = nbx::LLSeg{g.send, g.recv, (uint64_t)g.count, packs, p > 0 ? (uint64_t)p : 1};
+      packs += ((uint64_t)g.count * (uint64_t)eb + 7) / 8;
+    }
+    la.nSegs = nSegs;
+    la.nPacks = packs;
   }
   return nbx::launchLLColl(c.dt, c.op, la, c.stream);
 }
@@ -1239,23 +1256,60 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
 // destroyed stream's handle crashes the process: scripts/probe_stream_id.hip,
 // r3g). Inside a stream capture the graph's own edges order the captured
 // calls; they are numbered 0 and publish nothing.
-ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
+// The cross-stream order around one launch on `stream` (see above).
+template <class Launch>
+ncclResult_t runMpOrdered(ncclComm* comm, hipStream_t stream, Launch&& launch) {
   MpState* mp = comm->mp;
-  if (c.count == 0) return ncclSuccess;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  HIPCHECK(hipStreamIsCapturing(c.stream, &cap));
+  HIPCHECK(hipStreamIsCapturing(stream, &cap));
   const bool order = cap == hipStreamCaptureStatusNone && mp->streamOrder;
-  if (order && mp->lastSeq != 0 && mp->lastStream != c.stream)
+  if (order && mp->lastSeq != 0 && mp->lastStream != stream)
     NCCLCHECK(nbx::launchMpWaitDone((const uint64_t*)mp->orderMem, mp->lastSeq, mp->hostWordsDev, mp->hostWordsDev + 1,
-                                    (uint64_t)(mp->timeoutSec * 1.0e8), c.stream));
+                                    (uint64_t)(mp->timeoutSec * 1.0e8), stream));
   mp->curSeq = order ? mp->callSeq + 1 : 0;
   mp->launched = false;
-  const MpProto proto = mpProtoOf(comm, c);
-  NCCLCHECK(proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto));
+  NCCLCHECK(launch());
   if (order && mp->launched) {
     mp->callSeq++;
     mp->lastSeq = mp->callSeq;
-    mp->lastStream = c.stream;
+    mp->lastStream = stream;
+  }
+  return ncclSuccess;
+}
+
+ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
+  if (c.count == 0) return ncclSuccess;
+  return runMpOrdered(comm, c.stream, [&]() -> ncclResult_t {
+    const MpProto proto = mpProtoOf(comm, c);
+    return proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto);
+  });
+}
+
+// Several LL-sized calls of one group as ONE kernel (NCCL aggregates a group's
+// collectives into one launch, enqueue.cc:67-91): their slots concatenated
+// (LLSeg). The launch goes on the first call's stream; if the calls use other
+// streams too, the first waits for them before it and they wait for it after
+// (NCCL's fan-in / fan-out, enqueue.cc:964-995, 1135-1148).
+ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc) {
+  MpState* mp = comm->mp;
+  hipStream_t s0 = calls[0].stream;
+  std::vector<hipStream_t> others;
+  for (int k = 1; k < nc; k++)
+    if (calls[k].stream != s0 && std::find(others.begin(), others.end(), calls[k].stream) == others.end())
+      others.push_back(calls[k].stream);
+  while (mp->groupEvents.size() < others.size() + 1) {
+    hipEvent_t e;
+    HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    mp->groupEvents.push_back(e);
+  }
+  for (size_t k = 0; k < others.size(); k++) {
+    HIPCHECK(hipEventRecord(mp->groupEvents[k + 1], others[k]));
+    HIPCHECK(hipStreamWaitEvent(s0, mp->groupEvents[k + 1], 0));
+  }
+  NCCLCHECK(runMpOrdered(comm, s0, [&]() { return mpLaunchLL(comm, calls[0], kMpLL, calls, nc); }));
+  if (!others.empty()) {
+    HIPCHECK(hipEventRecord(mp->groupEvents[0], s0));
+    for (hipStream_t s : others) HIPCHECK(hipStreamWaitEvent(s, mp->groupEvents[0], 0));
   }
   return ncclSuccess;
 }
@@ -1355,15 +1409,40 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
 // calls in the same order, as NCCL requires.
 thread_local std::vector<ncclComm*> t_groupMpComms;
 
+// Maximal runs of consecutive LL-sized calls with the same kind, datatype, op
+// and root, whose slots fit one LL slot together (at most kLLMaxSegs), run as
+// one launch (runMpLLGroup) — a decision made from arguments every rank passes
+// identically, so every rank cuts the same runs. As in NCCL's aggregated
+// launch, collectives inside one group are independent operations: a call
+// must not read what an earlier call of the same group writes
+// (NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order).
 ncclResult_t runMpGroup(ncclComm* comm) {
   DevGuard g(comm->device);
+  MpState* mp = comm->mp;
   std::vector<MpCall> calls;
-  calls.swap(comm->mp->group);
+  calls.swap(mp->group);
   ncclResult_t r = ncclSuccess;
+  const uint64_t capPacks = mp->llSlotLines / 2;
+  auto packsOf = [](const MpCall& c) { return ((uint64_t)c.count * (uint64_t)typeSize(c.dt) + 7) / 8; };
+  auto sameOp = [](const MpCall& a, const MpCall& b) {
+    return a.kind == b.kind && a.dt == b.dt && a.op.op == b.op.op && a.op.scalarArg == b.op.scalarArg &&
+           a.op.scalarArgIsPtr == b.op.scalarArgIsPtr && (a.kind != kReduce || a.root == b.root);
+  };
   try {
-    for (const MpCall& c : calls) {
-      r = runMpColl(comm, c);
-      if (r != ncclSuccess) break;
+    size_t i = 0;
+    while (i < calls.size() && r == ncclSuccess) {
+      size_t j = i + 1;
+      if (mp->groupBatch && calls[i].count > 0 && mpProtoOf(comm, calls[i]) == kMpLL) {
+        uint64_t packs = packsOf(calls[i]);
+        while (j < calls.size() && j - i < (size_t)nbx::kLLMaxSegs && calls[j].count > 0 &&
+               sameOp(calls[i], calls[j]) && mpProtoOf(comm, calls[j]) == kMpLL &&
+               packs + packsOf(calls[j]) <= capPacks) {
+          packs += packsOf(calls[j]);
+          j++;
+        }
+      }
+      r = j - i > 1 ? runMpLLGroup(comm, &calls[i], (int)(j - i)) : runMpColl(comm, calls[i]);
+      i = j;
     }
   } catch (const std::exception& e) {
     warn("internal exception: %s", e.what());

@@ -55,6 +55,11 @@ def run(n: int, devs: list, count: int = COUNT) -> dict:
         for d in devs:
             torch.cuda.synchronize(d)
 
+    # the inputs and the -1 sentinels are written on each device's current
+    # stream; the collectives run on streams[r]: finish the former first (the
+    # N = 4 rehearsal r3k saw every element differ: the sentinel fill landed
+    # after the collective's output)
+    sync()
     def allreduce():
         nbx.group_start()
         for r in range(n):

@@ -980,3 +980,98 @@ def test_multiprocess_nonblocking_init(nbx, n, monkeypatch):
     assert res[0]["early"] == [("count", inval), ("all_reduce", inval)], res[0]
     for r in range(n):
         assert res[r]["final"] == 0 and res[r]["exact"], (r, res[r])
+
+
+# Groups of LL-sized calls run as ONE LL launch per run of compatible calls
+# (nccl_api.cc runMpGroup / runMpLLGroup): (kind, dtype, op, count, stream).
+# Runs are cut by kind / type / op / root changes, by the LL slot capacity
+# (64 KiB: the 16 x 4096-float AllReduces need four launches) and by the
+# 16-segment limit (the 40 x 10-element AllReduces: 16 + 16 + 8); stream 1
+# inside a run exercises the fan-in / fan-out across the rank's streams.
+GROUP_SMALL = ([("allreduce", 7, 0, c, 0) for c in (1, 7, 1000, 4099, 3)] + [("allreduce", 7, 0, 513, 1)] +
+               [("allreduce", 6, 4, c, 0) for c in (33, 2048, 9)] +
+               [("reducescatter", 2, 0, c, 0) for c in (5, 100, 1000, 17)] +
+               [("reduce", 9, 2, c, 0) for c in (77, 4000, 1)] +
+               [("allreduce", 7, 0, 4096, i % 2) for i in range(16)] +
+               [("allreduce", 8, 1, 10, 0) for _ in range(40)])
+
+
+def _small_inputs(oracle, k, kind, dtype, count, n, r):
+    cnt = count * n if kind == "reducescatter" else count
+    return oracle.random_inputs(dtype, n, cnt, seed=5000 + 7 * k)[r]
+
+
+def _child_group_small(uid_bytes, rank, n, q):
+    try:
+        import torch
+        from tests.conftest import load_package
+        from oracle import oracle
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        out = {}
+        for it in range(2):
+            live = []
+            nbx.group_start()
+            for k, (kind, dtype, op, count, si) in enumerate(GROUP_SMALL):
+                x = _small_inputs(oracle, k, kind, dtype, count, n, rank)
+                tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+                ty = torch.full((count * x.itemsize,), 0xAB, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                s = streams[si].cuda_stream
+                if kind == "allreduce":
+                    comm.all_reduce(tx.data_ptr(), ty.data_ptr(), count, dtype, op, s)
+                elif kind == "reducescatter":
+                    comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), count, dtype, op, s)
+                else:
+                    comm.reduce(tx.data_ptr(), ty.data_ptr() if rank == 1 % n else 0, count, dtype, op, 1 % n, s)
+                live.append((k, tx, ty))
+            nbx.group_end()
+            torch.cuda.synchronize()
+            for k, tx, ty in live:
+                out[(it, k)] = ty.cpu().numpy().copy()
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n,batch", [(2, "1"), (3, "1"), (3, "0")])
+def test_multiprocess_grouped_small_calls_one_launch(nbx, oracle, n, batch, monkeypatch):
+    """Bit-exact vs the oracle in the direct schedule's order, batched into LL
+    group launches (NBX_GROUP_BATCH=1, default) and one kernel per call (0)."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL_MAX_GRID", "64")
+    monkeypatch.setenv("NBX_GROUP_BATCH", batch)
+    res = _run_ranks(nbx, n, _child_group_small)
+    for k, (kind, dtype, op, count, si) in enumerate(GROUP_SMALL):
+        xs = [_small_inputs(oracle, k, kind, dtype, count, n, r) for r in range(n)]
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        st = oracle.NP_STORAGE[dtype]
+        eb = np.dtype(st).itemsize
+        blocks = ([(b * count, (b + 1) * count) for b in range(n)] if kind == "reducescatter"
+                  else _blocks(xs[0].size, eb, n))
+        full = np.empty(xs[0].size, dtype=st)
+        for b, (lo, hi) in enumerate(blocks):
+            if hi > lo:
+                first = (1 % n if kind == "reduce" else b) + 1
+                order = [(first + j) % n for j in range(n)]
+                full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg,
+                                                  n_pre_op_srcs=n, post_op=devop == 4)[0]
+        for it in range(2):
+            for r in range(n):
+                got = res[r][(it, k)].view(st)
+                if kind == "allreduce":
+                    exp = full
+                elif kind == "reducescatter":
+                    exp = full[r * count:(r + 1) * count]
+                elif r != 1 % n:
+                    continue
+                else:
+                    exp = full
+                assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, k, kind, dtype, op, count, r)
