@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""mp_stress.py — randomized stress of the multi-process communicator (one
+process per rank, every rank on GPU 0): each iteration every rank draws the
+same random plan from a shared seed — a sequence of AllReduce /
+ReduceScatter / Reduce calls of random datatype, op, size (spanning LL, LL128
+one- and two-shot and Simple), stream (two per rank, no caller ordering
+between them) and group boundaries (runs of calls inside ncclGroupStart/End,
+where compatible LL-sized calls become one launch) — issues it without host
+synchronisation, then checks every output exactly against torch on the GPU
+(small-integer inputs, so every fold order gives the same value; every rank
+regenerates every rank's input from the seed). Reports one JSON line per rank
+count: iterations, calls, mismatches, first errors.
+usage: mp_stress.py [ranks list, default 2,3] [iterations, default 40] [seed]
+"""
+from __future__ import annotations
+
+import json
+import multiprocessing as mp
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# (ncclDataType, torch dtype name); ops: 0 sum, 2 max, 3 min
+TYPES = [(7, "float32"), (2, "int32"), (4, "int64"), (6, "float16"), (9, "bfloat16")]
+SIZES = [1, 3, 100, 1000, 4099, 16384, 40000, 200000, 1 << 20, 3 << 20]
+
+
+def plan(rng, n):
+    calls = []
+    for _ in range(rng.randint(4, 24)):
+        kind = rng.choice(["allreduce", "allreduce", "reducescatter", "reduce"])
+        dt, tname = rng.choice(TYPES)
+        op = rng.choice([0, 0, 2, 3])
+        count = rng.choice(SIZES)
+        if tname in ("float16", "bfloat16") and op == 0:
+            count = min(count, 40000)
+        calls.append({"kind": kind, "dt": dt, "t": tname, "op": op, "count": count, "stream": rng.randint(0, 1),
+                      "root": rng.randrange(n), "group": rng.random() < 0.5})
+    return calls
+
+
+def _input(torch, c, r, it, k, n, dev):
+    total = c["count"] * (n if c["kind"] == "reducescatter" else 1)
+    i = torch.arange(total, device=dev, dtype=torch.int64)
+    # values small enough that any fold order of n <= 8 sums is exact in fp16 / bf16
+    v = (i * 7 + 13 * r + 31 * it + 5 * k) % 16
+    return v.to(getattr(torch, c["t"]))
+
+
+def rank_main(rank, n, iters, seed, q):
+    try:
+        import random
+
+        import torch
+        from __graft_entry__ import _load_package
+        nbx = _load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        uid_path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"nbx_mp_stress_{seed}_{n}.uid")
+        if rank == 0:
+            uid = bytes(nbx.get_unique_id())
+            with open(uid_path + ".tmp", "wb") as f:
+                f.write(uid)
+            os.replace(uid_path + ".tmp", uid_path)
+        else:
+            import time
+            t0 = time.time()
+            while not os.path.exists(uid_path):
+                if time.time() - t0 > 60:
+                    raise RuntimeError("no unique id")
+                time.sleep(0.05)
+            with open(uid_path, "rb") as f:
+                uid = f.read()
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid), rank)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        bad, ncalls, errs = 0, 0, []
+        for it in range(iters):
+            rng = random.Random(seed * 1000 + it)
+            calls = plan(rng, n)
+            live = []
+            in_group = False
+            torch.cuda.synchronize()
+            for k, c in enumerate(calls):
+                x = _input(torch, c, rank, it, k, n, dev)
+                y = torch.full((c["count"],), -3, device=dev, dtype=x.dtype)
+                torch.cuda.synchronize()
+                if c["group"] and not in_group:
+                    nbx.group_start()
+                    in_group = True
+                elif not c["group"] and in_group:
+                    nbx.group_end()
+                    in_group = False
+                s = streams[c["stream"]].cuda_stream
+                if c["kind"] == "allreduce":
+                    comm.all_reduce(x.data_ptr(), y.data_ptr(), c["count"], c["dt"], c["op"], s)
+                elif c["kind"] == "reducescatter":
+                    comm.reduce_scatter(x.data_ptr(), y.data_ptr(), c["count"], c["dt"], c["op"], s)
+                else:
+                    comm.reduce(x.data_ptr(), y.data_ptr() if rank == c["root"] else 0, c["count"], c["dt"], c["op"],
+                                c["root"], s)
+                live.append((k, c, x, y))   # x too: a queued or in-flight call still reads it
+            if in_group:
+                nbx.group_end()
+            torch.cuda.synchronize()
+            for k, c, _x, y in live:
+                ncalls += 1
+                xs = [_input(torch, c, r, it, k, n, dev) for r in range(n)]
+                st = torch.stack([t.to(torch.float64) for t in xs])
+                ref = st.sum(0) if c["op"] == 0 else (st.amax(0) if c["op"] == 2 else st.amin(0))
+                ref = ref.to(y.dtype)
+                if c["kind"] == "reducescatter":
+                    ref = ref[rank * c["count"]:(rank + 1) * c["count"]]
+                if c["kind"] == "reduce" and rank != c["root"]:
+                    continue
+                if not torch.equal(y, ref):
+                    bad += 1
+                    if len(errs) < 5:
+                        errs.append({"it": it, "k": k, "call": c, "wrong": int((y != ref).sum())})
+        ok = comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, {"calls": ncalls, "mismatches": bad, "errors": errs, "async_ok": ok}))
+    except Exception:
+        import traceback
+        q.put((rank, {"exception": traceback.format_exc()[-2000:]}))
+
+
+def main():
+    ns = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [2, 3]
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    seed = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
+    os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "60")
+    os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
+    os.environ.setdefault("NBX_LL_MAX_GRID", "64")
+    ctx = mp.get_context("spawn")
+    for n in ns:
+        q = ctx.Queue()
+        procs = [ctx.Process(target=rank_main, args=(r, n, iters, seed, q), daemon=True) for r in range(n)]
+        for p in procs:
+            p.start()
+        res = {}
+        try:
+            for _ in range(n):
+                r, out = q.get(timeout=600)
+                res[r] = out
+        finally:
+            for p in procs:
+                p.join(30)
+                if p.is_alive():
+                    p.terminate()
+        print(json.dumps({"n": n, "iters": iters, "seed": seed, "ranks": res}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
