@@ -50,7 +50,7 @@ def _input(torch, c, r, it, k, n, dev):
     return v.to(getattr(torch, c["t"]))
 
 
-def rank_main(rank, n, iters, seed, q):
+def rank_main(rank, n, iters, seed, uid, q):
     try:
         import random
 
@@ -60,21 +60,6 @@ def rank_main(rank, n, iters, seed, q):
         nbx.load_library()
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        uid_path = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"nbx_mp_stress_{seed}_{n}.uid")
-        if rank == 0:
-            uid = bytes(nbx.get_unique_id())
-            with open(uid_path + ".tmp", "wb") as f:
-                f.write(uid)
-            os.replace(uid_path + ".tmp", uid_path)
-        else:
-            import time
-            t0 = time.time()
-            while not os.path.exists(uid_path):
-                if time.time() - t0 > 60:
-                    raise RuntimeError("no unique id")
-                time.sleep(0.05)
-            with open(uid_path, "rb") as f:
-                uid = f.read()
         comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid), rank)
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
         bad, ncalls, errs = 0, 0, []
@@ -137,9 +122,12 @@ def main():
     os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
     os.environ.setdefault("NBX_LL_MAX_GRID", "64")
     ctx = mp.get_context("spawn")
+    from __graft_entry__ import _load_package
+    nbx = _load_package()   # the bootstrap root is a host thread of this process; no GPU use here
     for n in ns:
+        uid = bytes(nbx.get_unique_id())
         q = ctx.Queue()
-        procs = [ctx.Process(target=rank_main, args=(r, n, iters, seed, q), daemon=True) for r in range(n)]
+        procs = [ctx.Process(target=rank_main, args=(r, n, iters, seed, uid, q), daemon=True) for r in range(n)]
         for p in procs:
             p.start()
         res = {}
