@@ -127,8 +127,10 @@ __device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c) {
   mpPublish(a.order);
 }
 
-// The message that pack k of the launch belongs to (a group launch's segment,
-// or the launch's single message) and k's pack index inside it.
+// The message that unit k of the launch belongs to (a group launch's segment,
+// or the launch's single message) and k's index inside it. The unit is the
+// 8-byte pack in kLLColl and the 48-byte line in kLL128Coll (LLSeg.packOff
+// counts the launch's units).
 struct LLMsg {
   const unsigned char* send;
   unsigned char* recv;
@@ -367,7 +369,7 @@ __device__ __forceinline__ bool l128Poll(const LLArgs& a, __amdgpu_buffer_rsrc_t
 // to `sink(k, byteOffset, word)`: lane A words k = 0 (W0), 1 (W1); lane B k = 0 (W2).
 template <class Fn, class Sink>
 __device__ __forceinline__ void l128FoldLine(const Fn& fn, const LLArgs& a, const u32x4 (&v)[kL128MaxRanks], uint64_t i,
-                                             int t, int fixedFirst, Sink sink) {
+                                             int t, int fixedFirst, uint64_t blockElts, Sink sink) {
   using E = typename Fn::Elt;
   constexpr int EPK = 8 / (int)sizeof(E);
   const int n = a.nRanks;
@@ -380,7 +382,7 @@ __device__ __forceinline__ void l128FoldLine(const Fn& fn, const LLArgs& a, cons
     const uint64_t off = k ? l128PairOff(i, t) + 8 : l128WordOff(i, t);
     int first = fixedFirst;
     if (first < 0) {   // AllReduce: the word's block c folds c+1, ..., c (8-byte words never straddle blocks)
-      const int c = (int)((off / sizeof(E)) / a.blockElts);
+      const int c = (int)((off / sizeof(E)) / blockElts);
       first = (c + 1) % n;
     }
     union Pk {
@@ -416,7 +418,6 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   const Fn fn(llLoadArg<Fn>(a));
   const int n = a.nRanks, me = a.rank;
   const int t = (int)(threadIdx.x % kL128Lanes);   // lane within the line's group
-  const uint64_t bytes = a.count * sizeof(E);
   const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) / kL128Lanes;
   const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kL128Lanes;
   const uint64_t t0 = wall_clock64();
@@ -432,16 +433,16 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   __syncthreads();
   bool failed = sFailed != 0;
 
-  // 1. push: line i of the message into slot [parity][me] of every target
+  // 1. push: line i of the launch (line m.k of its message) into slot [parity][me] of every target
   if (!failed) {
     for (uint64_t i = g0; i < a.nLines; i += groups) {
+      const LLMsg m = llMsg<E>(a, i);
       u32x4 whole = {0, 0, 0, 0};
-      if (a.mode != kLLReduceScatter) whole = l128Chunk((const unsigned char*)a.send, bytes, i, t, call.flag);
+      if (a.mode != kLLReduceScatter) whole = l128Chunk(m.send, m.bytes, m.k, t, call.flag);
       for (int j = 0; j < n; j++) {
         if (!llIsTarget(a, j)) continue;
-        const u32x4 v = a.mode == kLLReduceScatter
-                            ? l128Chunk((const unsigned char*)a.send + (uint64_t)j * bytes, bytes, i, t, call.flag)
-                            : whole;
+        const u32x4 v = a.mode == kLLReduceScatter ? l128Chunk(m.send + (uint64_t)j * m.bytes, m.bytes, m.k, t, call.flag)
+                                                   : whole;
         l128StoreLine16(a.peerL128[j], a.l128Bytes,
                         ((uint64_t)(call.parity * n + me) * a.l128SlotLines + i) * (kL128LineBytes / 8) + 2 * t, v);
       }
@@ -450,26 +451,27 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
 
   // 2.+3. poll own slots (every source's chunk of line i in registers), fold, store
   const bool receives = a.mode != kLLReduce || me == a.root;
-  const unsigned char* own = (const unsigned char*)a.send + (a.mode == kLLReduceScatter ? (uint64_t)me * bytes : 0);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.myL128, (short)0, (int)a.l128Bytes,
                                                                       0x00020000);
   const int fixedFirst = a.mode == kLLAllReduce ? -1 : ((a.mode == kLLReduce ? a.root : me) + 1) % n;
   for (uint64_t i = g0; receives && !failed && i < a.nLines; i += groups) {
+    const LLMsg m = llMsg<E>(a, i);
+    const unsigned char* own = m.send + (a.mode == kLLReduceScatter ? (uint64_t)me * m.bytes : 0);
     u32x4 v[kL128MaxRanks];
     uint32_t need = 0;
 #pragma unroll
     for (int q = 0; q < kL128MaxRanks; q++) {
       v[q] = (u32x4){0, 0, 0, 0};
       if (q < n) {
-        if (q == me) v[q] = l128Chunk(own, bytes, i, t, 0);
+        if (q == me) v[q] = l128Chunk(own, m.bytes, m.k, t, 0);
         else need |= 1u << q;
       }
     }
     failed = !l128Poll(a, rs, v, need, call.flag, kDiagLL128Line, t0, t, [&](int q) {
       return (uint32_t)((((uint64_t)(call.parity * n + q)) * a.l128SlotLines + i) * kL128LineBytes);
     });
-    l128FoldLine(fn, a, v, i, t, fixedFirst, [&](int, uint64_t off, uint64_t w) {
-      llStoreBytes((unsigned char*)a.recv, off, bytes, w);
+    l128FoldLine(fn, a, v, m.k, t, fixedFirst, m.blockElts, [&](int, uint64_t off, uint64_t w) {
+      llStoreBytes(m.recv, off, m.bytes, w);
     });
   }
 
@@ -563,7 +565,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
       failed = !l128Poll(a, rs, v, need, call.flag, kDiagLL128RS, t0, t,
                          [&](int q) { return (uint32_t)((subSlot(0, q) + i) * kL128LineBytes); });
       uint64_t w[2] = {0, 0};
-      l128FoldLine(fn, a, v, i, t, first, [&](int k, uint64_t o, uint64_t r) {
+      l128FoldLine(fn, a, v, i, t, first, a.blockElts, [&](int k, uint64_t o, uint64_t r) {
         w[k] = r;
         if (!reduce || me == a.root) llStoreBytes(recv + off, o, len, r);
       });

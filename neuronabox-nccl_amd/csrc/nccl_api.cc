@@ -1158,32 +1158,36 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
                                        : nbx::kLLReduce;
   la.root = c.root;
   la.order = mpOrderArgs(mp);
+  // a group's calls as one launch (runMpLLGroup): their slots concatenated, in
+  // units of 8-byte packs (LL) or 48-byte lines (LL128 one-shot)
+  const uint64_t unit = proto == kMpLL ? 8 : (uint64_t)nbx::kL128DataBytesHost;
+  uint64_t units = 0;
+  if (nSegs > 1) {
+    for (int s = 0; s < nSegs; s++) {
+      const MpCall& g = segs[s];
+      size_t o, p;
+      blockRange(g.count, eb, n, 0, &o, &p);
+      la.seg[s] = nbx::LLSeg{g.send, g.recv, (uint64_t)g.count, units, p > 0 ? (uint64_t)p : 1};
+      units += ((uint64_t)g.count * (uint64_t)eb + unit - 1) / unit;
+    }
+    la.nSegs = nSegs;
+  }
   if (proto == kMpLL128 || proto == kMpLL128x2) {
     la.peerL128 = mp->peerL128Dev;
     la.myL128 = mp->l128;
     la.l128SlotLines = mp->l128SlotLines;
     la.l128Bytes = (uint32_t)mp->l128Bytes;
     if (proto == kMpLL128x2) {
+      la.nSegs = 0;   // never grouped (runMpGroup)
       la.nLines = mp->l128SlotLines / 2;   // sub-slot lines: [parity][RS|AG][source]
       const uint64_t blockLines =
           ((uint64_t)per * (uint64_t)eb + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
       return nbx::launchLL128AllReduce2(c.dt, c.op, la, blockLines, c.stream);
     }
-    la.nLines = (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+    la.nLines = nSegs > 1 ? units : (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
     return nbx::launchLL128Coll(c.dt, c.op, la, c.stream);
   }
-  if (nSegs > 1) {   // a group's calls as one launch (runMpLLGroup): their slots concatenated
-    uint64_t packs = 0;
-    for (int s = 0; s < nSegs; s++) {
-      const MpCall& g = segs[s];
-      size_t o, p;
-      blockRange(g.count, eb, n, 0, &o, &p);
-      la.seg[s] = nbx::LLSeg{g.send, g.recv, (uint64_t)g.count, packs, p > 0 ? (uint64_t)p : 1};
-      packs += ((uint64_t)g.count * (uint64_t)eb + 7) / 8;
-    }
-    la.nSegs = nSegs;
-    la.nPacks = packs;
-  }
+  if (nSegs > 1) la.nPacks = units;
   return nbx::launchLLColl(c.dt, c.op, la, c.stream);
 }
 
@@ -1285,12 +1289,12 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
   });
 }
 
-// Several LL-sized calls of one group as ONE kernel (NCCL aggregates a group's
+// Several LL / LL128 one-shot calls of one group as ONE kernel (NCCL aggregates a group's
 // collectives into one launch, enqueue.cc:67-91): their slots concatenated
 // (LLSeg). The launch goes on the first call's stream; if the calls use other
 // streams too, the first waits for them before it and they wait for it after
 // (NCCL's fan-in / fan-out, enqueue.cc:964-995, 1135-1148).
-ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc) {
+ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc, MpProto proto) {
   MpState* mp = comm->mp;
   hipStream_t s0 = calls[0].stream;
   std::vector<hipStream_t> others;
@@ -1306,7 +1310,7 @@ ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc) {
     HIPCHECK(hipEventRecord(mp->groupEvents[k + 1], others[k]));
     HIPCHECK(hipStreamWaitEvent(s0, mp->groupEvents[k + 1], 0));
   }
-  NCCLCHECK(runMpOrdered(comm, s0, [&]() { return mpLaunchLL(comm, calls[0], kMpLL, calls, nc); }));
+  NCCLCHECK(runMpOrdered(comm, s0, [&]() { return mpLaunchLL(comm, calls[0], proto, calls, nc); }));
   if (!others.empty()) {
     HIPCHECK(hipEventRecord(mp->groupEvents[0], s0));
     for (hipStream_t s : others) HIPCHECK(hipStreamWaitEvent(s, mp->groupEvents[0], 0));
@@ -1409,9 +1413,10 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
 // calls in the same order, as NCCL requires.
 thread_local std::vector<ncclComm*> t_groupMpComms;
 
-// Maximal runs of consecutive LL-sized calls with the same kind, datatype, op
-// and root, whose slots fit one LL slot together (at most kLLMaxSegs), run as
-// one launch (runMpLLGroup) — a decision made from arguments every rank passes
+// Maximal runs of consecutive calls of the same protocol (LL, or LL128
+// one-shot) with the same kind, datatype, op and root, whose slots fit one
+// slot of that protocol together (at most kLLMaxSegs), run as one launch
+// (runMpLLGroup) — a decision made from arguments every rank passes
 // identically, so every rank cuts the same runs. As in NCCL's aggregated
 // launch, collectives inside one group are independent operations: a call
 // must not read what an earlier call of the same group writes
@@ -1422,8 +1427,12 @@ ncclResult_t runMpGroup(ncclComm* comm) {
   std::vector<MpCall> calls;
   calls.swap(mp->group);
   ncclResult_t r = ncclSuccess;
-  const uint64_t capPacks = mp->llSlotLines / 2;
-  auto packsOf = [](const MpCall& c) { return ((uint64_t)c.count * (uint64_t)typeSize(c.dt) + 7) / 8; };
+  // units of one call in its protocol's slot, and the slot's capacity
+  auto unitsOf = [&](const MpCall& c, MpProto p) {
+    const uint64_t unit = p == kMpLL ? 8 : (uint64_t)nbx::kL128DataBytesHost;
+    return ((uint64_t)c.count * (uint64_t)typeSize(c.dt) + unit - 1) / unit;
+  };
+  auto capOf = [&](MpProto p) { return p == kMpLL ? mp->llSlotLines / 2 : mp->l128SlotLines; };
   auto sameOp = [](const MpCall& a, const MpCall& b) {
     return a.kind == b.kind && a.dt == b.dt && a.op.op == b.op.op && a.op.scalarArg == b.op.scalarArg &&
            a.op.scalarArgIsPtr == b.op.scalarArgIsPtr && (a.kind != kReduce || a.root == b.root);
@@ -1432,16 +1441,17 @@ ncclResult_t runMpGroup(ncclComm* comm) {
     size_t i = 0;
     while (i < calls.size() && r == ncclSuccess) {
       size_t j = i + 1;
-      if (mp->groupBatch && calls[i].count > 0 && mpProtoOf(comm, calls[i]) == kMpLL) {
-        uint64_t packs = packsOf(calls[i]);
+      const MpProto p = calls[i].count > 0 ? mpProtoOf(comm, calls[i]) : kMpSimple;
+      if (mp->groupBatch && (p == kMpLL || p == kMpLL128)) {
+        uint64_t used = unitsOf(calls[i], p);
         while (j < calls.size() && j - i < (size_t)nbx::kLLMaxSegs && calls[j].count > 0 &&
-               sameOp(calls[i], calls[j]) && mpProtoOf(comm, calls[j]) == kMpLL &&
-               packs + packsOf(calls[j]) <= capPacks) {
-          packs += packsOf(calls[j]);
+               sameOp(calls[i], calls[j]) && mpProtoOf(comm, calls[j]) == p &&
+               used + unitsOf(calls[j], p) <= capOf(p)) {
+          used += unitsOf(calls[j], p);
           j++;
         }
       }
-      r = j - i > 1 ? runMpLLGroup(comm, &calls[i], (int)(j - i)) : runMpColl(comm, calls[i]);
+      r = j - i > 1 ? runMpLLGroup(comm, &calls[i], (int)(j - i), p) : runMpColl(comm, calls[i]);
       i = j;
     }
   } catch (const std::exception& e) {
@@ -1554,7 +1564,7 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
     warn("ncclCommInitRank : unique id was not produced by ncclGetUniqueId");
     return ncclInvalidArgument;
   }
-  if (nranks > kMaxMpRanks) {   // 64-bit rank masks in the barrier kernel, one source per rank
+  if (nranks > kMaxMpRanks) {   // one staging source region and one counter set per rank (kSimpleMaxRanks)
     warn("ncclCommInitRank : %d ranks requested, this build supports up to %d per communicator", nranks,
          kMaxMpRanks);
     return ncclInvalidArgument;

@@ -982,8 +982,9 @@ def test_multiprocess_nonblocking_init(nbx, n, monkeypatch):
         assert res[r]["final"] == 0 and res[r]["exact"], (r, res[r])
 
 
-# Groups of LL-sized calls run as ONE LL launch per run of compatible calls
-# (nccl_api.cc runMpGroup / runMpLLGroup): (kind, dtype, op, count, stream).
+# Groups of LL-sized (and LL128 one-shot sized) calls run as ONE launch per run
+# of compatible calls (nccl_api.cc runMpGroup / runMpLLGroup): (kind, dtype,
+# op, count, stream).
 # Runs are cut by kind / type / op / root changes, by the LL slot capacity
 # (64 KiB: the 16 x 4096-float AllReduces need four launches) and by the
 # 16-segment limit (the 40 x 10-element AllReduces: 16 + 16 + 8); stream 1
@@ -993,7 +994,11 @@ GROUP_SMALL = ([("allreduce", 7, 0, c, 0) for c in (1, 7, 1000, 4099, 3)] + [("a
                [("reducescatter", 2, 0, c, 0) for c in (5, 100, 1000, 17)] +
                [("reduce", 9, 2, c, 0) for c in (77, 4000, 1)] +
                [("allreduce", 7, 0, 4096, i % 2) for i in range(16)] +
-               [("allreduce", 8, 1, 10, 0) for _ in range(40)])
+               [("allreduce", 8, 1, 10, 0) for _ in range(40)] +
+               # LL128 one-shot runs (64 KiB < slot <= 256 KiB per call)
+               [("allreduce", 7, 0, c, i % 2) for i, c in enumerate((30000, 17001, 60000, 20000, 40000, 33333))] +
+               [("reducescatter", 2, 3, c, 0) for c in (20000, 17003, 30000)] +
+               [("reduce", 4, 0, c, 0) for c in (20000, 9001)])
 
 
 def _small_inputs(oracle, k, kind, dtype, count, n, r):
