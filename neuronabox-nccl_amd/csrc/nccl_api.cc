@@ -467,9 +467,13 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
                                  /*nPreOpSrcs=*/n, /*postOp=*/1, (ncclStream_t)parts[r].stream,
                                  nbx::kReduceAcquireSystem));
   }
-  for (int r = 0; r < n; r++) {
-    DevGuard g(c->devs[r]);
-    HIPCHECK(hipEventRecord(c->evReduced[r], parts[r].stream));
+  // evReduced only orders the pull gather (n > 8); each marker costs ~5 us of
+  // device time per stream (scripts/probe_order_cost.hip)
+  if (p0.kind == kAllReduce && !push) {
+    for (int r = 0; r < n; r++) {
+      DevGuard g(c->devs[r]);
+      HIPCHECK(hipEventRecord(c->evReduced[r], parts[r].stream));
+    }
   }
   NBX_TRACE("clique reduce launched");
   // 3. gather (AllReduce with n > NBX_MAX_DSTS only): rank r pulls block j from rank j's recv buffer
