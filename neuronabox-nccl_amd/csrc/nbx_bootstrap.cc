@@ -43,6 +43,10 @@ struct Hello {
   int32_t nranks;
 };
 
+thread_local const int* t_abort = nullptr;
+
+bool aborted() { return t_abort && __atomic_load_n(t_abort, __ATOMIC_RELAXED) != 0; }
+
 int timeoutMs() {
   const char* v = std::getenv("NBX_BOOTSTRAP_TIMEOUT");
   int s = (v && *v) ? std::atoi(v) : 600;
@@ -57,8 +61,9 @@ bool ioAll(int fd, void* buf, size_t n, bool writing) {
     pollfd pf{fd, (short)(writing ? POLLOUT : POLLIN), 0};
     int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now())
                    .count();
-    if (left <= 0) return false;
-    int pr = ::poll(&pf, 1, left);
+    if (left <= 0 || aborted()) return false;
+    int pr = ::poll(&pf, 1, left < 100 ? left : 100);   // slices: an abort is seen within 0.1 s
+    if (pr == 0) continue;
     if (pr < 0 && errno == EINTR) continue;
     if (pr <= 0) return false;
     ssize_t r = writing ? ::send(fd, p, n, MSG_NOSIGNAL) : ::recv(fd, p, n, 0);
@@ -193,7 +198,7 @@ ncclResult_t bootstrapConnect(const ncclUniqueId& id, int rank, int nranks, Boot
     if (::connect(fd, (sockaddr*)&sa, sizeof(sa)) == 0) break;
     ::close(fd);
     fd = -1;
-    if (std::chrono::steady_clock::now() > deadline) return ncclRemoteError;
+    if (std::chrono::steady_clock::now() > deadline || aborted()) return ncclRemoteError;
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
   setNoDelay(fd);
@@ -217,6 +222,8 @@ ncclResult_t bootstrapAllGather(Bootstrap* b, const void* mine, size_t len, void
   if (len && !ioAll(b->fd, all, len * (size_t)b->nranks, false)) return ncclRemoteError;
   return ncclSuccess;
 }
+
+void bootstrapSetAbortFlag(const int* flag) { t_abort = flag; }
 
 void bootstrapClose(Bootstrap* b) {
   if (!b) return;

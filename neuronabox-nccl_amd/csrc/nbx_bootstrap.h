@@ -28,4 +28,9 @@ ncclResult_t bootstrapAllGather(Bootstrap* b, const void* mine, size_t len, void
 
 void bootstrapClose(Bootstrap* b);
 
+// The calling thread's bootstrap waits (connect, every send / receive) also
+// end, with ncclRemoteError, once *flag != 0 — how ncclCommAbort stops a
+// non-blocking communicator's initialisation thread. nullptr: no flag.
+void bootstrapSetAbortFlag(const int* flag);
+
 }  // namespace nbx

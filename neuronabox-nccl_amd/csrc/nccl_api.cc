@@ -166,6 +166,7 @@ struct ncclComm {
   std::shared_ptr<Clique> clique;  // nRanks > 1 (single process)
   MpState* mp = nullptr;           // nRanks > 1 (one process per rank)
   std::thread initThread;          // non-blocking ncclCommInitRankConfig: mpInit in the background
+  int initAbort = 0;               // set by ncclCommAbort: the init thread's bootstrap waits end
 };
 
 namespace {
@@ -1609,7 +1610,9 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
     try {
       c->initThread = std::thread([c, commId, dev, init] {
         (void)hipSetDevice(dev);
+        nbx::bootstrapSetAbortFlag(&c->initAbort);
         c->asyncError.store(init(c, commId));
+        nbx::bootstrapSetAbortFlag(nullptr);
       });
     } catch (const std::exception& e) {
       warn("ncclCommInitRankConfig : cannot start the initialisation thread: %s", e.what());
@@ -1727,7 +1730,10 @@ NBX_API(ncclResult_t, ncclCommDestroy, ncclComm_t comm) {
 NBX_API(ncclResult_t, ncclCommAbort, ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
   NCCLCHECK(commCheck(comm, "ncclCommAbort"));
-  if (comm->initThread.joinable()) comm->initThread.join();   // a failing bootstrap ends by its timeout
+  if (comm->initThread.joinable()) {   // a pending initialisation: its bootstrap waits end at the flag
+    __atomic_store_n(&comm->initAbort, 1, __ATOMIC_RELAXED);
+    comm->initThread.join();
+  }
   if (comm->mp && comm->mp->hostWords) comm->mp->hostWords[0] = 1;   // ends every spinning barrier
   return commFree(comm);
 }

@@ -334,3 +334,20 @@ def test_graph_capture_one_rank_kernel(nbx, oracle, torch_gpu, comm1):
     exp = oracle.reduce_multi([x], F16, 3, int(h), 1, True)[0]
     assert np.array_equal(np_of(ty, np.uint16), exp)
     comm1.redop_destroy(op)
+
+
+def test_nonblocking_init_abort_is_prompt(nbx, monkeypatch):
+    """ncclCommAbort on a non-blocking communicator whose initialisation is
+    still waiting for its peers (rank 1 never comes): the background thread's
+    bootstrap waits end at the abort flag within ~0.1 s, long before the
+    bootstrap timeout, and the communicator is freed."""
+    import time
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    uid = nbx.get_unique_id()
+    comm, rc = nbx.Communicator.init_rank_config(2, uid, 0, blocking=0)
+    assert rc == int(nbx.ncclResult.ncclInProgress)
+    time.sleep(0.3)
+    assert comm.async_error() == int(nbx.ncclResult.ncclInProgress)
+    t0 = time.monotonic()
+    comm.abort()
+    assert time.monotonic() - t0 < 5.0

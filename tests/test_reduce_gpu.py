@@ -602,7 +602,7 @@ def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
         torch.cuda.synchronize()
         fb0 = lib.nbxDebugBatchListSlots(dev_id, 3)
         with torch.cuda.stream(s):
-            torch.cuda._sleep(200_000_000)   # hold the stream so the calls below pile up
+            torch.cuda._sleep(1_500_000_000)   # hold the stream (~0.6 s) so the calls below pile up, however slow the host
             for _ in range(300):   # > 128 slots in flight: the rest fall back to kernel-argument tables
                 nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
         s.synchronize()
