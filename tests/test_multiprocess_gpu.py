@@ -1,9 +1,9 @@
 """Multi-process communicators (one process per rank, ncclCommInitRank with
 nranks > 1) on the GPU box. The box has one GPU, so the ranks share device 0:
-this exercises the bootstrap, hipIpc buffer exchange + mapping cache, the
-device flag barriers and the direct reduce/gather data path end to end.
-Results are compared bit-exact with the oracle folding block r in rank order
-r+1, ..., r."""
+this exercises the bootstrap, the connection buffers every peer IPC-maps once
+at init, and the LL / LL128 / Simple (direct and ring) kernels with their
+in-kernel flow control end to end. Results are compared bit-exact with the
+oracle folding block r in rank order r+1, ..., r."""
 import multiprocessing as mp
 
 import numpy as np
@@ -203,11 +203,11 @@ def _check_cases(oracle, n, res):
                 assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, kind, dtype, op, r)
 
 
-# NCCL_ALGO=Ring ReduceScatter / Reduce through the step FIFO (nbx_ring.h
-# kRingFifo): (kind, dtype, op, count, root). RS counts whose blocks are whole
-# 16-B packs take the FIFO kernel; the bf16 RS of 777 does not (direct
-# fallback, still checked). Reduce counts with a partial last pack exercise the
-# element tail.
+# NCCL_ALGO=Ring ReduceScatter / Reduce through the Simple ring schedule
+# (nbx_simple.h kSimpleRing, hop for hop through the right neighbour's
+# staging): (kind, dtype, op, count, root). Blocks that are not whole 16-B
+# packs (the bf16 RS of 777) take the element path; Reduce counts with a
+# partial last pack exercise the element tail.
 RING_FIFO_CASES = [
     ("rs", 7, 0, 4096, 0), ("rs", 6, 4, 1 << 20, 0), ("rs", 2, 2, 300000, 0), ("rs", 9, 0, 777, 0),
     ("rs", 8, 1, 65536, 0), ("red", 7, 0, 1000003, 0), ("red", 7, 0, 250000, -1), ("red", 8, 1, 200001, 1),
