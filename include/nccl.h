@@ -149,6 +149,18 @@ ncclResult_t  ncclCommCuDevice(const ncclComm_t comm, int* device);   /* :172 */
 ncclResult_t pncclCommCuDevice(const ncclComm_t comm, int* device);
 ncclResult_t  ncclCommUserRank(const ncclComm_t comm, int* rank);     /* :176 */
 ncclResult_t pncclCommUserRank(const ncclComm_t comm, int* rank);
+ncclResult_t  ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm,
+                            ncclConfig_t* config);                     /* :150 */
+ncclResult_t pncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t* newcomm,
+                            ncclConfig_t* config);
+ncclResult_t  ncclMemAlloc(void** ptr, size_t size);                  /* :84  */
+ncclResult_t pncclMemAlloc(void** ptr, size_t size);
+ncclResult_t  ncclMemFree(void* ptr);                                 /* :87  */
+ncclResult_t pncclMemFree(void* ptr);
+ncclResult_t  ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle); /* :430 */
+ncclResult_t pncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
+ncclResult_t  ncclCommDeregister(const ncclComm_t comm, void* handle); /* :434 */
+ncclResult_t pncclCommDeregister(const ncclComm_t comm, void* handle);
 
 /* ---- user reduction operators (nccl.h.in:237-248) ---- */
 ncclResult_t  ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,

@@ -134,6 +134,11 @@ _SIGS = {
     "ncclCommFinalize": [ctypes.c_void_p],
     "ncclCommDestroy": [ctypes.c_void_p],
     "ncclCommAbort": [ctypes.c_void_p],
+    "ncclCommSplit": [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p],
+    "ncclMemAlloc": [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t],
+    "ncclMemFree": [ctypes.c_void_p],
+    "ncclCommRegister": [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)],
+    "ncclCommDeregister": [ctypes.c_void_p, ctypes.c_void_p],
     "ncclCommGetAsyncError": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],
     "ncclCommCount": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],
     "ncclCommCuDevice": [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)],
@@ -401,6 +406,27 @@ class Communicator:
 
     def finalize(self) -> None:
         _check(load_library().ncclCommFinalize(self.handle), "ncclCommFinalize")
+
+    def split(self, color: int, key: int, blocking: int | None = None):
+        """ncclCommSplit (collective over this communicator); returns (child or
+        None for NCCL_SPLIT_NOCOLOR, result code)."""
+        h = ctypes.c_void_p()
+        cfg = ncclConfig.initializer(blocking) if blocking is not None else None
+        rc = load_library().ncclCommSplit(self.handle, int(color), int(key), ctypes.byref(h),
+                                          ctypes.cast(ctypes.pointer(cfg), ctypes.c_void_p) if cfg is not None else None)
+        if rc not in (ncclResult.ncclSuccess, ncclResult.ncclInProgress):
+            _check(rc, "ncclCommSplit")
+        return (Communicator(h.value) if h.value else None), int(rc)
+
+    def register(self, ptr: int, size: int) -> int:
+        """ncclCommRegister; returns the registration handle."""
+        h = ctypes.c_void_p()
+        _check(load_library().ncclCommRegister(self.handle, ctypes.c_void_p(ptr), int(size), ctypes.byref(h)),
+               "ncclCommRegister")
+        return h.value
+
+    def deregister(self, handle: int) -> None:
+        _check(load_library().ncclCommDeregister(self.handle, ctypes.c_void_p(handle)), "ncclCommDeregister")
 
     def destroy(self) -> None:
         if self.handle:

@@ -1634,6 +1634,131 @@ NBX_API(ncclResult_t, ncclCommInitRank, ncclComm_t* newcomm, int nranks, ncclUni
   return ncclCommInitRankConfig(newcomm, nranks, commId, myrank, nullptr);
 }
 
+// ncclCommSplit (init.cc:2027-2085, commGetSplitInfo init.cc:1303-1340): a
+// collective over the parent. Every rank's (color, key) travels over the
+// parent's bootstrap; the members of a color are ordered by key, ties by
+// parent rank; the color's first member starts the child's bootstrap root
+// and its unique id reaches the others in a second allgather; every member
+// then initialises the child like ncclCommInitRankConfig (the parent's
+// blocking mode unless `config` says otherwise). NCCL_SPLIT_NOCOLOR ranks take
+// part in the allgathers and get NULL. Multi-process (and one-rank)
+// communicators only: the ranks of an ncclCommInitAll clique are driven by
+// one thread, which cannot join a collective rank by rank.
+NBX_API(ncclResult_t, ncclCommSplit, ncclComm_t comm, int color, int key, ncclComm_t* newcomm, ncclConfig_t* config) {
+  NCCLCHECK(commCheck(comm, "CommSplit"));
+  if (newcomm == nullptr) {
+    warn("CommSplit : newcomm argument is NULL");
+    return ncclInvalidArgument;
+  }
+  NCCLCHECK(commEnsureReady(comm));
+  *newcomm = nullptr;
+  if (color < 0 && color != NCCL_SPLIT_NOCOLOR) {
+    warn("CommSplit : invalid color %d", color);
+    return ncclInvalidArgument;
+  }
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  if (config == nullptr) {
+    cfg.blocking = comm->blocking;
+    config = &cfg;
+  }
+  DevGuard g(comm->device);
+  if (comm->nRanks == 1) {
+    if (color == NCCL_SPLIT_NOCOLOR) return ncclSuccess;
+    ncclUniqueId id;
+    NCCLCHECK(ncclGetUniqueId(&id));
+    return ncclCommInitRankConfig(newcomm, 1, id, 0, config);
+  }
+  if (comm->mp == nullptr) {
+    warn("CommSplit : communicators from ncclCommInitAll cannot be split here (one thread drives every rank)");
+    return ncclInvalidUsage;
+  }
+  const int n = comm->nRanks, me = comm->rank;
+  struct ColorKey {
+    int32_t color, key;
+  };
+  const ColorKey mine{color, key};
+  std::vector<ColorKey> ck(n);
+  NCCLCHECK(nbx::bootstrapAllGather(comm->mp->bs, &mine, sizeof(mine), ck.data()));
+  std::vector<int> members;   // parent ranks of my color, in child rank order
+  if (color != NCCL_SPLIT_NOCOLOR) {
+    for (int i = 0; i < n; i++) {
+      if (ck[i].color != color) continue;
+      size_t at = 0;
+      while (at < members.size() && ck[members[at]].key <= ck[i].key) at++;
+      members.insert(members.begin() + (long)at, i);
+    }
+  }
+  struct IdMsg {
+    int32_t color, leader;
+    ncclUniqueId id;
+  };
+  IdMsg msg{};
+  msg.color = color;
+  msg.leader = !members.empty() && members[0] == me;
+  if (msg.leader) NCCLCHECK(ncclGetUniqueId(&msg.id));
+  std::vector<IdMsg> ids(n);
+  NCCLCHECK(nbx::bootstrapAllGather(comm->mp->bs, &msg, sizeof(msg), ids.data()));
+  if (color == NCCL_SPLIT_NOCOLOR) return ncclSuccess;
+  const int myNew = (int)(std::find(members.begin(), members.end(), me) - members.begin());
+  return ncclCommInitRankConfig(newcomm, (int)members.size(), ids[members[0]].id, myNew, config);
+}
+
+// ncclMemAlloc / ncclMemFree (nccl.h.in:84-87): device memory for
+// communication buffers. NCCL uses cuMem allocations there so that NVLS and
+// user-buffer registration can map them; plain device memory is what every
+// path of this library uses.
+NBX_API(ncclResult_t, ncclMemAlloc, void** ptr, size_t size) {
+  if (ptr == nullptr) return ncclInvalidArgument;
+  *ptr = nullptr;
+  if (size == 0) return ncclSuccess;
+  HIPCHECK(hipMalloc(ptr, size));
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclMemFree, void* ptr) {
+  if (ptr != nullptr) HIPCHECK(hipFree(ptr));
+  return ncclSuccess;
+}
+
+// ncclCommRegister / ncclCommDeregister (nccl.h.in:430-434): user-buffer
+// registration is a zero-copy optimisation in NCCL; no path here needs it
+// (peers only ever touch the connection buffers mapped at init), so a
+// registration is a checked, owned handle and nothing else.
+namespace {
+struct RegHandle {
+  uint64_t magic;
+  ncclComm* comm;
+  void* buff;
+  size_t size;
+};
+constexpr uint64_t kRegMagic = 0x4e42585245474831ull;   // "NBXREGH1"
+}  // namespace
+
+NBX_API(ncclResult_t, ncclCommRegister, const ncclComm_t comm, void* buff, size_t size, void** handle) {
+  NCCLCHECK(commCheck(comm, "CommRegister"));
+  NCCLCHECK(commEnsureReady(comm));
+  if (handle == nullptr || (buff == nullptr && size != 0)) {
+    warn("CommRegister : invalid buffer %p / handle %p", buff, (void*)handle);
+    return ncclInvalidArgument;
+  }
+  RegHandle* h = new (std::nothrow) RegHandle{kRegMagic, comm, buff, size};
+  if (h == nullptr) return ncclSystemError;
+  *handle = h;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommDeregister, const ncclComm_t comm, void* handle) {
+  NCCLCHECK(commCheck(comm, "CommDeregister"));
+  RegHandle* h = (RegHandle*)handle;
+  if (h == nullptr || h->magic != kRegMagic || h->comm != comm) {
+    warn("CommDeregister : %p is not a registration of comm %p", handle, (void*)comm);
+    return ncclInvalidArgument;
+  }
+  h->magic = 0;
+  delete h;
+  return ncclSuccess;
+}
+
 NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* devlist) {
   // init.cc:1678-1734. Several ranks may share one device (emulation / testing).
   if (comms == nullptr || ndev < 1 || ndev > kMaxMpRanks) {

@@ -1080,3 +1080,71 @@ def test_multiprocess_grouped_small_calls_one_launch(nbx, oracle, n, batch, monk
                 else:
                     exp = full
                 assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, k, kind, dtype, op, count, r)
+
+
+def _child_split(uid_bytes, rank, n, q):
+    """ncclCommSplit over a multi-process communicator: children ordered by
+    key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;
+    ncclCommRegister / Deregister and ncclMemAlloc / Free round trips."""
+    try:
+        import ctypes
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        out = {}
+        st = torch.cuda.current_stream().cuda_stream
+        # split 1: color = rank % 2, key = n - rank (reverse order inside a color)
+        child, rc = comm.split(rank % 2, n - rank)
+        out["rc1"] = rc
+        out["child1"] = (child.count(), child.user_rank())
+        x = torch.full((1000,), float(rank + 1), device="cuda")
+        y = torch.empty_like(x)
+        child.all_reduce(x.data_ptr(), y.data_ptr(), 1000, 7, 0, st)
+        torch.cuda.synchronize()
+        out["sum1"] = float(y[0]) if torch.all(y == y[0]) else None
+        # split 2: rank 1 opts out, the rest share color 5 with equal keys (parent order)
+        child2, rc2 = comm.split(-1 if rank == 1 else 5, 0)
+        out["rc2"] = rc2
+        if child2 is not None:
+            out["child2"] = (child2.count(), child2.user_rank())
+            child2.all_reduce(x.data_ptr(), y.data_ptr(), 1000, 7, 0, st)
+            torch.cuda.synchronize()
+            out["sum2"] = float(y[0]) if torch.all(y == y[0]) else None
+            child2.destroy()
+        else:
+            out["child2"] = None
+        # registration and ncclMemAlloc
+        h = comm.register(x.data_ptr(), x.numel() * 4)
+        comm.deregister(h)
+        p = ctypes.c_void_p()
+        assert lib.ncclMemAlloc(ctypes.byref(p), 1 << 20) == 0 and p.value
+        assert lib.ncclMemFree(p) == 0
+        child.destroy()
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_comm_split(nbx, monkeypatch):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    n = 4
+    res = _run_ranks(nbx, n, _child_split)
+    for r in range(n):
+        same = [p for p in range(n) if p % 2 == r % 2]
+        order = sorted(same, key=lambda p: (n - p, p))
+        assert res[r]["rc1"] == 0
+        assert res[r]["child1"] == (len(same), order.index(r)), (r, res[r])
+        assert res[r]["sum1"] == float(sum(p + 1 for p in same)), (r, res[r])
+        if r == 1:
+            assert res[r]["child2"] is None
+        else:
+            members = [p for p in range(n) if p != 1]
+            assert res[r]["child2"] == (len(members), members.index(r)), (r, res[r])
+            assert res[r]["sum2"] == float(sum(p + 1 for p in members)), (r, res[r])
