@@ -460,7 +460,9 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
 
 # fp32 counts -> protocol by default (2-3 ranks): LL, LL128 one-shot, LL128
 # two-shot (3 ranks; one-shot at 2), Simple
-GRAPH_CASES = [(1000, "LL"), (50003, "LL128"), (300001, "LL128 two-shot"), (1500000, "Simple")]
+GRAPH_CASES = [(1000, "LL"), (50003, "LL128"), (300001, "LL128 two-shot"), (1500000, "Simple"),
+               # one ncclGroupStart/End: two LL-sized calls and two LL128 one-shot calls -> two group launches
+               (777, "LL group"), (4099, "LL group"), (20000, "LL128 group"), (30001, "LL128 group")]
 
 
 def _child_graph(uid_bytes, uid_ring_bytes, rank, n, q):
@@ -486,10 +488,21 @@ def _child_graph(uid_bytes, uid_ring_bytes, rank, n, q):
             y = torch.empty(cnt, device="cuda")
             bufs.append((cnt, x, y))
 
+        labels = [lab for _, lab in GRAPH_CASES] + ["ring"]
+
         def issue(st):
+            grouped = False
             for i, (cnt, x, y) in enumerate(bufs):
+                if labels[i].endswith("group") and not grouped:
+                    nbx.group_start()
+                    grouped = True
+                elif not labels[i].endswith("group") and grouped:
+                    nbx.group_end()
+                    grouped = False
                 c = ring if i == len(bufs) - 1 else comm
                 c.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, st)
+            if grouped:
+                nbx.group_end()
 
         def fill(it):
             for cnt, x, y in bufs:
