@@ -1532,8 +1532,11 @@ ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclCo
   const char* cp = std::getenv("NCCL_CHECK_POINTERS");
   c->checkPointers = cp && std::atoi(cp) != 0;
   if (config && config->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = config->blocking;
-  const char* be = std::getenv("NCCL_COMM_BLOCKING");   // init.cc:1444-1446: the env overrides the config
-  if (be && (std::atoi(be) == 0 || std::atoi(be) == 1) && *be != '\0') c->blocking = std::atoi(be);
+  if (const char* be = std::getenv("NCCL_COMM_BLOCKING")) {   // init.cc:1444-1446: the env overrides the config
+    char* end = nullptr;
+    const long v = std::strtol(be, &end, 10);
+    if (end != be && *end == '\0' && (v == 0 || v == 1)) c->blocking = (int)v;
+  }
   *out = c;
   return ncclSuccess;
 }
