@@ -123,7 +123,7 @@ __device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c) {
     __hip_atomic_store(a.peerLL[j] + a.doneOff + a.rank, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __hip_atomic_store(&a.state->lastSeq[c.parity], c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&a.state->seq, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&a.state->seq, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (nbx_order.h)
   mpPublish(a.order);
 }
 

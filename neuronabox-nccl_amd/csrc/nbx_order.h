@@ -16,17 +16,25 @@ namespace nbx {
 // each sees <= 32 arrivals instead of 256 on one address, MI355X_MICROARCH.md
 // 'fanin'); the last block of an XCD group arrives at the top counter. True
 // for the launch's last block, which has reset every counter for the next
-// launch. Each arrival is a release: the block's stores are written back from
-// its XCD's L2 before the count can complete.
+// launch.
+// The arrivals are RELAXED atomics, not releases: the state a later kernel of
+// the communicator reads (Simple counters, LLState) is stored write-through
+// (agent-scope atomic stores, `sc1`) and drained by every wave before its
+// block arrives, and a later kernel's dispatch invalidates its caches — the
+// guide's write-through hand-off (MI355X_MICROARCH.md, "Valid forms": `sc1`
+// stores, drained, then the counter add; the adder whose add came last
+// signals). Caller buffers are the caller's to order across streams, as with
+// any kernel. A release here was an L2 write-back (`buffer_wbl2 sc1`) per
+// block and per step of the chain — four in the last block's path.
 __device__ __forceinline__ bool mpLastBlock(uint32_t* arrive) {
   const unsigned g = gridDim.x, x = blockIdx.x & 7u;
   const unsigned inGroup = (g - x + 7u) >> 3;   // blocks b < g with b % 8 == x
   const unsigned groups = g < 8u ? g : 8u;
   uint32_t* const mine = arrive + (size_t)x * kMpArriveStride;
   uint32_t* const top = arrive + (size_t)8 * kMpArriveStride;
-  if (__hip_atomic_fetch_add(mine, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u != inGroup) return false;
+  if (__hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != inGroup) return false;
   __hip_atomic_store(mine, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups) return false;
+  if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u != groups) return false;
   __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
@@ -37,10 +45,11 @@ __device__ __forceinline__ void mpDrain() {
   __syncthreads();
 }
 
-// The launch's last block publishes the call's number (a release after every
-// block's arrival) — the completion word a call on another stream waits for.
+// The launch's last block publishes the call's number (write-through, after
+// every block's arrival) — the completion word a call on another stream waits
+// for.
 __device__ __forceinline__ void mpPublish(const MpDone& d) {
-  if (d.seq != 0) __hip_atomic_store(d.done, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (d.seq != 0) __hip_atomic_store(d.done, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The Simple kernels' end, called by EVERY thread of every block as the

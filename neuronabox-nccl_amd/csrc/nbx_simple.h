@@ -293,8 +293,12 @@ __device__ __forceinline__ void simpleLoadCounters(const SimpleArgs& a, SimpleSh
 __device__ __forceinline__ void simpleStoreCounters(const SimpleArgs& a, SimpleShared& sh) {
   __syncthreads();
   const int n = a.nRanks;
+  // write-through (agent-scope atomic stores): the next call's kernel may run
+  // on another stream and start before this one's end-of-kernel write-back
+  // (nbx_order.h)
   for (int i = (int)threadIdx.x; i < 4 * n; i += kBlock)
-    a.counters[(uint64_t)i * a.gridMax + blockIdx.x] = sh.cnt[i / n][i % n];
+    __hip_atomic_store(&a.counters[(uint64_t)i * a.gridMax + blockIdx.x], sh.cnt[i / n][i % n], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <class Fn>

@@ -720,6 +720,7 @@ struct MpState {
   // completion word of the communicator's kernels (MpDone, nbx_ll_args.h):
   // [0, 8) done (last completed eager call), [64, 64 + 9 * 64) arrival counters
   char* orderMem = nullptr;
+  hipIpcMemHandle_t llHandle{}, l128Handle{}, stageHandle{}, sflagsHandle{};   // taken at allocation
   uint64_t callSeq = 0;             // eager calls numbered from 1
   uint64_t lastSeq = 0;             // number of the previous eager call that launched a kernel
   uint64_t curSeq = 0;              // number of the call being launched (0: captured)
@@ -830,13 +831,37 @@ long envLong(const char* name, long dflt) {
 // for its connection buffers too. NBX_SYNC_MEM=coarse selects plain hipMalloc
 // (A/B measurement only: coarse-grained memory shared between processes is
 // exactly what round 2's wrong results came from).
-hipError_t allocSyncMem(void** p, size_t bytes) {
+// A connection buffer every peer maps: uncached device memory (NBX_SYNC_MEM=
+// coarse: plain hipMalloc, for A/B only), its size rounded up to whole 2 MiB
+// pages so the buffer is an allocation of its own, and its IPC handle taken
+// at once. hipIpcGetMemHandle refused a small fresh allocation now and then
+// ('invalid argument': the second ncclCommSplit child of a 4-rank test, r3s;
+// round 2's churn run saw the same at communicator creation), so a refused
+// allocation is set aside — not freed, so the retry cannot get the same
+// address back — and a new one is tried, up to three times.
+hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle) {
   static const bool coarse = [] {
     const char* v = std::getenv("NBX_SYNC_MEM");
     return v && strcasecmp(v, "coarse") == 0;
   }();
-  if (coarse) return hipMalloc(p, bytes);
-  return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+  const size_t page = (size_t)2 << 20;
+  bytes = (bytes + page - 1) / page * page;
+  std::vector<void*> refused;
+  hipError_t e = hipSuccess;
+  for (int attempt = 0; attempt < 3; attempt++) {
+    *p = nullptr;
+    e = coarse ? hipMalloc(p, bytes) : hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) break;
+    e = hipIpcGetMemHandle(handle, *p);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    warn("hipIpcGetMemHandle refused a %zu-byte connection buffer (%s); allocating another", bytes,
+         hipGetErrorString(e));
+    refused.push_back(*p);
+    *p = nullptr;
+  }
+  for (void* q : refused) (void)hipFree(q);
+  return e;
 }
 
 ncclResult_t mpLL128SelfTest(ncclComm* c);
@@ -983,7 +1008,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     mp->llSlotLines = 2 * (mx / 8);
     mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
     const size_t llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
-    HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes));
+    HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes, &mp->llHandle));
     HIPCHECK(hipMemset(mp->ll, 0, llBytes));
   }
   // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
@@ -996,16 +1021,16 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
       mp->l128MaxBytes = mx;
       mp->l128SlotLines = l128SlotLinesFor(mx);
       mp->l128Bytes = 2 * (uint64_t)n * mp->l128SlotLines * nbx::kL128LineBytesHost;
-      HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes));
+      HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes, &mp->l128Handle));
       HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
     }
   }
   // Simple staging, flag words and counters
   const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
   mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
-  HIPCHECK(allocSyncMem((void**)&mp->stage, mp->stageBytes));
+  HIPCHECK(allocSyncMem((void**)&mp->stage, mp->stageBytes, &mp->stageHandle));
   HIPCHECK(hipMemset(mp->stage, 0, mp->stageBytes));
-  HIPCHECK(allocSyncMem((void**)&mp->sflags, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(allocSyncMem((void**)&mp->sflags, 4 * cells * sizeof(uint64_t), &mp->sflagsHandle));
   HIPCHECK(hipMemset(mp->sflags, 0, 4 * cells * sizeof(uint64_t)));
   HIPCHECK(hipMalloc((void**)&mp->scounters, 4 * cells * sizeof(uint64_t)));
   HIPCHECK(hipMemset(mp->scounters, 0, 4 * cells * sizeof(uint64_t)));
@@ -1024,10 +1049,10 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.simpleGrid = mp->simpleGrid;
   mine.nonce = std::random_device{}() * 0x100000001ull ^ (uint64_t)std::random_device{}() ^
                ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)mp;
-  HIPCHECK(hipIpcGetMemHandle(&mine.llHandle, mp->ll));
-  if (mp->l128) HIPCHECK(hipIpcGetMemHandle(&mine.l128Handle, mp->l128));
-  HIPCHECK(hipIpcGetMemHandle(&mine.stageHandle, mp->stage));
-  HIPCHECK(hipIpcGetMemHandle(&mine.sflagsHandle, mp->sflags));
+  mine.llHandle = mp->llHandle;
+  if (mp->l128) mine.l128Handle = mp->l128Handle;
+  mine.stageHandle = mp->stageHandle;
+  mine.sflagsHandle = mp->sflagsHandle;
   std::vector<MpInitInfo> all(n);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
   std::vector<uint64_t*> llTable(n), l128Table(n, nullptr), flagTable(n);
