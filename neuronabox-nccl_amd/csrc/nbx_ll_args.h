@@ -83,7 +83,7 @@ struct LLArgs {
   int32_t root;            // kLLReduce
   MpDone order;
   int32_t nSegs;           // kLLColl group launch: segments in seg[] (0: one message)
-  int32_t pad2;
+  uint32_t gridCap;        // the communicator's workgroup cap (ranks sharing a GPU split it), 0: none
   LLSeg seg[kLLMaxSegs];
 };
 

@@ -451,6 +451,7 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
   size_t grid = (a.nPacks + 255) / 256;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
+  if (a.gridCap != 0 && grid > a.gridCap) grid = a.gridCap;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
@@ -472,6 +473,7 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   size_t grid = (a.nLines + linesPerBlock - 1) / linesPerBlock;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
+  if (a.gridCap != 0 && grid > a.gridCap) grid = a.gridCap;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll128, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
@@ -506,6 +508,7 @@ ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op,
   size_t grid = (blockLines + linesPerBlock - 1) / linesPerBlock;
   if (grid < 1) grid = 1;
   if (grid > maxGrid) grid = maxGrid;
+  if (a.gridCap != 0 && grid > a.gridCap) grid = a.gridCap;
   void* args[] = {&a};
   hipError_t e = hipLaunchKernel(ks.ll128x2, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;

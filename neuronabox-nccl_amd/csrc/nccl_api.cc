@@ -713,6 +713,7 @@ struct MpState {
   int slots = 2;                    // NBX_SIMPLE_SLOTS
   int simpleGrid = 0;               // workgroups of a full-size Simple call (NBX_SIMPLE_MAX_GRID, CU-capped)
   int simplePrefetch = 1;           // NBX_SIMPLE_PREFETCH: next round's pushes before this round's fold
+  uint32_t llGridCap = 0, l128GridCap = 0;   // LL / LL128 workgroup caps: 4 / 1 per CU, split among ranks sharing a GPU
   // successive calls are ordered across streams, as NCCL serializes a
   // communicator's work: a call on another stream waits for the previous one
   hipStream_t lastStream = nullptr;
@@ -983,6 +984,10 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   {
     long g = envLong("NBX_SIMPLE_MAX_GRID", 128);
     g = std::min<long>(g, std::max(1, minCus / maxShare));
+    // the LL family's spinning grids too: every rank's grid stays co-resident
+    // when several ranks share one GPU (the env caps still apply on top)
+    mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);
+    mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
     mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
     long s = envLong("NBX_SIMPLE_SLICE_BYTES", 64 << 10);
     s = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(s, 1 << 20));
@@ -1188,6 +1193,7 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
                                        : nbx::kLLReduce;
   la.root = c.root;
   la.order = mpOrderArgs(mp);
+  la.gridCap = proto == kMpLL ? mp->llGridCap : mp->l128GridCap;
   // a group's calls as one launch (runMpLLGroup): their slots concatenated, in
   // units of 8-byte packs (LL) or 48-byte lines (LL128 one-shot)
   const uint64_t unit = proto == kMpLL ? 8 : (uint64_t)nbx::kL128DataBytesHost;

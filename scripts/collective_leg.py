@@ -336,11 +336,8 @@ def main():
     dev = int(os.environ.get("NBX_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
     os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "120")
-    if "NBX_BENCH_DEVICE" in os.environ:   # rehearsal: every rank on one GPU, keep LL/LL128 grids co-resident
-        # (the Simple grid needs no cap: the communicator splits a GPU's CUs
-        # among the ranks that share it)
-        os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
-        os.environ.setdefault("NBX_LL_MAX_GRID", "64")
+    # (rehearsals with every rank on one GPU need no grid caps: the communicator
+    # splits the GPU's CUs among the ranks that share it, for every protocol)
     for line in sys.stdin:
         parts = line.split()
         if not parts:

@@ -119,8 +119,6 @@ def main():
     seed = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
     os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "60")
-    os.environ.setdefault("NBX_LL128_MAX_GRID", "32")
-    os.environ.setdefault("NBX_LL_MAX_GRID", "64")
     ctx = mp.get_context("spawn")
     from __graft_entry__ import _load_package
     nbx = _load_package()   # the bootstrap root is a host thread of this process; no GPU use here
