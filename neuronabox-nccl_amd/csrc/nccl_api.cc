@@ -165,7 +165,8 @@ struct ncclComm {
   int freeHead = 0;
   std::shared_ptr<Clique> clique;  // nRanks > 1 (single process)
   MpState* mp = nullptr;           // nRanks > 1 (one process per rank)
-  std::thread initThread;          // non-blocking ncclCommInitRankConfig: mpInit in the background
+  MpState* lt = nullptr;           // clique rank: in-process LL / LL128 transport (cliqueInitTransport)
+  std::thread initThread;         // non-blocking ncclCommInitRankConfig: mpInit in the background
   int initAbort = 0;               // set by ncclCommAbort: the init thread's bootstrap waits end
 };
 
@@ -188,6 +189,7 @@ struct PendingColl {
 
 struct Clique {
   int n = 0;
+  bool ll = false;   // LL / LL128-sized calls run in-kernel (every rank has comm->lt)
   std::vector<ncclComm*> comms;
   std::vector<int> devs;
   std::vector<hipEvent_t> evEnter, evReduced, evDone;   // one per rank
@@ -434,6 +436,14 @@ ncclResult_t foldBlocksBatched(const std::vector<const PendingColl*>& colls, con
   return ncclSuccess;
 }
 
+// The in-process LL transport of a clique (defined with the multi-process code it shares).
+enum MpProto : int;
+MpProto cliqueProtoOf(Clique* c, const std::vector<PendingColl>& parts);
+bool cliqueInKernel(Clique* c, const std::vector<PendingColl>& parts);
+ncclResult_t cliqueRunLL(Clique* c, const std::vector<std::vector<PendingColl>>& rounds, size_t lo, size_t hi);
+ncclResult_t cliqueOrderBefore(Clique* c, int r, hipStream_t s);
+ncclResult_t cliqueOrderAfter(Clique* c, int r, hipStream_t s);
+
 // Run one collective across every rank of an in-process clique.
 ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   const int n = c->n;
@@ -444,9 +454,11 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   }
   const int eb = typeSize(p0.dt);
   NBX_TRACE("clique coll kind=%d n=%d count=%zu dt=%d op=%d", (int)p0.kind, n, p0.count, (int)p0.dt, p0.op.op);
-  // 1. enter: every rank's stream reaches the collective
+  // 1. enter: every rank's stream reaches the collective (after the previous
+  //    call of the rank when that ran on another stream)
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
+    NCCLCHECK(cliqueOrderBefore(c, r, parts[r].stream));
     HIPCHECK(hipEventRecord(c->evEnter[r], parts[r].stream));
   }
   for (int r = 0; r < n; r++) {
@@ -509,6 +521,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
     DevGuard g(c->devs[r]);
     for (int j = 0; j < n; j++)
       if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evDone[j], 0));
+    NCCLCHECK(cliqueOrderAfter(c, r, parts[r].stream));
   }
   return ncclSuccess;
 }
@@ -547,6 +560,7 @@ ncclResult_t runCliqueBatch(Clique* c, const std::vector<std::vector<PendingColl
   NBX_TRACE("clique batch of %zu collectives", hi - lo);
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
+    NCCLCHECK(cliqueOrderBefore(c, r, rounds[lo][r].stream));
     HIPCHECK(hipEventRecord(c->evEnter[r], rounds[lo][r].stream));
   }
   for (int r = 0; r < n; r++) {
@@ -569,6 +583,7 @@ ncclResult_t runCliqueBatch(Clique* c, const std::vector<std::vector<PendingColl
     DevGuard g(c->devs[r]);
     for (int j = 0; j < n; j++)
       if (j != r) HIPCHECK(hipStreamWaitEvent(rounds[lo][r].stream, c->evDone[j], 0));
+    NCCLCHECK(cliqueOrderAfter(c, r, rounds[lo][r].stream));
   }
   return ncclSuccess;
 }
@@ -588,10 +603,22 @@ ncclResult_t runCliqueRounds(Clique* c, const std::vector<std::vector<PendingCol
   while (i < rounds.size()) {
     size_t j = i;
     std::vector<Span> spans;
+    if (cliqueInKernel(c, rounds[i])) {   // a run of in-kernel collectives, independent of each other
+      collSpans(rounds[i], &spans);
+      for (j = i + 1; j < rounds.size() && cliqueInKernel(c, rounds[j]); j++) {
+        std::vector<Span> sj;
+        collSpans(rounds[j], &sj);
+        if (spansConflict(spans, sj)) break;
+        spans.insert(spans.end(), sj.begin(), sj.end());
+      }
+      NCCLCHECK(cliqueRunLL(c, rounds, i, j));
+      i = j;
+      continue;
+    }
     if (batchable(rounds[i])) {
       collSpans(rounds[i], &spans);
       for (j = i + 1; j < rounds.size() && j - i < kMaxCliqueBatch; j++) {
-        if (!batchable(rounds[j])) break;
+        if (!batchable(rounds[j]) || cliqueInKernel(c, rounds[j])) break;
         bool sameStreams = true;
         for (int r = 0; r < n; r++) sameStreams &= rounds[j][r].stream == rounds[i][r].stream;
         if (!sameStreams) break;
@@ -729,7 +756,16 @@ struct MpState {
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
   bool groupBatch = true;           // NBX_GROUP_BATCH=0: every grouped call its own kernel
   std::vector<hipEvent_t> groupEvents;   // fan-in / fan-out of a group launch over several streams
+  // clique ranks only: the previous call ran on the event-ordered fold path
+  // (runCliqueColl / runCliqueBatch) on extStream; it is complete once every
+  // rank's extDone event (the clique's evDone) is
+  hipStream_t extStream = nullptr;
+  std::vector<hipEvent_t> extDone;
 };
+
+// The LL-family transport of a communicator: its own (one process per rank)
+// or, for a rank of an in-process clique, the one cliqueInitTransport built.
+MpState* mpOf(const ncclComm* c) { return c->mp ? c->mp : c->lt; }
 
 // Exchanged before anything is allocated: where every rank runs.
 struct MpPreInfo {
@@ -792,7 +828,7 @@ int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
 // two-shot AllReduce / Reduce (reduce-scatter + gather hops) while a rank's
 // block fits half an LL128 slot; else Simple. ReduceScatter is one hop by
 // nature: one-shot up to the LL128 max.
-enum MpProto { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2, kMpLL128x2 = 3 };
+enum MpProto : int { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2, kMpLL128x2 = 3 };
 // Lines per (parity, source) slot: holds maxBytes one-shot, and each half (a
 // two-shot sub-slot) holds maxBytes / 2.
 uint64_t l128SlotLinesFor(uint64_t maxBytes) {
@@ -840,7 +876,7 @@ long envLong(const char* name, long dflt) {
 // round 2's churn run saw the same at communicator creation), so a refused
 // allocation is set aside — not freed, so the retry cannot get the same
 // address back — and a new one is tried, up to three times.
-hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle) {
+hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle /* nullptr: in-process only */) {
   static const bool coarse = [] {
     const char* v = std::getenv("NBX_SYNC_MEM");
     return v && strcasecmp(v, "coarse") == 0;
@@ -852,7 +888,7 @@ hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle) {
   for (int attempt = 0; attempt < 3; attempt++) {
     *p = nullptr;
     e = coarse ? hipMalloc(p, bytes) : hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
-    if (e != hipSuccess) break;
+    if (e != hipSuccess || handle == nullptr) break;
     e = hipIpcGetMemHandle(handle, *p);
     if (e == hipSuccess) break;
     (void)hipGetLastError();
@@ -870,7 +906,7 @@ ncclResult_t mpLL128SelfTest(ncclComm* c);
 // A device spin gave up (host error word set): name the wait, the peer, the
 // value it waited for and the last one it saw (nbx_diag.h), once per record.
 void mpReportDeviceError(ncclComm* c) {
-  MpState* mp = c->mp;
+  MpState* mp = mpOf(c);
   if (!mp || !mp->hostWords || mp->hostWords[1] == 0) return;
   const volatile uint64_t* d = (const volatile uint64_t*)((const volatile char*)mp->hostWords + nbx::kDiagByteOffset);
   static thread_local uint64_t lastReported[nbx::kDiagWords] = {};
@@ -948,13 +984,55 @@ ncclResult_t mpVerifyMappings(ncclComm* c, const std::vector<MpInitInfo>& all, c
   return ncclSuccess;
 }
 
+// One rank's LL-family state on the current device: completion word,
+// sequencing state, host abort / error words, and the LL and LL128 connection
+// buffers (IPC handles taken when `ipc`; a clique's buffers stay in-process).
+ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc) {
+  const char* t = std::getenv("NBX_TIMEOUT_SEC");
+  if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
+  mp->protoMask = protoFromEnv();
+  mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
+  mp->groupBatch = envLong("NBX_GROUP_BATCH", 1) != 0;
+  HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
+  HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
+  HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
+  HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
+  HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(mp->hostWords, 0, 64);
+  HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
+  // LL buffer: 2 parities x n sources x 2 lines per 8-byte pack
+  {
+    uint64_t mx = (uint64_t)envLong("NBX_LL_MAX_BYTES", 64 << 10);
+    mx = (mx + 15) & ~(uint64_t)15;
+    if (mx < 1024) mx = 1024;
+    mp->llMaxBytes = mx;
+    mp->llSlotLines = 2 * (mx / 8);
+    mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
+    const size_t llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
+    HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes, ipc ? &mp->llHandle : nullptr));
+    HIPCHECK(hipMemset(mp->ll, 0, llBytes));
+  }
+  // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
+  if (n <= nbx::kL128MaxRanksHost) {
+    uint64_t mx = (uint64_t)envLong("NBX_LL128_MAX_BYTES", 4 << 20);
+    mp->l128OneShotMax = (uint64_t)envLong("NBX_LL128_ONESHOT_MAX", 256 << 10);
+    if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
+    if (mx != 0) {
+      mx = (mx + 15) & ~(uint64_t)15;
+      mp->l128MaxBytes = mx;
+      mp->l128SlotLines = l128SlotLinesFor(mx);
+      mp->l128Bytes = 2 * (uint64_t)n * mp->l128SlotLines * nbx::kL128LineBytesHost;
+      HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes, ipc ? &mp->l128Handle : nullptr));
+      HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
+    }
+  }
+  return ncclSuccess;
+}
+
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   MpState* mp = new MpState();
   c->mp = mp;
   const int n = c->nRanks, me = c->rank;
-  const char* t = std::getenv("NBX_TIMEOUT_SEC");
-  if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
-  mp->protoMask = protoFromEnv();
   mp->ring = algoRingFromEnv();
   NCCLCHECK(nbx::bootstrapConnect(id, me, n, &mp->bs));
   // where every rank runs: decides LL128's self-test and the Simple grid
@@ -994,42 +1072,8 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
     mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
     mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
-    mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
-    mp->groupBatch = envLong("NBX_GROUP_BATCH", 1) != 0;
   }
-  HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
-  HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
-  HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
-  HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
-  HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  std::memset(mp->hostWords, 0, 64);
-  HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
-  // LL buffer: 2 parities x n sources x 2 lines per 8-byte pack
-  {
-    uint64_t mx = (uint64_t)envLong("NBX_LL_MAX_BYTES", 64 << 10);
-    mx = (mx + 15) & ~(uint64_t)15;
-    if (mx < 1024) mx = 1024;
-    mp->llMaxBytes = mx;
-    mp->llSlotLines = 2 * (mx / 8);
-    mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
-    const size_t llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
-    HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes, &mp->llHandle));
-    HIPCHECK(hipMemset(mp->ll, 0, llBytes));
-  }
-  // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
-  if (n <= nbx::kL128MaxRanksHost) {
-    uint64_t mx = (uint64_t)envLong("NBX_LL128_MAX_BYTES", 4 << 20);
-    mp->l128OneShotMax = (uint64_t)envLong("NBX_LL128_ONESHOT_MAX", 256 << 10);
-    if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
-    if (mx != 0) {
-      mx = (mx + 15) & ~(uint64_t)15;
-      mp->l128MaxBytes = mx;
-      mp->l128SlotLines = l128SlotLinesFor(mx);
-      mp->l128Bytes = 2 * (uint64_t)n * mp->l128SlotLines * nbx::kL128LineBytesHost;
-      HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes, &mp->l128Handle));
-      HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
-    }
-  }
+  NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true));
   // Simple staging, flag words and counters
   const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
   mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
@@ -1125,10 +1169,8 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   return ncclSuccess;
 }
 
-void mpFree(ncclComm* c) {
-  MpState* mp = c->mp;
-  if (!mp) return;
-  DevGuard g(c->device);
+void mpFreeState(MpState* mp, int device) {
+  DevGuard g(device);
   (void)hipDeviceSynchronize();
   for (void* p : mp->peerMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : {(void*)mp->peerStageDev, (void*)mp->peerSFlagsDev, (void*)mp->scounters, (void*)mp->sflags,
@@ -1139,14 +1181,20 @@ void mpFree(ncclComm* c) {
   for (hipEvent_t e : mp->groupEvents) (void)hipEventDestroy(e);
   nbx::bootstrapClose(mp->bs);
   delete mp;
+}
+
+void mpFree(ncclComm* c) {
+  if (c->mp) mpFreeState(c->mp, c->device);
+  if (c->lt) mpFreeState(c->lt, c->device);
   c->mp = nullptr;
+  c->lt = nullptr;
 }
 
 // The protocol of a call. It depends only on arguments every rank passes
 // identically (and on the init-time settings checked equal), so every rank
 // picks the same one.
 MpProto mpProtoOf(const ncclComm* comm, const MpCall& c) {
-  const MpState* mp = comm->mp;
+  const MpState* mp = mpOf(comm);
   const int n = comm->nRanks;
   const int eb = typeSize(c.dt);
   const uint64_t slotBytes = (uint64_t)c.count * (uint64_t)eb;   // RS: recvcount per block
@@ -1165,7 +1213,7 @@ nbx::MpDone mpOrderArgs(MpState* mp) {
 // LL / LL128 protocols: small and medium collectives in one kernel (nbx_ll.h).
 ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const MpCall* segs = nullptr,
                         int nSegs = 0) {
-  MpState* mp = comm->mp;
+  MpState* mp = mpOf(comm);
   const int n = comm->nRanks, me = comm->rank;
   const int eb = typeSize(c.dt);
   const uint64_t slotBytes = (uint64_t)c.count * (uint64_t)eb;
@@ -1299,13 +1347,15 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
 // The cross-stream order around one launch on `stream` (see above).
 template <class Launch>
 ncclResult_t runMpOrdered(ncclComm* comm, hipStream_t stream, Launch&& launch) {
-  MpState* mp = comm->mp;
+  MpState* mp = mpOf(comm);
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   HIPCHECK(hipStreamIsCapturing(stream, &cap));
   const bool order = cap == hipStreamCaptureStatusNone && mp->streamOrder;
   if (order && mp->lastSeq != 0 && mp->lastStream != stream)
     NCCLCHECK(nbx::launchMpWaitDone((const uint64_t*)mp->orderMem, mp->lastSeq, mp->hostWordsDev, mp->hostWordsDev + 1,
                                     (uint64_t)(mp->timeoutSec * 1.0e8), stream));
+  if (order && mp->extStream != nullptr && mp->extStream != stream)   // clique: after a fold-path call
+    for (hipEvent_t e : mp->extDone) HIPCHECK(hipStreamWaitEvent(stream, e, 0));
   mp->curSeq = order ? mp->callSeq + 1 : 0;
   mp->launched = false;
   NCCLCHECK(launch());
@@ -1313,6 +1363,7 @@ ncclResult_t runMpOrdered(ncclComm* comm, hipStream_t stream, Launch&& launch) {
     mp->callSeq++;
     mp->lastSeq = mp->callSeq;
     mp->lastStream = stream;
+    mp->extStream = nullptr;
   }
   return ncclSuccess;
 }
@@ -1331,7 +1382,7 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
 // streams too, the first waits for them before it and they wait for it after
 // (NCCL's fan-in / fan-out, enqueue.cc:964-995, 1135-1148).
 ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc, MpProto proto) {
-  MpState* mp = comm->mp;
+  MpState* mp = mpOf(comm);
   hipStream_t s0 = calls[0].stream;
   std::vector<hipStream_t> others;
   for (int k = 1; k < nc; k++)
@@ -1459,7 +1510,7 @@ thread_local std::vector<ncclComm*> t_groupMpComms;
 // (NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order).
 ncclResult_t runMpGroup(ncclComm* comm) {
   DevGuard g(comm->device);
-  MpState* mp = comm->mp;
+  MpState* mp = mpOf(comm);
   std::vector<MpCall> calls;
   calls.swap(mp->group);
   ncclResult_t r = ncclSuccess;
@@ -1510,6 +1561,124 @@ ncclResult_t flushMpGroups() {
     if (first == ncclSuccess) first = r;
   }
   return first;
+}
+
+// ---------------------------------------------------------------------------
+// In-process clique over the LL family. Every rank of a clique whose devices
+// are all distinct (NCCL's own rule for one communicator) gets the LL / LL128
+// connection buffers a multi-process rank has, with its peers' buffers reached
+// through plain device pointers — peer access is enabled by ncclCommInitAll,
+// so nothing is IPC-mapped and nothing is exchanged. LL- and LL128-sized calls
+// then run as ONE kernel per rank with the flow control inside it (nbx_ll.h),
+// ordered across streams by the completion word (nbx_order.h), instead of the
+// fold path's event exchange (2 markers and 2(n-1) waits per rank and call,
+// ~5 us of device time per marker). Simple-sized calls keep the fold path
+// (runCliqueColl): one kernel per rank that reads every rank's buffers in
+// place, bandwidth-bound rather than latency-bound.
+// NBX_CLIQUE_LL=1 forces the transport on for ranks sharing a GPU (each rank's
+// kernel waits for its peers', so their streams must then be distinct and on
+// distinct hardware queues, e.g. GPU_MAX_HW_QUEUES >= ranks + 2); 0 turns it
+// off. A call whose ranks share a stream takes the fold path either way.
+ncclResult_t cliqueInitTransport(Clique* cl) {
+  const int n = cl->n;
+  bool distinct = true;
+  for (int r = 0; r < n; r++)
+    for (int j = 0; j < r; j++) distinct &= cl->devs[r] != cl->devs[j];
+  const char* v = std::getenv("NBX_CLIQUE_LL");
+  if (!((v && *v) ? std::atoi(v) != 0 : distinct)) return ncclSuccess;
+  int minCus = 1 << 30, maxShare = 1;
+  for (int r = 0; r < n; r++) {
+    int cus = 0, share = 0;
+    HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cl->devs[r]));
+    minCus = std::min(minCus, cus);
+    for (int j = 0; j < n; j++) share += cl->devs[j] == cl->devs[r];
+    maxShare = std::max(maxShare, share);
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(cl->devs[r]);
+    MpState* mp = new MpState();
+    cl->comms[r]->lt = mp;
+    NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/false));
+    mp->multiGpu = distinct;
+    mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);   // co-resident, as mpInit
+    mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
+    mp->extDone = cl->evDone;
+  }
+  std::vector<uint64_t*> llTable(n), l128Table(n);
+  for (int r = 0; r < n; r++) {
+    llTable[r] = cl->comms[r]->lt->ll;
+    l128Table[r] = cl->comms[r]->lt->l128;
+  }
+  for (int r = 0; r < n; r++) {
+    DevGuard g(cl->devs[r]);
+    MpState* mp = cl->comms[r]->lt;
+    HIPCHECK(hipMalloc((void**)&mp->peerLLDev, n * sizeof(uint64_t*)));
+    HIPCHECK(hipMemcpy(mp->peerLLDev, llTable.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice));
+    if (mp->l128) {
+      HIPCHECK(hipMalloc((void**)&mp->peerL128Dev, n * sizeof(uint64_t*)));
+      HIPCHECK(hipMemcpy(mp->peerL128Dev, l128Table.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice));
+    }
+    HIPCHECK(hipDeviceSynchronize());   // zeroed and uploaded before any peer's first kernel
+  }
+  cl->ll = true;
+  info("clique of %d ranks: LL / LL128-sized calls run in-kernel (grid caps %u / %u)", n,
+       cl->comms[0]->lt->llGridCap, cl->comms[0]->lt->l128GridCap);
+  return ncclSuccess;
+}
+
+// The protocol a clique collective runs with on the in-process transport, or
+// kMpSimple for the fold path. Decided once for all ranks.
+MpProto cliqueProtoOf(Clique* c, const std::vector<PendingColl>& parts) {
+  if (!c->ll || parts[0].count == 0 || !sameCollective(parts)) return kMpSimple;
+  for (int r = 0; r < c->n; r++) {
+    if (c->comms[r] == nullptr || c->comms[r]->lt == nullptr) return kMpSimple;
+    for (int j = 0; j < r; j++)
+      if (parts[j].stream == parts[r].stream) return kMpSimple;   // one rank's kernel would queue behind another's
+  }
+  return mpProtoOf(c->comms[0], parts[0]);
+}
+
+bool cliqueInKernel(Clique* c, const std::vector<PendingColl>& parts) { return cliqueProtoOf(c, parts) != kMpSimple; }
+
+// Consecutive in-kernel collectives [lo, hi): every rank runs them as a group
+// (runMpGroup cuts the same batched launches on every rank).
+ncclResult_t cliqueRunLL(Clique* c, const std::vector<std::vector<PendingColl>>& rounds, size_t lo, size_t hi) {
+  for (int r = 0; r < c->n; r++) {
+    ncclComm* comm = c->comms[r];
+    comm->lt->group.clear();
+    for (size_t k = lo; k < hi; k++) comm->lt->group.push_back(rounds[k][r]);
+    NCCLCHECK(runMpGroup(comm));
+  }
+  return ncclSuccess;
+}
+
+// Around a fold-path call on rank r's stream s: like runMpOrdered, it first
+// waits for the communicator's previous call when that ran on another stream
+// (the completion word after an in-kernel call, every rank's evDone after a
+// fold-path call), and leaves the state the next call orders against.
+ncclResult_t cliqueOrderBefore(Clique* c, int r, hipStream_t s) {
+  MpState* mp = c->comms[r] ? c->comms[r]->lt : nullptr;
+  if (mp == nullptr || !mp->streamOrder) return ncclSuccess;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) return ncclSuccess;
+  if (mp->lastSeq != 0 && mp->lastStream != s)
+    NCCLCHECK(nbx::launchMpWaitDone((const uint64_t*)mp->orderMem, mp->lastSeq, mp->hostWordsDev, mp->hostWordsDev + 1,
+                                    (uint64_t)(mp->timeoutSec * 1.0e8), s));
+  if (mp->extStream != nullptr && mp->extStream != s)
+    for (hipEvent_t e : mp->extDone) HIPCHECK(hipStreamWaitEvent(s, e, 0));
+  return ncclSuccess;
+}
+
+ncclResult_t cliqueOrderAfter(Clique* c, int r, hipStream_t s) {
+  MpState* mp = c->comms[r] ? c->comms[r]->lt : nullptr;
+  if (mp == nullptr || !mp->streamOrder) return ncclSuccess;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(s, &cap));
+  if (cap != hipStreamCaptureStatusNone) return ncclSuccess;
+  mp->lastSeq = 0;   // complete once every evDone is: that is what a later call on another stream waits for
+  mp->extStream = s;
+  return ncclSuccess;
 }
 
 // ncclEnqueueCheck + taskAppend for the reducing collectives.
@@ -1843,6 +2012,15 @@ NBX_API(ncclResult_t, ncclCommInitAll, ncclComm_t* comms, int ndev, const int* d
     comms[r]->clique = clique;
   }
   clique->comms.assign(comms, comms + ndev);
+  if (cliqueInitTransport(clique.get()) != ncclSuccess) {   // every call keeps the fold path
+    warn("ncclCommInitAll : in-process LL transport unavailable; every call uses the fold path");
+    for (int r = 0; r < ndev; r++)
+      if (comms[r]->lt) {
+        mpFreeState(comms[r]->lt, devs[r]);
+        comms[r]->lt = nullptr;
+      }
+    clique->ll = false;
+  }
   {
     std::lock_guard<std::mutex> g(g_pendMu);
     g_cliques.push_back(clique);
@@ -1893,7 +2071,7 @@ NBX_API(ncclResult_t, ncclCommAbort, ncclComm_t comm) {
     __atomic_store_n(&comm->initAbort, 1, __ATOMIC_RELAXED);
     comm->initThread.join();
   }
-  if (comm->mp && comm->mp->hostWords) comm->mp->hostWords[0] = 1;   // ends every spinning barrier
+  if (MpState* mp = mpOf(comm); mp && mp->hostWords) mp->hostWords[0] = 1;   // ends every spinning barrier
   return commFree(comm);
 }
 
@@ -1920,7 +2098,8 @@ NBX_API(ncclResult_t, ncclCommGetAsyncError, ncclComm_t comm, ncclResult_t* asyn
   NCCLCHECK(commCheck(comm, "ncclGetAsyncError"));
   if (asyncError == nullptr) return ncclInvalidArgument;
   *asyncError = (ncclResult_t)comm->asyncError.load();
-  if (*asyncError == ncclSuccess && comm->mp && comm->mp->hostWords && comm->mp->hostWords[1] != 0) {
+  const MpState* mp = mpOf(comm);
+  if (*asyncError == ncclSuccess && mp && mp->hostWords && mp->hostWords[1] != 0) {
     *asyncError = ncclRemoteError;   // a peer barrier timed out or was aborted
     mpReportDeviceError(comm);
   }
@@ -2048,8 +2227,8 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
 NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
 
 NBX_EXPORT int nbxDebugCommProtoMask(ncclComm_t comm) {
-  if (comm == nullptr || comm->magic != kCommMagic || comm->mp == nullptr) return -1;
-  return comm->mp->protoMask;
+  if (comm == nullptr || comm->magic != kCommMagic || mpOf(comm) == nullptr) return -1;
+  return mpOf(comm)->protoMask;   // a clique rank: its in-process transport's
 }
 
 NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
