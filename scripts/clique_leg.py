@@ -12,6 +12,8 @@ Spawned by bench.py rank 0 before it touches the GPU, idle until told:
   child  -> parent  "RESULT <json>\\n"
 Inputs are small integers in fp32 (x_r[i] = (7 i + 13 r) mod 1024), so every
 fold order gives the exact sum and every rank's whole output is checked.
+Then 4 KiB / 64 KiB / 1 MiB AllReduces (the in-kernel LL / LL128 transport when
+the devices are distinct), each checked and timed per call.
 """
 from __future__ import annotations
 
@@ -26,6 +28,8 @@ if ROOT not in sys.path:
 
 COUNT = 256 << 20   # fp32 elements per rank: 1 GiB (config D)
 WARMUP, ITERS = 2, 5
+SMALL_BYTES, SMALL_ITERS = (4096, 65536, 1 << 20), 100   # then LL / LL128 latency, one thread driving every rank
+os.environ.setdefault("NBX_TIMEOUT_SEC", "30")   # before the library loads: a stuck wait ends the probe, not the bench
 
 
 def run(n: int, devs: list, count: int = COUNT) -> dict:
@@ -97,9 +101,57 @@ def run(n: int, devs: list, count: int = COUNT) -> dict:
             res["ok"] = False
             res["errors"].append(f"reduce_scatter rank {r}: {int((rs[r] != want).sum())} elements differ")
     res["reduce_scatter_ms"] = timed(reduce_scatter)
+    small_calls(nbx, torch, comms, xs, ys, exps, streams, sync, res)
     for c in comms:
         c.destroy()
     return res
+
+
+def small_calls(nbx, torch, comms, xs, ys, exps, streams, sync, res):
+    """LL / LL128-sized AllReduces (in-kernel when the clique's devices are
+    distinct, cliqueInitTransport): each size checked exactly against a -1
+    sentinel, then timed; the first device error ends the probe (a stuck wait
+    gives up after NBX_TIMEOUT_SEC, set low for this child)."""
+    import ctypes
+    lib = nbx.load_library()
+    lib.nbxDebugCommProtoMask.argtypes = [ctypes.c_void_p]
+    lib.nbxDebugCommProtoMask.restype = ctypes.c_int
+    n = len(comms)
+    res["small_in_kernel"] = all(lib.nbxDebugCommProtoMask(c.handle) >= 0 for c in comms)
+    us = {}
+    for nbytes in SMALL_BYTES:
+        cnt = nbytes // 4
+
+        def ar():
+            nbx.group_start()
+            for r in range(n):
+                comms[r].all_reduce(xs[r].data_ptr(), ys[r].data_ptr(), cnt, 7, 0, streams[r].cuda_stream)
+            nbx.group_end()
+
+        for r in range(n):
+            with torch.cuda.device(ys[r].device):
+                ys[r][:cnt].fill_(-1.0)
+        sync()
+        ar()
+        sync()
+        if any(c.async_error() != 0 for c in comms):
+            res["ok"] = False
+            res["errors"].append(f"small allreduce {nbytes} B: device wait gave up")
+            break
+        wrong = [r for r in range(n) if not torch.equal(ys[r][:cnt], exps[r][:cnt])]
+        if wrong:
+            res["ok"] = False
+            res["errors"].append(f"small allreduce {nbytes} B: ranks {wrong} differ")
+            break
+        for _ in range(10):
+            ar()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(SMALL_ITERS):
+            ar()
+        sync()
+        us[str(nbytes)] = round((time.perf_counter() - t0) * 1e6 / SMALL_ITERS, 2)
+    res["allreduce_small_us_per_call"] = us
 
 
 def main():
