@@ -80,11 +80,20 @@ def _dist_init():
     if torch.cuda.is_available():
         torch.cuda.set_device(dev)
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = os.environ.get("NBX_BENCH_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-        dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                device_id=torch.device("cuda", dev) if backend == "nccl" else None)
+        init_process_group(backend, rank, world, dev)
     return world, rank, dev
+
+
+def init_process_group(backend: str, rank: int, world: int, dev: int):
+    """The bench's process group (tests/test_bench_rccl_gpu.py runs this with
+    backend "nccl" at one rank, so the RCCL path is exercised before the
+    driver's multi-GPU run)."""
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                            device_id=torch.device("cuda", dev) if backend == "nccl" else None)
 
 
 def _barrier(world):
@@ -94,11 +103,12 @@ def _barrier(world):
 
 
 def max_over_ranks(value: float, world: int) -> float:
-    """Max of a host float over ranks (the contract's max-over-ranks timing)."""
-    if world == 1:
+    """Max of a host float over ranks (the contract's max-over-ranks timing);
+    through the process group whenever one exists (also at one rank)."""
+    import torch.distributed as dist
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return value
     import torch
-    import torch.distributed as dist
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

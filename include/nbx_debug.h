@@ -49,6 +49,17 @@ int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint
  * NBX_LL128_SELFTEST_FAIL=1 makes that self-test report a failure (test hook). */
 int nbxDebugCommProtoMask(ncclComm_t comm);
 
+/* The transport settings a communicator runs with (after NCCL_BUFFSIZE /
+ * NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE / NCCL_MAX_NCHANNELS /
+ * NCCL_MIN_NCHANNELS and the NBX_* overrides are applied at creation):
+ * out[0] LL max bytes, [1] LL128 max bytes, [2] Simple slice bytes, [3] Simple
+ * slots, [4] Simple grid, [5] LL grid cap, [6] LL128 grid cap, [7] group
+ * batching, [8] connection buffers re-exported at creation because a peer's
+ * IPC mapping of them showed other memory (verified before first use). Writes
+ * min(nOut, 9) values and returns that count; -1 for a bad handle or a
+ * communicator without a multi-rank transport. */
+int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut);
+
 /* Stream ceilings in the caller's process (SURVEY §8(d) "a measured stream
  * ceiling"): kind 0 reads nSrcs == 8 buffers of `bytes` each with the hot
  * kernel's loads and tile (16-B nontemporal, 8 x 4 packs per lane, one
@@ -97,6 +108,13 @@ int nbxDebugSetDynMinTiles(int tilesPerWorkgroup);
  * (which: 0 = big-tile reduce's tile counters, 1 = realigning kernel's class
  * counters); keyed by stream handle (nbx_reduce.cc). -1 bad device. */
 int nbxDebugDynStreamSlots(int device, int which);
+
+/* Holds `stream` with a one-wave kernel until nbxDebugReleaseStream(hold) or
+ * timeoutMs pass, so a test can queue work behind it deterministically
+ * (instead of racing a sleep against the host). Returns the hold (>= 0), -1
+ * no free hold (16 at once) or bad timeout, -2 HIP error. Test hook. */
+int nbxDebugHoldStream(ncclStream_t stream, int timeoutMs);
+int nbxDebugReleaseStream(int hold);
 
 #ifdef __cplusplus
 }

@@ -47,8 +47,12 @@ __device__ __forceinline__ void mpDrain() {
 
 // The launch's last block publishes the call's number (write-through, after
 // every block's arrival) — the completion word a call on another stream waits
-// for.
+// for. Its own stores before this point (the arrival counters' resets, and in
+// llEnd the peers' done words and the LLState advance) are drained first: a
+// relaxed store to another address may otherwise become visible after the
+// completion word, and the next call's kernel would read the old state.
 __device__ __forceinline__ void mpPublish(const MpDone& d) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (d.seq != 0) __hip_atomic_store(d.done, d.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

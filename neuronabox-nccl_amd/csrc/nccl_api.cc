@@ -23,6 +23,7 @@
 // LL128 protocols for small / medium messages (nbx_ll.h).
 #include <hip/hip_runtime_api.h>
 
+#include <array>
 #include <atomic>
 #include <exception>
 #include <cstdarg>
@@ -168,6 +169,15 @@ struct ncclComm {
   MpState* lt = nullptr;           // clique rank: in-process LL / LL128 transport (cliqueInitTransport)
   std::thread initThread;         // non-blocking ncclCommInitRankConfig: mpInit in the background
   int initAbort = 0;               // set by ncclCommAbort: the init thread's bootstrap waits end
+  // pinned, device-mapped words every device wait of this rank polls: [0]
+  // abort, [1] error, diag record at byte 16 (nbx_diag.h). Owned here, not by
+  // the transport state, so ncclCommAbort can end a wait of a background
+  // initialisation (the LL128 self-test's kernels) before it joins that thread.
+  int* hostWords = nullptr;
+  int* hostWordsDev = nullptr;
+  ~ncclComm() {
+    if (hostWords) (void)hipHostFree(hostWords);
+  }
 };
 
 namespace {
@@ -706,7 +716,7 @@ using MpCall = PendingColl;
 
 struct MpState {
   nbx::Bootstrap* bs = nullptr;
-  int* hostWords = nullptr;            // pinned: [0] abort, [1] error, diag record at byte 16
+  int* hostWords = nullptr;            // the communicator's (ncclComm::hostWords), not owned
   int* hostWordsDev = nullptr;
   double timeoutSec = 300.0;
   std::vector<void*> peerMaps;         // every IPC mapping this communicator opened (closed at destroy)
@@ -732,6 +742,8 @@ struct MpState {
   // words [4][n][grid] (uncached, IPC-mapped by every peer), counters [4][n][grid]
   char* stage = nullptr;
   uint64_t stageBytes = 0;
+  uint64_t llBytes = 0, sflagsBytes = 0;   // used bytes of the LL buffer and the Simple flag words
+  int ipcRepairs = 0;               // connection buffers re-exported at init because a mapping was wrong (mpConnect)
   uint64_t* sflags = nullptr;
   uint64_t* scounters = nullptr;
   char** peerStageDev = nullptr;
@@ -781,7 +793,7 @@ struct MpInitInfo {
   hipIpcMemHandle_t l128Handle;
   hipIpcMemHandle_t stageHandle;
   hipIpcMemHandle_t sflagsHandle;
-  uint64_t nonce;          // this communicator's mapping self-check pattern (mpVerifyMappings)
+  uint64_t nonce;          // this communicator's mapping self-check pattern (mpConnect)
   // settings every rank must share: every rank must pick the same protocol,
   // grid and staging layout for the same call
   uint64_t llMaxBytes;
@@ -792,6 +804,7 @@ struct MpInitInfo {
   int32_t ring;            // NCCL_ALGO=Ring
   int32_t slots;
   int32_t simpleGrid;
+  int32_t groupBatch;      // NBX_GROUP_BATCH: one launch per run of grouped calls, or one per call
 };
 
 // NCCL_PROTO (tuning.cc:254-259, parseList): a comma-separated list of the
@@ -862,20 +875,53 @@ long envLong(const char* name, long dflt) {
   return (v && *v) ? std::atol(v) : dflt;
 }
 
+// The reference's own tuning knobs on this path, read at communicator
+// creation like NCCL reads them (init.cc:523-541 computeBuffSizes,
+// connect.cc:314-315, tuning.cc:12), each mapped onto the setting that plays
+// its role here; the NBX_* variable of that setting, when set, wins:
+//   NCCL_BUFFSIZE       Simple connection buffer per (peer, channel): the
+//                       Simple staging per (peer, workgroup, region) is
+//                       slots x slice, so slice = NCCL_BUFFSIZE / slots
+//                       (NBX_SIMPLE_SLICE_BYTES);
+//   NCCL_LL_BUFFSIZE    LL buffer: half of every 8-byte line is flag, so LL
+//                       carries messages up to NCCL_LL_BUFFSIZE / 2 (NBX_LL_MAX_BYTES);
+//   NCCL_LL128_BUFFSIZE LL128 buffer: 48 payload bytes per 64-byte line, so
+//                       LL128 carries up to 3/4 of it (NBX_LL128_MAX_BYTES);
+//   NCCL_MAX_NCHANNELS / NCCL_MIN_NCHANNELS  a channel is a workgroup here:
+//                       the Simple grid (NBX_SIMPLE_MAX_GRID) and the LL /
+//                       LL128 grids are capped at the max, and the Simple grid
+//                       raised to the min (both within the co-residency cap).
+// Unset, the measured defaults stay (64 KiB slices, 64 KiB LL, 4 MiB LL128,
+// 128 Simple workgroups). NCCL_NTHREADS has no counterpart: every
+// kernel is compiled for 256-thread workgroups (a warning says it is ignored).
+long ncclEnvMapped(const char* nbxName, const char* ncclName, long dflt, long num, long den) {
+  const char* v = std::getenv(nbxName);
+  if (v && *v) return std::atol(v);
+  const char* w = std::getenv(ncclName);
+  if (w && *w && std::atol(w) > 0) return std::atol(w) / den * num;
+  return dflt;
+}
+
 // Memory that other GPUs write and this GPU reads (LL lines, Simple staging
 // and flag words). Uncached (MTYPE UC) by default: a peer's stores over xGMI
 // land in HBM and no XCD L2 can hold a stale copy, which is what RCCL uses
 // for its connection buffers too. NBX_SYNC_MEM=coarse selects plain hipMalloc
-// (A/B measurement only: coarse-grained memory shared between processes is
-// exactly what round 2's wrong results came from).
-// A connection buffer every peer maps: uncached device memory (NBX_SYNC_MEM=
-// coarse: plain hipMalloc, for A/B only), its size rounded up to whole 2 MiB
-// pages so the buffer is an allocation of its own, and its IPC handle taken
-// at once. hipIpcGetMemHandle refused a small fresh allocation now and then
-// ('invalid argument': the second ncclCommSplit child of a 4-rank test, r3s;
-// round 2's churn run saw the same at communicator creation), so a refused
-// allocation is set aside — not freed, so the retry cannot get the same
-// address back — and a new one is tried, up to three times.
+// (A/B measurement only).
+// A connection buffer every peer maps: uncached device memory, its size
+// rounded up to whole 2 MiB pages so the buffer is an allocation of its own,
+// and its IPC handle taken at once.
+// The runtime rule behind the retry (scripts/probe_ipc_export.py: N processes
+// replaying communicator creation / destruction with the library's buffer
+// sizes, raw HIP, no libnbxccl; profiles/r4/probe_ipc_export_r4.jsonl):
+// hipIpcGetMemHandle refuses ('invalid argument') a new allocation placed at a
+// virtual address where an earlier allocation of the same process was
+// exported and then freed — 0-7 of 4,800 exports per run, every refusal at
+// such an address, the same pointer refused again on retry, a fresh
+// allocation (the refused one still held, so at another address) accepted
+// every time. So a refused allocation is held aside while the next one is
+// made (at most 4 tries), then freed. The same runtime condition also makes
+// a successful export name the wrong memory now and then (mpConnect, which
+// verifies every mapping and re-exports what is wrong).
 hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle /* nullptr: in-process only */) {
   static const bool coarse = [] {
     const char* v = std::getenv("NBX_SYNC_MEM");
@@ -885,15 +931,15 @@ hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle /* nul
   bytes = (bytes + page - 1) / page * page;
   std::vector<void*> refused;
   hipError_t e = hipSuccess;
-  for (int attempt = 0; attempt < 3; attempt++) {
+  for (int attempt = 0; attempt < 4; attempt++) {
     *p = nullptr;
     e = coarse ? hipMalloc(p, bytes) : hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
     if (e != hipSuccess || handle == nullptr) break;
     e = hipIpcGetMemHandle(handle, *p);
     if (e == hipSuccess) break;
     (void)hipGetLastError();
-    warn("hipIpcGetMemHandle refused a %zu-byte connection buffer (%s); allocating another", bytes,
-         hipGetErrorString(e));
+    info("hipIpcGetMemHandle refused a %zu-byte connection buffer at %p (%s): a reused exported address; "
+         "allocating another", bytes, *p, hipGetErrorString(e));
     refused.push_back(*p);
     *p = nullptr;
   }
@@ -936,58 +982,19 @@ void checkWord(uint64_t nonce, int from, int at, uint64_t out[2]) {
   out[1] = ~nonce ^ (0xc2b2ae3d27d4eb4full * (uint64_t)(at + 1));
 }
 
-// Every peer mapping is checked once, before first use, with this
-// communicator's random nonces: each rank stores a word through its mapping
-// of every peer's staging (slot = its rank) and its own word at slot n; after
-// a bootstrap barrier each rank checks the words peers stored into its own
-// staging and reads every peer's own word through its mapping. A mapping that
-// reaches other pages than the peer's allocation (the round-2 failure mode)
-// makes ncclCommInitRank fail loudly instead of a collective going silently
-// wrong. The words live in the AG region's last bytes, which a call rewrites
-// before reading.
-ncclResult_t mpVerifyMappings(ncclComm* c, const std::vector<MpInitInfo>& all, const std::vector<char*>& stages) {
-  MpState* mp = c->mp;
-  const int n = c->nRanks, me = c->rank;
-  const uint64_t base = mp->stageBytes - 16ull * (uint64_t)(n + 1);
-  uint64_t w[2];
-  for (int j = 0; j < n; j++) {
-    if (j == me) continue;
-    checkWord(all[me].nonce, me, j, w);
-    HIPCHECK(hipMemcpy(stages[j] + base + 16ull * (uint64_t)me, w, 16, hipMemcpyHostToDevice));
-  }
-  checkWord(all[me].nonce, me, n, w);
-  HIPCHECK(hipMemcpy(mp->stage + base + 16ull * (uint64_t)n, w, 16, hipMemcpyHostToDevice));
-  HIPCHECK(hipDeviceSynchronize());
-  int32_t bad = 0, dummy = 0;
-  std::vector<int32_t> gathered(n);
-  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), gathered.data()));
-  std::vector<uint64_t> mine(2 * (size_t)(n + 1));
-  HIPCHECK(hipMemcpy(mine.data(), mp->stage + base, 16ull * (uint64_t)(n + 1), hipMemcpyDeviceToHost));
-  for (int j = 0; j < n; j++) {
-    if (j == me) continue;
-    checkWord(all[j].nonce, j, me, w);
-    if (mine[2 * j] != w[0] || mine[2 * j + 1] != w[1]) {
-      warn("ncclCommInitRank : rank %d's store through its mapping of rank %d's staging did not land", j, me);
-      bad = 1;
-    }
-    uint64_t got[2];
-    HIPCHECK(hipMemcpy(got, stages[j] + base + 16ull * (uint64_t)n, 16, hipMemcpyDeviceToHost));
-    checkWord(all[j].nonce, j, n, w);
-    if (got[0] != w[0] || got[1] != w[1]) {
-      warn("ncclCommInitRank : rank %d's mapping of rank %d's staging reads other bytes", me, j);
-      bad = 1;
-    }
-  }
-  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &bad, sizeof(bad), gathered.data()));
-  for (int32_t b : gathered)
-    if (b) return ncclSystemError;
-  return ncclSuccess;
-}
+// Every connection buffer carries a check region after its used bytes:
+// 16 bytes per writer rank plus the owner's own word (mpConnect).
+uint64_t connCheckOff(uint64_t used) { return (used + 15) & ~(uint64_t)15; }
+uint64_t connAllocBytes(uint64_t used, int n) { return connCheckOff(used) + 16ull * (uint64_t)(n + 1); }
+
+// The connection buffers a multi-process rank exports (LL lines, LL128 lines,
+// Simple staging, Simple flag words).
+enum { kConnLL, kConnL128, kConnStage, kConnFlags, kNumConn };
 
 // One rank's LL-family state on the current device: completion word,
 // sequencing state, host abort / error words, and the LL and LL128 connection
 // buffers (IPC handles taken when `ipc`; a clique's buffers stay in-process).
-ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc) {
+ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
   const char* t = std::getenv("NBX_TIMEOUT_SEC");
   if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
   mp->protoMask = protoFromEnv();
@@ -997,24 +1004,25 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc) {
   HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
   HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
-  HIPCHECK(hipHostMalloc((void**)&mp->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent));
-  std::memset(mp->hostWords, 0, 64);
-  HIPCHECK(hipHostGetDevicePointer((void**)&mp->hostWordsDev, mp->hostWords, 0));
+  if (comm->hostWords == nullptr) return ncclInternalError;
+  mp->hostWords = comm->hostWords;
+  mp->hostWordsDev = comm->hostWordsDev;
   // LL buffer: 2 parities x n sources x 2 lines per 8-byte pack
   {
-    uint64_t mx = (uint64_t)envLong("NBX_LL_MAX_BYTES", 64 << 10);
+    uint64_t mx = (uint64_t)ncclEnvMapped("NBX_LL_MAX_BYTES", "NCCL_LL_BUFFSIZE", 64 << 10, 1, 2);
     mx = (mx + 15) & ~(uint64_t)15;
     if (mx < 1024) mx = 1024;
     mp->llMaxBytes = mx;
     mp->llSlotLines = 2 * (mx / 8);
     mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
-    const size_t llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
-    HIPCHECK(allocSyncMem((void**)&mp->ll, llBytes, ipc ? &mp->llHandle : nullptr));
-    HIPCHECK(hipMemset(mp->ll, 0, llBytes));
+    mp->llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
+    const uint64_t llAlloc = connAllocBytes(mp->llBytes, n);
+    HIPCHECK(allocSyncMem((void**)&mp->ll, llAlloc, ipc ? &mp->llHandle : nullptr));
+    HIPCHECK(hipMemset(mp->ll, 0, llAlloc));
   }
   // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
   if (n <= nbx::kL128MaxRanksHost) {
-    uint64_t mx = (uint64_t)envLong("NBX_LL128_MAX_BYTES", 4 << 20);
+    uint64_t mx = (uint64_t)ncclEnvMapped("NBX_LL128_MAX_BYTES", "NCCL_LL128_BUFFSIZE", 4 << 20, 3, 4);
     mp->l128OneShotMax = (uint64_t)envLong("NBX_LL128_ONESHOT_MAX", 256 << 10);
     if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
     if (mx != 0) {
@@ -1022,10 +1030,176 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc) {
       mp->l128MaxBytes = mx;
       mp->l128SlotLines = l128SlotLinesFor(mx);
       mp->l128Bytes = 2 * (uint64_t)n * mp->l128SlotLines * nbx::kL128LineBytesHost;
-      HIPCHECK(allocSyncMem((void**)&mp->l128, mp->l128Bytes, ipc ? &mp->l128Handle : nullptr));
-      HIPCHECK(hipMemset(mp->l128, 0, mp->l128Bytes));
+      const uint64_t l128Alloc = connAllocBytes(mp->l128Bytes, n);
+      HIPCHECK(allocSyncMem((void**)&mp->l128, l128Alloc, ipc ? &mp->l128Handle : nullptr));
+      HIPCHECK(hipMemset(mp->l128, 0, l128Alloc));
     }
   }
+  return ncclSuccess;
+}
+
+// Opens every peer's connection buffers and checks every mapping before first
+// use, re-exporting any buffer whose mapping is wrong (the reference maps its
+// peers' buffers once at connection time, transport/p2p.cc:290-330 p2pMap).
+// Why the check is needed: scripts/probe_ipc_export.py (raw HIP, N processes
+// on one GPU replaying communicator creation / destruction with this
+// library's buffer sizes and memory kinds) found IPC mappings that do not
+// show the exported allocation — an importer reads zeros or ANOTHER rank's
+// buffer through it, and its stores never reach the owner — in 12-20 of
+// 4,800 imports per run (uncached, 2 MiB-rounded: the library's buffers), the
+// same wrong bytes seen by every importer of that handle (so it is the
+// export, not one importer's mapping, that is wrong), at owner addresses that
+// an earlier, freed allocation of the owner had been exported from. Round 2's
+// wrong results (peers reading stale bytes through a mapping of a freshly
+// allocated buffer, their stores lost) are the same failure.
+// Check, per buffer and round (each with a fresh per-communicator nonce):
+// every rank stores a 16-byte word through its mapping of every peer's buffer
+// (slot = its rank) and its own word into its own buffer (slot n), all in the
+// check region after the used bytes; after a bootstrap barrier every rank
+// checks the words its peers stored into its buffers and reads every peer's
+// own word through its mappings. A wrong (owner, buffer) seen by anyone —
+// agreed by an allgather — is re-exported: its owner allocates a new buffer
+// (the old one held until the end, so the new one lands elsewhere), every
+// peer closes the wrong mapping and opens the new handle, and the round
+// repeats (at most 4). Only then does ncclCommInitRank fail (ncclSystemError).
+// NBX_IPC_VERIFY_FAIL=<rank>:<buffer> (test hook) makes round 0 report that
+// rank's buffer (0 LL, 1 LL128, 2 staging, 3 flags) wrong.
+ncclResult_t mpConnect(ncclComm* c, const std::vector<MpInitInfo>& all) {
+  MpState* mp = c->mp;
+  const int n = c->nRanks, me = c->rank;
+  void** own[kNumConn] = {(void**)&mp->ll, (void**)&mp->l128, (void**)&mp->stage, (void**)&mp->sflags};
+  hipIpcMemHandle_t* ownHandle[kNumConn] = {&mp->llHandle, &mp->l128Handle, &mp->stageHandle, &mp->sflagsHandle};
+  const uint64_t used[kNumConn] = {mp->llBytes, mp->l128Bytes, mp->stageBytes, mp->sflagsBytes};
+  const bool present[kNumConn] = {true, mp->l128 != nullptr, true, true};   // the same on every rank (n <= 8)
+  auto handleOf = [](const MpInitInfo& i, int t) -> const hipIpcMemHandle_t& {
+    return t == kConnLL ? i.llHandle : t == kConnL128 ? i.l128Handle : t == kConnStage ? i.stageHandle : i.sflagsHandle;
+  };
+  std::vector<std::array<char*, kNumConn>> peer(n);
+  std::vector<hipIpcMemHandle_t> cur((size_t)n * kNumConn);   // the handle each mapping was opened from
+  for (int j = 0; j < n; j++)
+    for (int t = 0; t < kNumConn; t++) {
+      peer[j][t] = nullptr;
+      cur[(size_t)j * kNumConn + t] = handleOf(all[j], t);
+    }
+  auto open = [&](int j, int t) -> ncclResult_t {
+    void* p = nullptr;
+    NCCLCHECK(mpOpenPeer(mp, cur[(size_t)j * kNumConn + t], &p));
+    peer[j][t] = (char*)p;
+    return ncclSuccess;
+  };
+  for (int j = 0; j < n; j++)
+    for (int t = 0; t < kNumConn; t++)
+      if (j != me && present[t]) NCCLCHECK(open(j, t));
+  int failRank = -1, failBuf = -1;
+  if (const char* v = std::getenv("NBX_IPC_VERIFY_FAIL"); v && *v) std::sscanf(v, "%d:%d", &failRank, &failBuf);
+  std::vector<void*> retired;
+  ncclResult_t res = ncclSuccess;
+  constexpr int kRounds = 4;
+  for (int round = 0;; round++) {
+    const uint64_t salt = 0x632be59bd9b4e019ull * (uint64_t)(round + 1);
+    auto nonceOf = [&](int j, int t) { return all[j].nonce ^ salt ^ (0xd6e8feb86659fd93ull * (uint64_t)(t + 1)); };
+    uint64_t w[2];
+    for (int t = 0; t < kNumConn; t++) {
+      if (!present[t]) continue;
+      const uint64_t off = connCheckOff(used[t]);
+      for (int j = 0; j < n; j++) {
+        if (j == me) continue;
+        checkWord(nonceOf(me, t), me, j, w);
+        HIPCHECK(hipMemcpy(peer[j][t] + off + 16ull * (uint64_t)me, w, 16, hipMemcpyHostToDevice));
+      }
+      checkWord(nonceOf(me, t), me, n, w);
+      HIPCHECK(hipMemcpy((char*)*own[t] + off + 16ull * (uint64_t)n, w, 16, hipMemcpyHostToDevice));
+    }
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<uint8_t> bad((size_t)n * kNumConn, 0), allBad((size_t)n * n * kNumConn);
+    int32_t dummy = 0;
+    std::vector<int32_t> gathered(n);
+    NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), gathered.data()));   // every word stored
+    std::vector<uint64_t> mine(2 * (size_t)(n + 1));
+    for (int t = 0; t < kNumConn; t++) {
+      if (!present[t]) continue;
+      const uint64_t off = connCheckOff(used[t]);
+      HIPCHECK(hipMemcpy(mine.data(), (char*)*own[t] + off, 16ull * (uint64_t)(n + 1), hipMemcpyDeviceToHost));
+      for (int j = 0; j < n; j++) {
+        if (j == me) continue;
+        checkWord(nonceOf(j, t), j, me, w);
+        if (mine[2 * j] != w[0] || mine[2 * j + 1] != w[1]) {
+          info("comm %p rank %d: rank %d's store through its mapping of my buffer %d did not land (round %d)",
+               (void*)c, me, j, t, round);
+          bad[(size_t)me * kNumConn + t] = 1;
+        }
+        uint64_t got[2];
+        HIPCHECK(hipMemcpy(got, peer[j][t] + off + 16ull * (uint64_t)n, 16, hipMemcpyDeviceToHost));
+        checkWord(nonceOf(j, t), j, n, w);
+        if (got[0] != w[0] || got[1] != w[1]) {
+          info("comm %p rank %d: my mapping of rank %d's buffer %d shows other bytes (round %d)", (void*)c, me, j, t,
+               round);
+          bad[(size_t)j * kNumConn + t] = 1;
+        }
+      }
+    }
+    if (round == 0 && failRank == me && failBuf >= 0 && failBuf < kNumConn && present[failBuf])
+      bad[(size_t)me * kNumConn + failBuf] = 1;
+    NCCLCHECK(nbx::bootstrapAllGather(mp->bs, bad.data(), bad.size(), allBad.data()));
+    for (int q = 0; q < n; q++)
+      for (size_t i = 0; i < bad.size(); i++) bad[i] |= allBad[(size_t)q * bad.size() + i];
+    int nBad = 0;
+    for (uint8_t b : bad) nBad += b;
+    if (nBad == 0) break;
+    if (round + 1 == kRounds) {
+      warn("ncclCommInitRank : %d peer mapping(s) still wrong after %d re-exports; giving up", nBad, kRounds - 1);
+      res = ncclSystemError;
+      break;
+    }
+    mp->ipcRepairs += nBad;
+    // re-export: the owner of a wrong buffer allocates another (the old one held)
+    struct Fresh {
+      hipIpcMemHandle_t h[kNumConn];
+    } fresh{};
+    for (int t = 0; t < kNumConn; t++) {
+      if (!bad[(size_t)me * kNumConn + t]) continue;
+      retired.push_back(*own[t]);
+      *own[t] = nullptr;
+      const uint64_t bytes = connAllocBytes(used[t], n);
+      HIPCHECK(allocSyncMem(own[t], bytes, ownHandle[t]));
+      HIPCHECK(hipMemset(*own[t], 0, bytes));
+      fresh.h[t] = *ownHandle[t];
+      info("comm %p rank %d: buffer %d re-exported at %p (round %d)", (void*)c, me, t, *own[t], round);
+    }
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<Fresh> allFresh(n);
+    NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &fresh, sizeof(fresh), allFresh.data()));
+    for (int j = 0; j < n; j++) {
+      if (j == me) continue;
+      for (int t = 0; t < kNumConn; t++) {
+        if (!bad[(size_t)j * kNumConn + t]) continue;
+        auto it = std::find(mp->peerMaps.begin(), mp->peerMaps.end(), (void*)peer[j][t]);
+        if (it != mp->peerMaps.end()) mp->peerMaps.erase(it);
+        HIPCHECK(hipIpcCloseMemHandle(peer[j][t]));
+        cur[(size_t)j * kNumConn + t] = allFresh[j].h[t];
+        NCCLCHECK(open(j, t));
+      }
+    }
+  }
+  for (void* q : retired) (void)hipFree(q);
+  NCCLCHECK(res);
+  // the device tables of peer buffers (own entry: own buffer)
+  std::vector<uint64_t*> llTable(n), l128Table(n, nullptr), flagTable(n);
+  std::vector<char*> stageTable(n);
+  for (int j = 0; j < n; j++) {
+    llTable[j] = j == me ? mp->ll : (uint64_t*)peer[j][kConnLL];
+    l128Table[j] = j == me ? mp->l128 : (uint64_t*)peer[j][kConnL128];
+    stageTable[j] = j == me ? mp->stage : peer[j][kConnStage];
+    flagTable[j] = j == me ? mp->sflags : (uint64_t*)peer[j][kConnFlags];
+  }
+  auto upload = [](void** dev, const void* host, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(dev, bytes);
+    return e != hipSuccess ? e : hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice);
+  };
+  HIPCHECK(upload((void**)&mp->peerLLDev, llTable.data(), n * sizeof(uint64_t*)));
+  if (mp->l128) HIPCHECK(upload((void**)&mp->peerL128Dev, l128Table.data(), n * sizeof(uint64_t*)));
+  HIPCHECK(upload((void**)&mp->peerStageDev, stageTable.data(), n * sizeof(char*)));
+  HIPCHECK(upload((void**)&mp->peerSFlagsDev, flagTable.data(), n * sizeof(uint64_t*)));
   return ncclSuccess;
 }
 
@@ -1060,27 +1234,40 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   // Simple grid: one workgroup per CU, all co-resident (workgroup g of a rank
   // waits on workgroup g of its peers); ranks sharing a GPU split its CUs.
   {
-    long g = envLong("NBX_SIMPLE_MAX_GRID", 128);
+    const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0), minCh = envLong("NCCL_MIN_NCHANNELS", 0);
+    long g = envLong("NBX_SIMPLE_MAX_GRID", 0);
+    if (g <= 0) {
+      g = 128;
+      if (maxCh > 0) g = std::min(g, maxCh);
+      if (minCh > 0) g = std::max(g, minCh);
+    }
     g = std::min<long>(g, std::max(1, minCus / maxShare));
     // the LL family's spinning grids too: every rank's grid stays co-resident
     // when several ranks share one GPU (the env caps still apply on top)
     mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);
     mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
+    if (maxCh > 0) {
+      mp->llGridCap = std::min<uint32_t>(mp->llGridCap, (uint32_t)maxCh);
+      mp->l128GridCap = std::min<uint32_t>(mp->l128GridCap, (uint32_t)maxCh);
+    }
     mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
-    long s = envLong("NBX_SIMPLE_SLICE_BYTES", 64 << 10);
+    mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
+    long s = ncclEnvMapped("NBX_SIMPLE_SLICE_BYTES", "NCCL_BUFFSIZE", 64 << 10, 1, mp->slots);
     s = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(s, 1 << 20));
     mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
-    mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
+    if (const char* nt = std::getenv("NCCL_NTHREADS"); nt && *nt && std::atol(nt) != 256)
+      info("NCCL_NTHREADS=%s ignored: every kernel of this library runs 256-thread workgroups", nt);
     mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
   }
-  NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true));
+  NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true, c));
   // Simple staging, flag words and counters
   const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
   mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
-  HIPCHECK(allocSyncMem((void**)&mp->stage, mp->stageBytes, &mp->stageHandle));
-  HIPCHECK(hipMemset(mp->stage, 0, mp->stageBytes));
-  HIPCHECK(allocSyncMem((void**)&mp->sflags, 4 * cells * sizeof(uint64_t), &mp->sflagsHandle));
-  HIPCHECK(hipMemset(mp->sflags, 0, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(allocSyncMem((void**)&mp->stage, connAllocBytes(mp->stageBytes, n), &mp->stageHandle));
+  HIPCHECK(hipMemset(mp->stage, 0, connAllocBytes(mp->stageBytes, n)));
+  mp->sflagsBytes = 4 * cells * sizeof(uint64_t);
+  HIPCHECK(allocSyncMem((void**)&mp->sflags, connAllocBytes(mp->sflagsBytes, n), &mp->sflagsHandle));
+  HIPCHECK(hipMemset(mp->sflags, 0, connAllocBytes(mp->sflagsBytes, n)));
   HIPCHECK(hipMalloc((void**)&mp->scounters, 4 * cells * sizeof(uint64_t)));
   HIPCHECK(hipMemset(mp->scounters, 0, 4 * cells * sizeof(uint64_t)));
   HIPCHECK(hipDeviceSynchronize());   // zeroed before any peer can map and write them
@@ -1096,6 +1283,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.ring = mp->ring;
   mine.slots = mp->slots;
   mine.simpleGrid = mp->simpleGrid;
+  mine.groupBatch = mp->groupBatch;
   mine.nonce = std::random_device{}() * 0x100000001ull ^ (uint64_t)std::random_device{}() ^
                ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)mp;
   mine.llHandle = mp->llHandle;
@@ -1104,8 +1292,6 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.sflagsHandle = mp->sflagsHandle;
   std::vector<MpInitInfo> all(n);
   NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
-  std::vector<uint64_t*> llTable(n), l128Table(n, nullptr), flagTable(n);
-  std::vector<char*> stageTable(n);
   for (int j = 0; j < n; j++) {
     // every rank must pick the same protocol, grid and layout for the same call
     if (all[j].llMaxBytes != mp->llMaxBytes || all[j].l128MaxBytes != mp->l128MaxBytes ||
@@ -1120,48 +1306,27 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
            "across ranks");
       return ncclInvalidUsage;
     }
-    if (j == me) {
-      llTable[j] = mp->ll;
-      l128Table[j] = mp->l128;
-      stageTable[j] = mp->stage;
-      flagTable[j] = mp->sflags;
-      continue;
+    // a group's calls become one launch or one per call, and every launch
+    // advances the device-resident sequence by one: ranks must cut alike
+    if (all[j].groupBatch != mine.groupBatch) {
+      warn("ncclCommInitRank : NBX_GROUP_BATCH differs across ranks");
+      return ncclInvalidUsage;
     }
-    if (all[j].device != c->device) {
-      int can = 0;
-      HIPCHECK(hipDeviceCanAccessPeer(&can, c->device, all[j].device));
-      if (!can) {
-        // every data path here is a kernel store to peer memory; there is no
-        // host-staged transport, so fail cleanly instead of faulting later
-        warn("ncclCommInitRank : device %d cannot access peer device %d (no P2P)", c->device, all[j].device);
-        return ncclSystemError;
-      }
-      hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
-      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
-      (void)hipGetLastError();
+    if (j == me || all[j].device == c->device) continue;
+    int can = 0;
+    HIPCHECK(hipDeviceCanAccessPeer(&can, c->device, all[j].device));
+    if (!can) {
+      // every data path here is a kernel store to peer memory; there is no
+      // host-staged transport, so fail cleanly instead of faulting later
+      warn("ncclCommInitRank : device %d cannot access peer device %d (no P2P)", c->device, all[j].device);
+      return ncclSystemError;
     }
-    void* p = nullptr;
-    NCCLCHECK(mpOpenPeer(mp, all[j].llHandle, &p));
-    llTable[j] = (uint64_t*)p;
-    if (mp->l128) {
-      NCCLCHECK(mpOpenPeer(mp, all[j].l128Handle, &p));
-      l128Table[j] = (uint64_t*)p;
-    }
-    NCCLCHECK(mpOpenPeer(mp, all[j].stageHandle, &p));
-    stageTable[j] = (char*)p;
-    NCCLCHECK(mpOpenPeer(mp, all[j].sflagsHandle, &p));
-    flagTable[j] = (uint64_t*)p;
+    hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+    (void)hipGetLastError();
   }
-  auto upload = [](void** dev, const void* host, size_t bytes) -> hipError_t {
-    hipError_t e = hipMalloc(dev, bytes);
-    return e != hipSuccess ? e : hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice);
-  };
-  HIPCHECK(upload((void**)&mp->peerLLDev, llTable.data(), n * sizeof(uint64_t*)));
-  if (mp->l128) HIPCHECK(upload((void**)&mp->peerL128Dev, l128Table.data(), n * sizeof(uint64_t*)));
-  HIPCHECK(upload((void**)&mp->peerStageDev, stageTable.data(), n * sizeof(char*)));
-  HIPCHECK(upload((void**)&mp->peerSFlagsDev, flagTable.data(), n * sizeof(uint64_t*)));
-  // every mapping checked, and everyone has mapped everyone, before the first collective
-  NCCLCHECK(mpVerifyMappings(c, all, stageTable));
+  // every peer buffer mapped and checked before the first collective
+  NCCLCHECK(mpConnect(c, all));
   NCCLCHECK(mpLL128SelfTest(c));
   info("comm %p rank %d nranks %d device %d: multi-process communicator ready (Simple grid %d, slice %llu B, "
        "staging %llu MiB)", (void*)c, me, n, c->device, mp->simpleGrid, (unsigned long long)mp->sliceBytes,
@@ -1177,7 +1342,6 @@ void mpFreeState(MpState* mp, int device) {
                   (void*)mp->stage, (void*)mp->peerL128Dev, (void*)mp->l128, (void*)mp->peerLLDev, (void*)mp->ll,
                   (void*)mp->llState, (void*)mp->orderMem})
     if (p) (void)hipFree(p);
-  if (mp->hostWords) (void)hipHostFree(mp->hostWords);
   for (hipEvent_t e : mp->groupEvents) (void)hipEventDestroy(e);
   nbx::bootstrapClose(mp->bs);
   delete mp;
@@ -1504,10 +1668,23 @@ thread_local std::vector<ncclComm*> t_groupMpComms;
 // one-shot) with the same kind, datatype, op and root, whose slots fit one
 // slot of that protocol together (at most kLLMaxSegs), run as one launch
 // (runMpLLGroup) — a decision made from arguments every rank passes
-// identically, so every rank cuts the same runs. As in NCCL's aggregated
-// launch, collectives inside one group are independent operations: a call
-// must not read what an earlier call of the same group writes
-// (NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order).
+// identically, so every rank cuts the same runs. A run also ends before a call
+// that reads or writes what an earlier call of the run writes (or writes what
+// it reads): the segments of one launch run concurrently, so such a chain
+// (AllReduce a->b, then b->c) must stay separate launches, in order. That cut
+// looks at this rank's own buffers; the ranks of an SPMD program alias alike
+// and cut alike. Ranks that alias differently cut different runs, and their
+// kernels then wait for lines that never come and time out with the wait
+// named (nbx_diag.h) — an error, never a silently wrong result.
+// (NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order.)
+void mpCallSpans(const MpCall& c, int n, int rank, std::vector<Span>* out) {
+  const size_t eb = (size_t)typeSize(c.dt);
+  const size_t sendBytes = (c.kind == kReduceScatter ? c.count * (size_t)n : c.count) * eb;
+  out->push_back({(uintptr_t)c.send, (uintptr_t)c.send + sendBytes, false});
+  if (c.recv != nullptr && (c.kind != kReduce || rank == c.root))
+    out->push_back({(uintptr_t)c.recv, (uintptr_t)c.recv + c.count * eb, true});
+}
+
 ncclResult_t runMpGroup(ncclComm* comm) {
   DevGuard g(comm->device);
   MpState* mp = mpOf(comm);
@@ -1531,9 +1708,15 @@ ncclResult_t runMpGroup(ncclComm* comm) {
       const MpProto p = calls[i].count > 0 ? mpProtoOf(comm, calls[i]) : kMpSimple;
       if (mp->groupBatch && (p == kMpLL || p == kMpLL128)) {
         uint64_t used = unitsOf(calls[i], p);
+        std::vector<Span> spans, sj;
+        mpCallSpans(calls[i], comm->nRanks, comm->rank, &spans);
         while (j < calls.size() && j - i < (size_t)nbx::kLLMaxSegs && calls[j].count > 0 &&
                sameOp(calls[i], calls[j]) && mpProtoOf(comm, calls[j]) == p &&
                used + unitsOf(calls[j], p) <= capOf(p)) {
+          sj.clear();
+          mpCallSpans(calls[j], comm->nRanks, comm->rank, &sj);
+          if (spansConflict(spans, sj)) break;
+          spans.insert(spans.end(), sj.begin(), sj.end());
           used += unitsOf(calls[j], p);
           j++;
         }
@@ -1598,10 +1781,14 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
     DevGuard g(cl->devs[r]);
     MpState* mp = new MpState();
     cl->comms[r]->lt = mp;
-    NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/false));
+    NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/false, cl->comms[r]));
     mp->multiGpu = distinct;
     mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);   // co-resident, as mpInit
     mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
+    if (const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0); maxCh > 0) {   // a channel is a workgroup (mpInit)
+      mp->llGridCap = std::min<uint32_t>(mp->llGridCap, (uint32_t)maxCh);
+      mp->l128GridCap = std::min<uint32_t>(mp->l128GridCap, (uint32_t)maxCh);
+    }
     mp->extDone = cl->evDone;
   }
   std::vector<uint64_t*> llTable(n), l128Table(n);
@@ -1731,6 +1918,16 @@ ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclCo
   c->device = dev;
   const char* cp = std::getenv("NCCL_CHECK_POINTERS");
   c->checkPointers = cp && std::atoi(cp) != 0;
+  if (nRanks > 1) {
+    DevGuard g(dev);
+    if (hipHostMalloc((void**)&c->hostWords, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->hostWordsDev, c->hostWords, 0) != hipSuccess) {
+      warn("cannot allocate the communicator's pinned wait words");
+      delete c;
+      return ncclUnhandledCudaError;
+    }
+    std::memset(c->hostWords, 0, 64);
+  }
   if (config && config->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = config->blocking;
   if (const char* be = std::getenv("NCCL_COMM_BLOCKING")) {   // init.cc:1444-1446: the env overrides the config
     char* end = nullptr;
@@ -2067,11 +2264,14 @@ NBX_API(ncclResult_t, ncclCommDestroy, ncclComm_t comm) {
 NBX_API(ncclResult_t, ncclCommAbort, ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
   NCCLCHECK(commCheck(comm, "ncclCommAbort"));
-  if (comm->initThread.joinable()) {   // a pending initialisation: its bootstrap waits end at the flag
+  // every device wait of this rank polls the abort word; set first, so a
+  // pending initialisation's kernels (the LL128 self-test) end too, not only
+  // its bootstrap waits (the flag), before the init thread is joined
+  if (comm->hostWords) __atomic_store_n(&comm->hostWords[0], 1, __ATOMIC_SEQ_CST);
+  if (comm->initThread.joinable()) {
     __atomic_store_n(&comm->initAbort, 1, __ATOMIC_RELAXED);
     comm->initThread.join();
   }
-  if (MpState* mp = mpOf(comm); mp && mp->hostWords) mp->hostWords[0] = 1;   // ends every spinning barrier
   return commFree(comm);
 }
 
@@ -2098,8 +2298,11 @@ NBX_API(ncclResult_t, ncclCommGetAsyncError, ncclComm_t comm, ncclResult_t* asyn
   NCCLCHECK(commCheck(comm, "ncclGetAsyncError"));
   if (asyncError == nullptr) return ncclInvalidArgument;
   *asyncError = (ncclResult_t)comm->asyncError.load();
+  // the transport pointer only after a finished initialisation: the init
+  // thread's final asyncError store orders its assignment before this load
+  if (*asyncError != ncclSuccess) return ncclSuccess;
   const MpState* mp = mpOf(comm);
-  if (*asyncError == ncclSuccess && mp && mp->hostWords && mp->hostWords[1] != 0) {
+  if (mp && mp->hostWords && mp->hostWords[1] != 0) {
     *asyncError = ncclRemoteError;   // a peer barrier timed out or was aborted
     mpReportDeviceError(comm);
   }
@@ -2229,6 +2432,26 @@ NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString
 NBX_EXPORT int nbxDebugCommProtoMask(ncclComm_t comm) {
   if (comm == nullptr || comm->magic != kCommMagic || mpOf(comm) == nullptr) return -1;
   return mpOf(comm)->protoMask;   // a clique rank: its in-process transport's
+}
+
+// The transport settings a communicator runs with (its own, or a clique
+// rank's in-process transport's): out[0] LL max bytes, [1] LL128 max bytes,
+// [2] Simple slice bytes, [3] Simple slots, [4] Simple grid, [5] LL grid cap,
+// [6] LL128 grid cap, [7] group batching, [8] connection buffers re-exported
+// at creation because a peer's mapping of them was wrong (mpConnect). Returns
+// how many were written, -1
+// for a bad handle or a communicator without that transport.
+NBX_EXPORT int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut) {
+  if (comm == nullptr || comm->magic != kCommMagic || out == nullptr) return -1;
+  if (comm->asyncError.load() != ncclSuccess) return -1;
+  const MpState* mp = mpOf(comm);
+  if (mp == nullptr) return -1;
+  const int64_t v[9] = {(int64_t)mp->llMaxBytes, (int64_t)mp->l128MaxBytes, (int64_t)mp->sliceBytes, mp->slots,
+                        mp->simpleGrid,          (int64_t)mp->llGridCap,    (int64_t)mp->l128GridCap, mp->groupBatch,
+                        mp->ipcRepairs};
+  int k = 0;
+  for (; k < nOut && k < 9; k++) out[k] = v[k];
+  return k;
 }
 
 NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,

@@ -62,11 +62,16 @@ def _child(uid_bytes, rank, n, q, grouped=False):
                 first_out = live[0][4]   # ("allreduce", 7, 0)
                 dep = torch.zeros_like(first_out)
                 comm.all_reduce(first_out.data_ptr(), dep.data_ptr(), COUNT, 7, 0, st.cuda_stream)
+                # right behind it, same kind / type / op / size: a run candidate
+                # that reads what the call before it writes (must be cut there)
+                dep2 = torch.zeros_like(first_out)
+                comm.all_reduce(dep.data_ptr(), dep2.data_ptr(), COUNT, 7, 0, st.cuda_stream)
                 nbx.group_end()
                 st.synchronize()
                 for kind, dtype, op, tx, ty in live:
                     out[(it, kind, dtype, op)] = ty.cpu().numpy().copy()
                 out[(it, "dep")] = dep.cpu().numpy().copy()
+                out[(it, "dep2")] = dep2.cpu().numpy().copy()
         for it in range(0 if grouped else 2):   # twice: the second round hits the IPC mapping cache
             for kind, dtype, op in CASES:
                 x = _inputs(oracle, kind, dtype, n, rank)
@@ -145,9 +150,14 @@ def test_multiprocess_grouped_collectives(nbx, oracle, n, proto, monkeypatch):
         if hi > lo:
             order = [(r + 1 + k) % n for k in range(n)]
             exp[lo:hi] = oracle.reduce_multi([first[j][lo:hi] for j in order], 7, 0, 0, n_pre_op_srcs=n)[0]
+    exp2 = np.empty(COUNT, dtype=np.float32)
+    for r, (lo, hi) in enumerate(blocks):
+        if hi > lo:
+            exp2[lo:hi] = oracle.reduce_multi([exp[lo:hi]] * n, 7, 0, 0, n_pre_op_srcs=n)[0]
     for it in range(2):
         for r in range(n):
             assert np.array_equal(res[r][(it, "dep")].view(np.float32), exp), (it, r)
+            assert np.array_equal(res[r][(it, "dep2")].view(np.float32), exp2), (it, r)
 
 
 def _run_ranks(nbx, n, target, *extra):
@@ -1161,3 +1171,187 @@ def test_multiprocess_comm_split(nbx, monkeypatch):
             members = [p for p in range(n) if p != 1]
             assert res[r]["child2"] == (len(members), members.index(r)), (r, res[r])
             assert res[r]["sum2"] == float(sum(p + 1 for p in members)), (r, res[r])
+
+
+def _child_knobs(uid_bytes, rank, n, q, env):
+    """The reference's own knobs (NCCL_BUFFSIZE, NCCL_LL_BUFFSIZE,
+    NCCL_LL128_BUFFSIZE, NCCL_MAX/MIN_NCHANNELS) as the communicator applies
+    them, then exact AllReduces at an LL, an LL128 and a Simple size. `env`:
+    per-rank environment set before ncclCommInitRank (values may differ by
+    rank: {name: [value of rank 0, value of rank 1, ...]})."""
+    try:
+        import ctypes
+        import os
+
+        import torch
+        from tests.conftest import load_package
+        for k, vals in env.items():
+            os.environ[k] = vals[rank]
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        uid = nbx.ncclUniqueId.from_buffer_copy(uid_bytes)
+        try:
+            comm = nbx.Communicator.init_rank(n, uid, rank)
+        except nbx.NcclError as e:
+            q.put((rank, "ok", {"init": int(e.code)}))
+            return
+        vals = (ctypes.c_int64 * 9)()
+        got = lib.nbxDebugCommSettings(comm.handle, vals, 9)
+        out = {"init": 0, "settings": list(vals)[:got]}
+        st = torch.cuda.current_stream().cuda_stream
+        for cnt in (2048, 131072, 1 << 20):   # 8 KiB (LL), 512 KiB (LL128), 4 MiB (Simple) of fp32
+            x = torch.remainder(torch.arange(cnt, device="cuda", dtype=torch.float32) * 3 + rank, 101)
+            y = torch.full((cnt,), -1.0, device="cuda")
+            comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, st)
+            torch.cuda.synchronize()
+            want = sum(torch.remainder(torch.arange(cnt, device="cuda", dtype=torch.float32) * 3 + r, 101)
+                       for r in range(n))
+            out[cnt] = bool(torch.equal(y, want))
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_reference_knobs(nbx, monkeypatch):
+    """NCCL_BUFFSIZE 256 KiB -> 128 KiB Simple slices (2 slots), NCCL_LL_BUFFSIZE
+    64 KiB -> LL up to 32 KiB, NCCL_LL128_BUFFSIZE 1 MiB -> LL128 up to 768 KiB,
+    NCCL_MAX_NCHANNELS 16 -> every grid capped at 16 workgroups; results exact."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    for k in ("NBX_SIMPLE_SLICE_BYTES", "NBX_SIMPLE_MAX_GRID", "NBX_LL_MAX_BYTES", "NBX_LL128_MAX_BYTES"):
+        monkeypatch.delenv(k, raising=False)
+    n = 2
+    env = {"NCCL_BUFFSIZE": ["262144"] * n, "NCCL_LL_BUFFSIZE": ["65536"] * n,
+           "NCCL_LL128_BUFFSIZE": ["1048576"] * n, "NCCL_MAX_NCHANNELS": ["16"] * n}
+    res = _run_ranks(nbx, n, _child_knobs, env)
+    for r in range(n):
+        assert res[r]["init"] == 0
+        ll, l128, slice_, slots, grid, llcap, l128cap, batch = res[r]["settings"][:8]
+        assert (ll, l128, slice_, slots, grid) == (32768, 786432, 131072, 2, 16), res[r]["settings"]
+        assert llcap <= 16 and l128cap <= 16 and batch == 1
+        assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
+
+
+def test_multiprocess_nbx_override_wins(nbx, monkeypatch):
+    """An NBX_* setting set next to the reference knob it maps wins."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    n = 2
+    env = {"NCCL_BUFFSIZE": ["262144"] * n, "NBX_SIMPLE_SLICE_BYTES": ["16384"] * n,
+           "NCCL_MIN_NCHANNELS": ["8"] * n, "NCCL_MAX_NCHANNELS": ["4"] * n, "NBX_SIMPLE_MAX_GRID": ["6"] * n}
+    res = _run_ranks(nbx, n, _child_knobs, env)
+    for r in range(n):
+        assert res[r]["settings"][2] == 16384 and res[r]["settings"][4] == 6, res[r]["settings"]
+        assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
+
+
+@pytest.mark.parametrize("name,vals", [("NCCL_BUFFSIZE", ["262144", "131072"]), ("NBX_GROUP_BATCH", ["1", "0"]),
+                                       ("NCCL_LL_BUFFSIZE", ["65536", "32768"])])
+def test_multiprocess_settings_must_agree(nbx, monkeypatch, name, vals):
+    """Settings that decide a call's protocol, grid, staging layout or launch
+    cut must be equal on every rank: ncclCommInitRank fails with
+    ncclInvalidUsage on every rank instead of the ranks' kernels disagreeing."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    for k in ("NBX_SIMPLE_SLICE_BYTES", "NBX_LL_MAX_BYTES", "NBX_GROUP_BATCH"):
+        monkeypatch.delenv(k, raising=False)
+    res = _run_ranks(nbx, 2, _child_knobs, {name: vals})
+    for r in range(2):
+        assert res[r]["init"] == int(nbx.ncclResult.ncclInvalidUsage), (r, res[r])
+
+
+@pytest.mark.parametrize("buf", [0, 1, 2, 3])
+def test_multiprocess_ipc_mapping_repair(nbx, monkeypatch, buf):
+    """A connection buffer whose peers' mappings fail the creation-time check
+    is re-exported and re-mapped, and the communicator then works exactly
+    (NBX_IPC_VERIFY_FAIL: rank 1 reports buffer `buf` — LL, LL128, staging,
+    flags — wrong in the first check round)."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_IPC_VERIFY_FAIL", f"1:{buf}")
+    n = 3
+    res = _run_ranks(nbx, n, _child_knobs, {})
+    for r in range(n):
+        assert res[r]["init"] == 0
+        assert res[r]["settings"][8] == 1, res[r]["settings"]   # one buffer re-exported, seen by every rank
+        assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
+
+
+def _child_comm_churn(uid_list, rank, n, q):
+    """Communicators created and destroyed back to back (the pattern that
+    makes the runtime hand out wrong IPC mappings now and then,
+    scripts/probe_ipc_export.py): every one must come up with verified
+    mappings and run an LL, an LL128 and a Simple AllReduce exactly."""
+    try:
+        import ctypes
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {"repairs": 0, "exact": 0, "wrong": []}
+        keep = None
+        for i, ub in enumerate(uid_list):
+            comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(ub), rank)
+            vals = (ctypes.c_int64 * 9)()
+            assert lib.nbxDebugCommSettings(comm.handle, vals, 9) == 9
+            out["repairs"] += vals[8]
+            for cnt in (1000 + i, 70001 + 7 * i, (1 << 20) + 3 * i):   # LL, LL128, Simple
+                x = torch.remainder(torch.arange(cnt, device="cuda", dtype=torch.float32) * 3 + rank + i, 89)
+                y = torch.full((cnt,), -1.0, device="cuda")
+                comm.all_reduce(x.data_ptr(), y.data_ptr(), cnt, 7, 0, st)
+                torch.cuda.synchronize()
+                want = sum(torch.remainder(torch.arange(cnt, device="cuda", dtype=torch.float32) * 3 + r + i, 89)
+                           for r in range(n))
+                if torch.equal(y, want):
+                    out["exact"] += 1
+                else:
+                    out["wrong"].append((i, cnt))
+            # like ncclCommSplit: now and then the previous communicator outlives the next one's creation
+            if keep is not None:
+                keep.destroy()
+                keep = None
+            if i % 3 == 1:
+                keep = comm
+            else:
+                comm.destroy()
+        if keep is not None:
+            keep.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_comm_churn_verified_mappings(nbx, monkeypatch):
+    """40 communicators of 3 ranks in a row: every collective exact; the
+    creation-time check re-exports whatever mapping the runtime got wrong."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    n, k = 3, 40
+    uids = [bytes(nbx.get_unique_id()) for _ in range(k)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_child_comm_churn, args=(uids, r, n, q), daemon=True) for r in range(n)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=280)
+            assert status == "ok", f"rank {rank}:\n{payload}"
+            res[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+    for r in range(n):
+        assert res[r]["wrong"] == [] and res[r]["exact"] == 3 * k, (r, res[r])
+    print("re-exported connection buffers over", k, "communicators:", [res[r]["repairs"] for r in range(n)])

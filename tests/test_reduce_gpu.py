@@ -601,10 +601,16 @@ def test_batch_work_list_slots_and_graph_ownership(nbx, oracle, torch_gpu):
         host = fill(0)
         torch.cuda.synchronize()
         fb0 = lib.nbxDebugBatchListSlots(dev_id, 3)
-        with torch.cuda.stream(s):
-            torch.cuda._sleep(1_500_000_000)   # hold the stream (~0.6 s) so the calls below pile up, however slow the host
-            for _ in range(300):   # > 128 slots in flight: the rest fall back to kernel-argument tables
-                nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
+        # hold the stream until every call below is enqueued, so more than 128
+        # slots are in flight however fast or slow the host is
+        hold = lib.nbxDebugHoldStream(ctypes.c_void_p(s.cuda_stream), 60_000)
+        assert hold >= 0
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(300):   # > 128 slots in flight: the rest fall back to kernel-argument tables
+                    nbx.reduce_multi_batch(buckets, dtype, op, 0, False, s.cuda_stream)
+        finally:
+            assert lib.nbxDebugReleaseStream(hold) == 0
         s.synchronize()
         check(host)
         assert lib.nbxDebugBatchListSlots(dev_id, 3) > fb0   # the fallback ran, and came out right
