@@ -114,6 +114,22 @@ constexpr int kSimpleMaxGrid = 256;
 constexpr int kSimpleMaxRanks = 64;
 constexpr int kSimpleMinSliceBytes = 4096;   // a call uses at most ceil(block / 4 KiB) workgroups
 
+// A group of Simple-sized collectives as ONE launch (nccl_api.cc runMpGroup;
+// NCCL packs a group's collectives into one kernel's work, enqueue.cc:67-91):
+// every block b of the launch is the concatenation of block b of each
+// message, cut into the launch's slices; segment s owns the virtual slices
+// [sliceOff, next sliceOff) of every block. Every segment has the launch's
+// kind, datatype, op (and root). nSegs = 0: the single message of send / recv
+// / total / blockElts.
+constexpr int kSimpleMaxSegs = 16;
+struct SimpleSeg {
+  const void* send;
+  void* recv;
+  uint64_t total;       // elements of the message (ReduceScatter: recvcount * n)
+  uint64_t blockElts;   // its block (as SimpleArgs::blockElts)
+  uint64_t sliceOff;    // its first virtual slice of every block
+};
+
 struct SimpleArgs {
   const void* send;
   void* recv;                  // nullptr on Reduce non-roots
@@ -137,8 +153,9 @@ struct SimpleArgs {
   int32_t slots;               // staging slots per (region, source, workgroup), >= 2
   int32_t gridMax;
   int32_t prefetch;            // direct: push round k+1 before folding round k (a rank-local choice)
-  int32_t pad;
+  int32_t nSegs;               // group launch: segments in seg[] (0: one message)
   MpDone order;
+  SimpleSeg seg[kSimpleMaxSegs];
 };
 
 }  // namespace nbx

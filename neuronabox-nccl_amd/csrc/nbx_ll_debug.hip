@@ -50,6 +50,19 @@ __global__ __launch_bounds__(64) void kL128TearReader(LLArgs a, uint32_t flag, u
 }
 
 }  // namespace
+
+// The Simple rig's call as ONE dispatch (kSimpleFused, fp32 sum only): every
+// rank's workgroups in one grid, so rocprofv3's PMC passes can count the
+// call's HBM bytes (nbxDebugSimpleRun, NBX_DEBUG_SIMPLE_FUSED=1).
+ncclResult_t launchSimpleFusedF32Sum(const SimpleArgs* argsDev, int n, unsigned grid, bool ring, hipStream_t stream) {
+  if (ring)
+    hipLaunchKernelGGL((kSimpleFused<FnSumF<TyF32>, true>), dim3((unsigned)n * grid), dim3(kBlock), 0, stream, argsDev,
+                       (int)grid);
+  else
+    hipLaunchKernelGGL((kSimpleFused<FnSumF<TyF32>, false>), dim3((unsigned)n * grid), dim3(kBlock), 0, stream,
+                       argsDev, (int)grid);
+  return hipGetLastError() == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
 }  // namespace nbx
 
 extern "C" __attribute__((visibility("default"))) int nbxDebugLL128TearTest(int delayUs, int tear,

@@ -127,16 +127,39 @@ __device__ __forceinline__ char* simpleStage(const SimpleArgs& a, int owner, int
   return a.peerStage[owner] + idx * a.stageSlice;
 }
 
-// Elements [*off, *off + *cnt) of block b that workgroup g moves in round k.
+// What workgroup g (of `grid`) moves of block b in round k: elements
+// [off, off + cnt) of the message whose send / recv buffers are given (a
+// group launch's segment, or the launch's one message), and that message's
+// block size (ReduceScatter's output offset).
+struct SimpleSpan {
+  const char* send;
+  char* recv;
+  uint64_t off, cnt, blockElts;
+};
 template <class E>
-__device__ __forceinline__ void simpleSlice(const SimpleArgs& a, int b, uint64_t k, uint64_t* off, uint64_t* cnt) {
-  uint64_t lo = (uint64_t)b * a.blockElts;
-  if (lo > a.total) lo = a.total;
-  const uint64_t hi = a.total - lo < a.blockElts ? a.total : lo + a.blockElts;
+__device__ __forceinline__ SimpleSpan simpleSlice(const SimpleArgs& a, int b, uint64_t k, int g, int grid) {
+  uint64_t v = k * (uint64_t)grid + (uint64_t)g;   // the launch's virtual slice of block b
+  SimpleSpan sp{(const char*)a.send, (char*)a.recv, 0, 0, a.blockElts};
+  uint64_t total = a.total;
+  if (a.nSegs > 0) {
+    int s = 0;
+    for (int q = 1; q < a.nSegs; q++)
+      if (v >= a.seg[q].sliceOff) s = q;
+    const SimpleSeg& sg = a.seg[s];
+    sp.send = (const char*)sg.send;
+    sp.recv = (char*)sg.recv;
+    sp.blockElts = sg.blockElts;
+    total = sg.total;
+    v -= sg.sliceOff;
+  }
+  uint64_t lo = (uint64_t)b * sp.blockElts;
+  if (lo > total) lo = total;
+  const uint64_t hi = total - lo < sp.blockElts ? total : lo + sp.blockElts;
   const uint64_t sliceE = a.sliceBytes / sizeof(E);
-  const uint64_t s0 = (k * gridDim.x + blockIdx.x) * sliceE;
-  *off = lo + s0;
-  *cnt = s0 >= hi - lo ? 0 : (hi - lo - s0 < sliceE ? hi - lo - s0 : sliceE);
+  const uint64_t s0 = v * sliceE;
+  sp.off = lo + s0;
+  sp.cnt = s0 >= hi - lo ? 0 : (hi - lo - s0 < sliceE ? hi - lo - s0 : sliceE);
+  return sp;
 }
 
 // Workgroup copy of nElts elements into up to two destinations (any alignment;
@@ -282,41 +305,42 @@ struct SimpleShared {
   int fail;
 };
 
-__device__ __forceinline__ void simpleLoadCounters(const SimpleArgs& a, SimpleShared& sh) {
+__device__ __forceinline__ void simpleLoadCounters(const SimpleArgs& a, SimpleShared& sh, int g) {
   const int n = a.nRanks;
   for (int i = (int)threadIdx.x; i < 4 * n; i += kBlock)
-    sh.cnt[i / n][i % n] = a.counters[(uint64_t)i * a.gridMax + blockIdx.x];
+    sh.cnt[i / n][i % n] = a.counters[(uint64_t)i * a.gridMax + g];
   if (threadIdx.x == 0) sh.fail = 0;
   __syncthreads();
 }
 
-__device__ __forceinline__ void simpleStoreCounters(const SimpleArgs& a, SimpleShared& sh) {
+__device__ __forceinline__ void simpleStoreCounters(const SimpleArgs& a, SimpleShared& sh, int g) {
   __syncthreads();
   const int n = a.nRanks;
   // write-through (agent-scope atomic stores): the next call's kernel may run
   // on another stream and start before this one's end-of-kernel write-back
   // (nbx_order.h)
   for (int i = (int)threadIdx.x; i < 4 * n; i += kBlock)
-    __hip_atomic_store(&a.counters[(uint64_t)i * a.gridMax + blockIdx.x], sh.cnt[i / n][i % n], __ATOMIC_RELAXED,
+    __hip_atomic_store(&a.counters[(uint64_t)i * a.gridMax + g], sh.cnt[i / n][i % n], __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The direct schedule as run by workgroup g of a `grid`-workgroup launch
+// (kSimpleColl: the launch's own block index; kSimpleCollFused: one launch
+// running every rank of a one-process rig, for the PMC passes).
 template <class Fn>
-__global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
+__device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, int g, int grid) {
   using E = typename Fn::Elt;
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
-  const int n = a.nRanks, me = a.rank, g = (int)blockIdx.x, gm = a.gridMax, tid = (int)threadIdx.x;
+  const int n = a.nRanks, me = a.rank, gm = a.gridMax, tid = (int)threadIdx.x;
   const uint64_t slots = (uint64_t)a.slots;
   __shared__ SimpleShared sh;
-  simpleLoadCounters(a, sh);
+  simpleLoadCounters(a, sh, g);
   uint64_t* const myFlags = a.peerFlags[me];
   const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce, rs = a.mode == kSimpleReduceScatter;
   const bool storeLocal = !red || me == a.root;        // B writes this rank's output block
   const bool gathers = ar || (red && me == a.root);    // C runs here
   const int first = ((red ? a.root : me) + 1) % n;      // fold order of block `me`
   auto pushTarget = [&](int p) { return p != me && (ar || (red && p == a.root)); };
-  const char* const send = (const char*)a.send;
-  char* const recv = (char*)a.recv;
 
   auto phaseA = [&](uint64_t k) -> bool {
     // ---- A: slice g of block j into rank j's RS region, slot rsSent[j] % slots
@@ -330,10 +354,9 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
-      uint64_t off, cnt;
-      simpleSlice<E>(a, j, k, &off, &cnt);
-      if (cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
-                             send + off * sizeof(E), false, cnt);
+      const SimpleSpan sp = simpleSlice<E>(a, j, k, g, grid);
+      if (sp.cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
+                                sp.send + sp.off * sizeof(E), false, sp.cnt);
     }
     simpleDrain();
     if (tid < n && tid != me) simplePost(simpleFlag(a.peerFlags[tid], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][tid]);
@@ -351,15 +374,15 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
           !simpleWait(simpleFlag(myFlags, kFlAgCredit, n, tid, gm, g), sent + 1 - slots, a, tid, kDiagSimpleAgCredit))
         sh.fail = 1;
     }
-    uint64_t off, cnt;
-    simpleSlice<E>(a, me, k, &off, &cnt);
+    const SimpleSpan sp = simpleSlice<E>(a, me, k, g, grid);
+    const uint64_t off = sp.off, cnt = sp.cnt;
     // the output holds the whole message, except ReduceScatter's: block `me` only
-    const uint64_t outOff = rs ? off - (uint64_t)me * a.blockElts : off;
+    const uint64_t outOff = rs ? off - (uint64_t)me * sp.blockElts : off;
     if (tid < n) {
       const int j = (first + tid) % n;
-      sh.src[tid] = j == me ? send + off * sizeof(E) : simpleStage(a, me, 0, sh.cnt[kCtRsRecv][j] % slots, j, g);
+      sh.src[tid] = j == me ? sp.send + off * sizeof(E) : simpleStage(a, me, 0, sh.cnt[kCtRsRecv][j] % slots, j, g);
       // destinations: [own output], then the push targets in the order me+1, ...
-      if (tid == 0 && storeLocal) sh.dst[0] = recv + outOff * sizeof(E);
+      if (tid == 0 && storeLocal) sh.dst[0] = sp.recv + outOff * sizeof(E);
       if (tid > 0) {
         const int p = (me + tid) % n;
         if (ar) sh.dst[tid] = simpleStage(a, p, 1, sh.cnt[kCtAgSent][p] % slots, me, g);
@@ -370,7 +393,8 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     if (sh.fail) return false;
     const int nDsts = ar ? n : 1;
     if (cnt) {
-      const bool aligned = simpleAligned(send + off * sizeof(E)) && (!storeLocal || simpleAligned(recv + outOff * sizeof(E)));
+      const bool aligned =
+          simpleAligned(sp.send + off * sizeof(E)) && (!storeLocal || simpleAligned(sp.recv + outOff * sizeof(E)));
       // destination 0 is the caller's output unless a Reduce non-root pushes to the root
       const uint64_t sysMask = storeLocal ? ~1ull : ~0ull;
       // every source but the own input (at fold position (me - first) mod n) is staging
@@ -395,10 +419,9 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
-      uint64_t o2, c2;
-      simpleSlice<E>(a, j, k, &o2, &c2);
-      if (c2) simpleCopy<E>(recv + o2 * sizeof(E), false, nullptr, false,
-                            simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, c2);
+      const SimpleSpan sp = simpleSlice<E>(a, j, k, g, grid);
+      if (sp.cnt) simpleCopy<E>(sp.recv + sp.off * sizeof(E), false, nullptr, false,
+                                simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, sp.cnt);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slots are read: they may be refilled
     __syncthreads();
@@ -421,8 +444,13 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
     if (!phaseB(k)) return;
     if (gathers && !phaseC(k)) return;
   }
-  simpleStoreCounters(a, sh);
+  simpleStoreCounters(a, sh, g);
   mpArrive(a.order);
+}
+
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
+  simpleCollBody<Fn>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Ring schedule through the right neighbour's staging. AllReduce /
@@ -431,18 +459,16 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
 // the ring (all_reduce.h:60-93). Reduce: the chain root+1 -> ... -> root over
 // the one block of the message (reduce.h:44-67).
 template <class Fn>
-__global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
+__device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int grid) {
   using E = typename Fn::Elt;
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
-  const int n = a.nRanks, me = a.rank, g = (int)blockIdx.x, gm = a.gridMax, tid = (int)threadIdx.x;
+  const int n = a.nRanks, me = a.rank, gm = a.gridMax, tid = (int)threadIdx.x;
   const int left = (me + n - 1) % n, right = (me + 1) % n;
   const uint64_t slots = (uint64_t)a.slots;
   __shared__ SimpleShared sh;
-  simpleLoadCounters(a, sh);
+  simpleLoadCounters(a, sh, g);
   uint64_t* const myFlags = a.peerFlags[me];
   const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
-  const char* const send = (const char*)a.send;
-  char* const recv = (char*)a.recv;
   // thread 0 waits for what a hop needs: the left neighbour's slice (recvFrom)
   // and free slots at the right neighbour (RS region: pushRs, AG region: pushAg)
   auto hopWait = [&](int recvRegion, bool pushRs, bool pushAg) {
@@ -479,21 +505,21 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
     if (red) {
       // chain position: 0 = root+1 (sends its raw input), n-1 = the root
       const int pos = (me - a.root - 1 + 2 * n) % n;
-      uint64_t off, cnt;
-      simpleSlice<E>(a, 0, k, &off, &cnt);
+      const SimpleSpan sp = simpleSlice<E>(a, 0, k, g, grid);
+      const uint64_t off = sp.off, cnt = sp.cnt;
       const bool push = pos < n - 1;
       if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
-      char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : recv + off * sizeof(E);
+      char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : sp.recv + off * sizeof(E);
       if (pos == 0) {
-        if (cnt) simpleCopy<E>(out, push, nullptr, false, send + off * sizeof(E), false, cnt);
+        if (cnt) simpleCopy<E>(out, push, nullptr, false, sp.send + off * sizeof(E), false, cnt);
       } else if (cnt) {
         if (tid == 0) {
-          sh.src[0] = send + off * sizeof(E);
+          sh.src[0] = sp.send + off * sizeof(E);
           sh.src[1] = simpleStage(a, me, 0, sh.cnt[kCtRsRecv][left] % slots, left, g);
           sh.dst[0] = out;
         }
         __syncthreads();
-        const bool aligned = simpleAligned(send + off * sizeof(E)) && simpleAligned(out);
+        const bool aligned = simpleAligned(sp.send + off * sizeof(E)) && simpleAligned(out);
         simpleFold<Fn>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned);
       }
       simpleDrain();
@@ -502,11 +528,10 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
     }
     // send step: the raw chunk me-1 into the right neighbour's RS region
     {
-      uint64_t off, cnt;
-      simpleSlice<E>(a, left, k, &off, &cnt);
+      const SimpleSpan sp = simpleSlice<E>(a, left, k, g, grid);
       if (!hopWait(-1, true, false)) return;
-      if (cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr, false,
-                             send + off * sizeof(E), false, cnt);
+      if (sp.cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr,
+                                false, sp.send + sp.off * sizeof(E), false, sp.cnt);
       simpleDrain();
       hopPost(-1, true, false);
     }
@@ -514,14 +539,14 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
     for (int st = 0; st < n - 1; st++) {
       const int c = (me + 2 * n - 2 - st) % n;
       const bool last = st == n - 2;
-      uint64_t off, cnt;
-      simpleSlice<E>(a, c, k, &off, &cnt);
+      const SimpleSpan sp = simpleSlice<E>(a, c, k, g, grid);
+      const uint64_t off = sp.off, cnt = sp.cnt;
       if (!hopWait(0, !last, last && ar)) return;
       if (tid == 0) {
-        sh.src[0] = send + off * sizeof(E);
+        sh.src[0] = sp.send + off * sizeof(E);
         sh.src[1] = simpleStage(a, me, 0, sh.cnt[kCtRsRecv][left] % slots, left, g);
         // the last hop's chunk is `me`; ReduceScatter's output holds that block only
-        sh.dst[0] = last ? recv + (ar ? off : off - (uint64_t)me * a.blockElts) * sizeof(E)
+        sh.dst[0] = last ? sp.recv + (ar ? off : off - (uint64_t)me * sp.blockElts) * sizeof(E)
                          : simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g);
         sh.dst[1] = simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g);
       }
@@ -540,19 +565,35 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
     for (int st = 0; st < n - 1; st++) {
       const int c = (me + 2 * n - 1 - st) % n;
       const bool fwd = st < n - 2;
-      uint64_t off, cnt;
-      simpleSlice<E>(a, c, k, &off, &cnt);
+      const SimpleSpan sp = simpleSlice<E>(a, c, k, g, grid);
       if (!hopWait(1, false, fwd)) return;
-      if (cnt)
-        simpleCopy<E>(recv + off * sizeof(E), false,
+      if (sp.cnt)
+        simpleCopy<E>(sp.recv + sp.off * sizeof(E), false,
                       fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr, true,
-                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, cnt);
+                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, sp.cnt);
       simpleDrain();
       hopPost(1, false, fwd);
     }
   }
-  simpleStoreCounters(a, sh);
+  simpleStoreCounters(a, sh, g);
   mpArrive(a.order);
+}
+
+template <class Fn>
+__global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
+  simpleRingBody<Fn>(a, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// Every rank of a one-process rig in ONE launch (workgroup b runs rank
+// b / grid's workgroup b % grid): the rig's call as a single dispatch, so a
+// rocprofv3 PMC pass — which serializes dispatches — can count its HBM bytes
+// (the per-rank launches wait for each other and cannot be serialized).
+// Measurement only (nbxDebugSimpleRun with NBX_DEBUG_SIMPLE_FUSED=1).
+template <class Fn, bool RING>
+__global__ __launch_bounds__(kBlock) void kSimpleFused(const SimpleArgs* __restrict__ as, int grid) {
+  const int r = (int)blockIdx.x / grid, g = (int)blockIdx.x % grid;
+  if (RING) simpleRingBody<Fn>(as[r], g, grid);
+  else simpleCollBody<Fn>(as[r], g, grid);
 }
 
 }  // namespace nbx

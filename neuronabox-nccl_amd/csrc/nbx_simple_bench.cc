@@ -8,6 +8,7 @@
 // collectives calls it.
 #include <hip/hip_runtime_api.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/nbx_debug.h"
@@ -135,12 +136,34 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugSimpleRun(
     sa.gridMax = gridMax;
     sa.prefetch = prefetch;
   }
+  // NBX_DEBUG_SIMPLE_FUSED=1: every rank's workgroups in ONE dispatch (fp32
+  // sum), so a rocprofv3 PMC pass (which serializes dispatches) can count the
+  // call's HBM bytes; the per-rank launches wait on each other and cannot be
+  // serialized
+  const char* fv = std::getenv("NBX_DEBUG_SIMPLE_FUSED");
+  const bool fused = fv && *fv == '1';
+  nbx::SimpleArgs* argsDev = nullptr;
+  if (fused) {
+    if (datatype != 7 || opFull.op != nbxDevSum || (uint64_t)n * grid > 2048) return ncclInvalidArgument;
+    for (auto& sa : args) {
+      sa.arg = 0;
+      sa.argPtr = nullptr;
+    }
+    if (hipMalloc((void**)&argsDev, n * sizeof(nbx::SimpleArgs)) != hipSuccess ||
+        hipMemcpy(argsDev, args.data(), n * sizeof(nbx::SimpleArgs), hipMemcpyHostToDevice) != hipSuccess)
+      return ncclUnhandledCudaError;
+  }
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return ncclUnhandledCudaError;
   float ms = 0.f;
   // one untimed call, then `iters` timed ones; the n launches of a call run together
   for (int it = 0; it <= iters; it++) {
     if (it == 1 && hipEventRecord(e0, rig.streams[0]) != hipSuccess) return ncclUnhandledCudaError;
+    if (fused) {
+      if (nbx::launchSimpleFusedF32Sum(argsDev, n, (unsigned)grid, ring != 0, rig.streams[0]) != ncclSuccess)
+        return ncclUnhandledCudaError;
+      continue;
+    }
     for (int r = 0; r < n; r++) {
       if (it == 1 && r > 0 && hipStreamWaitEvent(rig.streams[r], e0, 0) != hipSuccess) return ncclUnhandledCudaError;
       if (nbx::launchSimple((ncclDataType_t)datatype, opFull, args[r], (unsigned)grid, ring != 0, rig.streams[r]) !=
@@ -161,6 +184,7 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugSimpleRun(
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (hipDeviceSynchronize() != hipSuccess) return ncclUnhandledCudaError;
+  if (argsDev) (void)hipFree(argsDev);
   if (msPerCall) *msPerCall = ms / (float)iters;
   return rig.hostWords[1] != 0 ? ncclRemoteError : ncclSuccess;
 }

@@ -199,7 +199,8 @@ struct PendingColl {
 
 struct Clique {
   int n = 0;
-  bool ll = false;   // LL / LL128-sized calls run in-kernel (every rank has comm->lt)
+  bool ll = false;       // LL / LL128-sized calls run in-kernel (every rank has comm->lt)
+  bool simple = false;   // and Simple-sized calls too (every rank's lt has Simple staging)
   std::vector<ncclComm*> comms;
   std::vector<int> devs;
   std::vector<hipEvent_t> evEnter, evReduced, evDone;   // one per rank
@@ -448,7 +449,6 @@ ncclResult_t foldBlocksBatched(const std::vector<const PendingColl*>& colls, con
 
 // The in-process LL transport of a clique (defined with the multi-process code it shares).
 enum MpProto : int;
-MpProto cliqueProtoOf(Clique* c, const std::vector<PendingColl>& parts);
 bool cliqueInKernel(Clique* c, const std::vector<PendingColl>& parts);
 ncclResult_t cliqueRunLL(Clique* c, const std::vector<std::vector<PendingColl>>& rounds, size_t lo, size_t hi);
 ncclResult_t cliqueOrderBefore(Clique* c, int r, hipStream_t s);
@@ -1064,6 +1064,50 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
 // repeats (at most 4). Only then does ncclCommInitRank fail (ncclSystemError).
 // NBX_IPC_VERIFY_FAIL=<rank>:<buffer> (test hook) makes round 0 report that
 // rank's buffer (0 LL, 1 LL128, 2 staging, 3 flags) wrong.
+// Grid caps and Simple settings of one rank's transport. Simple grid: one
+// workgroup per CU, all co-resident (workgroup g of a rank waits on workgroup
+// g of its peers); ranks sharing a GPU split its CUs, and so do the LL
+// family's spinning grids (the env caps still apply on top).
+void mpTransportSettings(MpState* mp, int minCus, int maxShare) {
+  const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0), minCh = envLong("NCCL_MIN_NCHANNELS", 0);
+  long g = envLong("NBX_SIMPLE_MAX_GRID", 0);
+  if (g <= 0) {
+    g = 128;
+    if (maxCh > 0) g = std::min(g, maxCh);
+    if (minCh > 0) g = std::max(g, minCh);
+  }
+  g = std::min<long>(g, std::max(1, minCus / maxShare));
+  mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);
+  mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
+  if (maxCh > 0) {   // a channel is a workgroup here
+    mp->llGridCap = std::min<uint32_t>(mp->llGridCap, (uint32_t)maxCh);
+    mp->l128GridCap = std::min<uint32_t>(mp->l128GridCap, (uint32_t)maxCh);
+  }
+  mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
+  mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
+  long sl = ncclEnvMapped("NBX_SIMPLE_SLICE_BYTES", "NCCL_BUFFSIZE", 64 << 10, 1, mp->slots);
+  sl = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(sl, 1 << 20));
+  mp->sliceBytes = (uint64_t)(sl + 15) & ~(uint64_t)15;
+  if (const char* nt = std::getenv("NCCL_NTHREADS"); nt && *nt && std::atol(nt) != 256)
+    info("NCCL_NTHREADS=%s ignored: every kernel of this library runs 256-thread workgroups", nt);
+  mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
+}
+
+// The Simple protocol's staging and flag words (uncached, exported when
+// `ipc`, with the check region mpConnect uses) and its counters.
+ncclResult_t mpAllocSimple(MpState* mp, int n, bool ipc) {
+  const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
+  mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
+  HIPCHECK(allocSyncMem((void**)&mp->stage, connAllocBytes(mp->stageBytes, n), ipc ? &mp->stageHandle : nullptr));
+  HIPCHECK(hipMemset(mp->stage, 0, connAllocBytes(mp->stageBytes, n)));
+  mp->sflagsBytes = 4 * cells * sizeof(uint64_t);
+  HIPCHECK(allocSyncMem((void**)&mp->sflags, connAllocBytes(mp->sflagsBytes, n), ipc ? &mp->sflagsHandle : nullptr));
+  HIPCHECK(hipMemset(mp->sflags, 0, connAllocBytes(mp->sflagsBytes, n)));
+  HIPCHECK(hipMalloc((void**)&mp->scounters, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->scounters, 0, 4 * cells * sizeof(uint64_t)));
+  return ncclSuccess;
+}
+
 ncclResult_t mpConnect(ncclComm* c, const std::vector<MpInitInfo>& all) {
   MpState* mp = c->mp;
   const int n = c->nRanks, me = c->rank;
@@ -1231,45 +1275,9 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     for (int q = 0; q < n; q++) share += pres[q].pciKey == pres[j].pciKey;
     maxShare = std::max(maxShare, share);
   }
-  // Simple grid: one workgroup per CU, all co-resident (workgroup g of a rank
-  // waits on workgroup g of its peers); ranks sharing a GPU split its CUs.
-  {
-    const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0), minCh = envLong("NCCL_MIN_NCHANNELS", 0);
-    long g = envLong("NBX_SIMPLE_MAX_GRID", 0);
-    if (g <= 0) {
-      g = 128;
-      if (maxCh > 0) g = std::min(g, maxCh);
-      if (minCh > 0) g = std::max(g, minCh);
-    }
-    g = std::min<long>(g, std::max(1, minCus / maxShare));
-    // the LL family's spinning grids too: every rank's grid stays co-resident
-    // when several ranks share one GPU (the env caps still apply on top)
-    mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);
-    mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
-    if (maxCh > 0) {
-      mp->llGridCap = std::min<uint32_t>(mp->llGridCap, (uint32_t)maxCh);
-      mp->l128GridCap = std::min<uint32_t>(mp->l128GridCap, (uint32_t)maxCh);
-    }
-    mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
-    mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
-    long s = ncclEnvMapped("NBX_SIMPLE_SLICE_BYTES", "NCCL_BUFFSIZE", 64 << 10, 1, mp->slots);
-    s = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(s, 1 << 20));
-    mp->sliceBytes = (uint64_t)(s + 15) & ~(uint64_t)15;
-    if (const char* nt = std::getenv("NCCL_NTHREADS"); nt && *nt && std::atol(nt) != 256)
-      info("NCCL_NTHREADS=%s ignored: every kernel of this library runs 256-thread workgroups", nt);
-    mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
-  }
+  mpTransportSettings(mp, minCus, maxShare);
   NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true, c));
-  // Simple staging, flag words and counters
-  const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
-  mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
-  HIPCHECK(allocSyncMem((void**)&mp->stage, connAllocBytes(mp->stageBytes, n), &mp->stageHandle));
-  HIPCHECK(hipMemset(mp->stage, 0, connAllocBytes(mp->stageBytes, n)));
-  mp->sflagsBytes = 4 * cells * sizeof(uint64_t);
-  HIPCHECK(allocSyncMem((void**)&mp->sflags, connAllocBytes(mp->sflagsBytes, n), &mp->sflagsHandle));
-  HIPCHECK(hipMemset(mp->sflags, 0, connAllocBytes(mp->sflagsBytes, n)));
-  HIPCHECK(hipMalloc((void**)&mp->scounters, 4 * cells * sizeof(uint64_t)));
-  HIPCHECK(hipMemset(mp->scounters, 0, 4 * cells * sizeof(uint64_t)));
+  NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/true));
   HIPCHECK(hipDeviceSynchronize());   // zeroed before any peer can map and write them
 
   MpInitInfo mine{};
@@ -1445,34 +1453,61 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
 // whole message as one block (a chain). A call of B-byte blocks runs on
 // min(grid, B / 4 KiB) workgroups in rounds of one slice per workgroup and
 // block, the slice at most the staging slice — every rank derives the same
-// numbers from the same arguments.
-ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall& c) {
-  MpState* mp = comm->mp;
+// numbers from the same arguments. Several calls of one group (nc > 1, same
+// kind / type / op / root) run as ONE launch: block b of the launch is block
+// b of every message in turn (SimpleSeg), cut into the launch's slices.
+ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc) {
+  MpState* mp = mpOf(comm);
+  const MpCall& c = calls[0];
   const int n = comm->nRanks, me = comm->rank;
   const uint64_t eb = (uint64_t)typeSize(c.dt);
+  auto shape = [&](const MpCall& m, uint64_t* blockElts, uint64_t* total) {
+    if (m.kind == kReduceScatter) {
+      *blockElts = m.count;
+      *total = (uint64_t)m.count * (uint64_t)n;
+    } else if (m.kind == kReduce && mp->ring) {
+      *blockElts = m.count;
+      *total = m.count;
+    } else {
+      size_t o0, per;
+      blockRange(m.count, (int)eb, n, 0, &o0, &per);
+      *blockElts = per;
+      *total = m.count;
+    }
+  };
   nbx::SimpleArgs sa{};
   sa.send = c.send;
   sa.recv = c.recv;
-  if (c.kind == kReduceScatter) {
-    sa.blockElts = c.count;
-    sa.total = (uint64_t)c.count * (uint64_t)n;
-  } else if (c.kind == kReduce && mp->ring) {
-    sa.blockElts = c.count;
-    sa.total = c.count;
-  } else {
-    size_t o0, per;
-    blockRange(c.count, (int)eb, n, 0, &o0, &per);
-    sa.blockElts = per;
-    sa.total = c.count;
+  shape(c, &sa.blockElts, &sa.total);
+  uint64_t blockBytes = std::min<uint64_t>(sa.blockElts, sa.total) * eb;   // every message's block 0 together
+  std::vector<uint64_t> segBlockBytes;
+  if (nc > 1) {
+    blockBytes = 0;
+    for (int s = 0; s < nc; s++) {
+      uint64_t be, tot;
+      shape(calls[s], &be, &tot);
+      sa.seg[s] = nbx::SimpleSeg{calls[s].send, calls[s].recv, tot, be, 0};
+      segBlockBytes.push_back(std::min<uint64_t>(be, tot) * eb);
+      blockBytes += segBlockBytes.back();
+    }
+    sa.nSegs = nc;
   }
-  const uint64_t blockBytes = std::min<uint64_t>(sa.blockElts, sa.total) * eb;
   if (blockBytes == 0) return ncclSuccess;
   uint64_t grid = (blockBytes + nbx::kSimpleMinSliceBytes - 1) / nbx::kSimpleMinSliceBytes;
   grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, (uint64_t)mp->simpleGrid));
   uint64_t slice = ((blockBytes + grid - 1) / grid + 15) & ~(uint64_t)15;
   slice = std::min<uint64_t>(slice, mp->sliceBytes);
   sa.sliceBytes = slice;
-  sa.nRounds = (blockBytes + grid * slice - 1) / (grid * slice);
+  if (nc > 1) {   // every message's slices of a block, back to back
+    uint64_t off = 0;
+    for (int s = 0; s < nc; s++) {
+      sa.seg[s].sliceOff = off;
+      off += (segBlockBytes[s] + slice - 1) / slice;
+    }
+    sa.nRounds = (off + grid - 1) / grid;
+  } else {
+    sa.nRounds = (blockBytes + grid * slice - 1) / (grid * slice);
+  }
   sa.peerStage = mp->peerStageDev;
   sa.peerFlags = mp->peerSFlagsDev;
   sa.counters = mp->scounters;
@@ -1536,13 +1571,14 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
   if (c.count == 0) return ncclSuccess;
   return runMpOrdered(comm, c.stream, [&]() -> ncclResult_t {
     const MpProto proto = mpProtoOf(comm, c);
-    return proto == kMpSimple ? mpLaunchSimple(comm, c) : mpLaunchLL(comm, c, proto);
+    return proto == kMpSimple ? mpLaunchSimple(comm, &c, 1) : mpLaunchLL(comm, c, proto);
   });
 }
 
-// Several LL / LL128 one-shot calls of one group as ONE kernel (NCCL aggregates a group's
-// collectives into one launch, enqueue.cc:67-91): their slots concatenated
-// (LLSeg). The launch goes on the first call's stream; if the calls use other
+// Several LL / LL128 one-shot / Simple calls of one group as ONE kernel (NCCL
+// aggregates a group's collectives into one launch, enqueue.cc:67-91): their
+// LL slots concatenated (LLSeg), or their Simple blocks (SimpleSeg). The
+// launch goes on the first call's stream; if the calls use other
 // streams too, the first waits for them before it and they wait for it after
 // (NCCL's fan-in / fan-out, enqueue.cc:964-995, 1135-1148).
 ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc, MpProto proto) {
@@ -1561,7 +1597,9 @@ ncclResult_t runMpLLGroup(ncclComm* comm, const MpCall* calls, int nc, MpProto p
     HIPCHECK(hipEventRecord(mp->groupEvents[k + 1], others[k]));
     HIPCHECK(hipStreamWaitEvent(s0, mp->groupEvents[k + 1], 0));
   }
-  NCCLCHECK(runMpOrdered(comm, s0, [&]() { return mpLaunchLL(comm, calls[0], proto, calls, nc); }));
+  NCCLCHECK(runMpOrdered(comm, s0, [&]() {
+    return proto == kMpSimple ? mpLaunchSimple(comm, calls, nc) : mpLaunchLL(comm, calls[0], proto, calls, nc);
+  }));
   if (!others.empty()) {
     HIPCHECK(hipEventRecord(mp->groupEvents[0], s0));
     for (hipStream_t s : others) HIPCHECK(hipStreamWaitEvent(s, mp->groupEvents[0], 0));
@@ -1664,19 +1702,20 @@ ncclResult_t mpLL128SelfTest(ncclComm* c) {
 // calls in the same order, as NCCL requires.
 thread_local std::vector<ncclComm*> t_groupMpComms;
 
-// Maximal runs of consecutive calls of the same protocol (LL, or LL128
-// one-shot) with the same kind, datatype, op and root, whose slots fit one
-// slot of that protocol together (at most kLLMaxSegs), run as one launch
-// (runMpLLGroup) — a decision made from arguments every rank passes
-// identically, so every rank cuts the same runs. A run also ends before a call
-// that reads or writes what an earlier call of the run writes (or writes what
-// it reads): the segments of one launch run concurrently, so such a chain
-// (AllReduce a->b, then b->c) must stay separate launches, in order. That cut
-// looks at this rank's own buffers; the ranks of an SPMD program alias alike
-// and cut alike. Ranks that alias differently cut different runs, and their
-// kernels then wait for lines that never come and time out with the wait
-// named (nbx_diag.h) — an error, never a silently wrong result.
-// (NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order.)
+// Maximal runs of consecutive calls of the same protocol (LL, LL128
+// one-shot, or Simple) with the same kind, datatype, op and root — LL / LL128
+// runs whose slots fit one slot of that protocol together, at most
+// kLLMaxSegs / kSimpleMaxSegs calls — run as one launch (runMpLLGroup): a
+// decision made from arguments every rank passes identically, so every rank
+// cuts the same runs. A run also ends before a call that reads or writes
+// what an earlier call of the run writes (or writes what it reads): the
+// segments of one launch run concurrently, so such a chain (AllReduce a->b,
+// then b->c) must stay separate launches, in order. That cut looks at this
+// rank's own buffers; the ranks of an SPMD program alias alike and cut alike.
+// A group whose calls alias differently on different ranks is outside what
+// the batching supports (LL / LL128 ranks then time out waiting for lines
+// that never come; Simple ranks could fold misplaced slices):
+// NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order.
 void mpCallSpans(const MpCall& c, int n, int rank, std::vector<Span>* out) {
   const size_t eb = (size_t)typeSize(c.dt);
   const size_t sendBytes = (c.kind == kReduceScatter ? c.count * (size_t)n : c.count) * eb;
@@ -1696,7 +1735,9 @@ ncclResult_t runMpGroup(ncclComm* comm) {
     const uint64_t unit = p == kMpLL ? 8 : (uint64_t)nbx::kL128DataBytesHost;
     return ((uint64_t)c.count * (uint64_t)typeSize(c.dt) + unit - 1) / unit;
   };
-  auto capOf = [&](MpProto p) { return p == kMpLL ? mp->llSlotLines / 2 : mp->l128SlotLines; };
+  auto capOf = [&](MpProto p) {
+    return p == kMpLL ? mp->llSlotLines / 2 : p == kMpLL128 ? mp->l128SlotLines : ~(uint64_t)0;   // Simple: rounds
+  };
   auto sameOp = [](const MpCall& a, const MpCall& b) {
     return a.kind == b.kind && a.dt == b.dt && a.op.op == b.op.op && a.op.scalarArg == b.op.scalarArg &&
            a.op.scalarArgIsPtr == b.op.scalarArgIsPtr && (a.kind != kReduce || a.root == b.root);
@@ -1706,18 +1747,18 @@ ncclResult_t runMpGroup(ncclComm* comm) {
     while (i < calls.size() && r == ncclSuccess) {
       size_t j = i + 1;
       const MpProto p = calls[i].count > 0 ? mpProtoOf(comm, calls[i]) : kMpSimple;
-      if (mp->groupBatch && (p == kMpLL || p == kMpLL128)) {
-        uint64_t used = unitsOf(calls[i], p);
+      const size_t maxSegs = p == kMpSimple ? (size_t)nbx::kSimpleMaxSegs : (size_t)nbx::kLLMaxSegs;
+      if (mp->groupBatch && (p == kMpLL || p == kMpLL128 || p == kMpSimple)) {
+        uint64_t used = p == kMpSimple ? 0 : unitsOf(calls[i], p);
         std::vector<Span> spans, sj;
         mpCallSpans(calls[i], comm->nRanks, comm->rank, &spans);
-        while (j < calls.size() && j - i < (size_t)nbx::kLLMaxSegs && calls[j].count > 0 &&
-               sameOp(calls[i], calls[j]) && mpProtoOf(comm, calls[j]) == p &&
-               used + unitsOf(calls[j], p) <= capOf(p)) {
+        while (j < calls.size() && j - i < maxSegs && calls[j].count > 0 && sameOp(calls[i], calls[j]) &&
+               mpProtoOf(comm, calls[j]) == p && (p == kMpSimple || used + unitsOf(calls[j], p) <= capOf(p))) {
           sj.clear();
           mpCallSpans(calls[j], comm->nRanks, comm->rank, &sj);
           if (spansConflict(spans, sj)) break;
           spans.insert(spans.end(), sj.begin(), sj.end());
-          used += unitsOf(calls[j], p);
+          if (p != kMpSimple) used += unitsOf(calls[j], p);
           j++;
         }
       }
@@ -1769,6 +1810,10 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
     for (int j = 0; j < r; j++) distinct &= cl->devs[r] != cl->devs[j];
   const char* v = std::getenv("NBX_CLIQUE_LL");
   if (!((v && *v) ? std::atoi(v) != 0 : distinct)) return ncclSuccess;
+  // Simple sizes in-kernel too (the multi-process Simple kernels over the
+  // clique's staging, reached by direct peer pointers) unless NBX_CLIQUE_SIMPLE=0
+  // keeps them on the event-ordered fold
+  const bool simple = envLong("NBX_CLIQUE_SIMPLE", 1) != 0;
   int minCus = 1 << 30, maxShare = 1;
   for (int r = 0; r < n; r++) {
     int cus = 0, share = 0;
@@ -1783,18 +1828,18 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
     cl->comms[r]->lt = mp;
     NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/false, cl->comms[r]));
     mp->multiGpu = distinct;
-    mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);   // co-resident, as mpInit
-    mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
-    if (const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0); maxCh > 0) {   // a channel is a workgroup (mpInit)
-      mp->llGridCap = std::min<uint32_t>(mp->llGridCap, (uint32_t)maxCh);
-      mp->l128GridCap = std::min<uint32_t>(mp->l128GridCap, (uint32_t)maxCh);
-    }
+    mp->ring = algoRingFromEnv();
+    mpTransportSettings(mp, minCus, maxShare);   // co-resident grids, as mpInit
+    if (simple) NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/false));
     mp->extDone = cl->evDone;
   }
-  std::vector<uint64_t*> llTable(n), l128Table(n);
+  std::vector<uint64_t*> llTable(n), l128Table(n), flagTable(n);
+  std::vector<char*> stageTable(n);
   for (int r = 0; r < n; r++) {
     llTable[r] = cl->comms[r]->lt->ll;
     l128Table[r] = cl->comms[r]->lt->l128;
+    stageTable[r] = cl->comms[r]->lt->stage;
+    flagTable[r] = cl->comms[r]->lt->sflags;
   }
   for (int r = 0; r < n; r++) {
     DevGuard g(cl->devs[r]);
@@ -1805,27 +1850,33 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
       HIPCHECK(hipMalloc((void**)&mp->peerL128Dev, n * sizeof(uint64_t*)));
       HIPCHECK(hipMemcpy(mp->peerL128Dev, l128Table.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice));
     }
+    if (simple) {
+      HIPCHECK(hipMalloc((void**)&mp->peerStageDev, n * sizeof(char*)));
+      HIPCHECK(hipMemcpy(mp->peerStageDev, stageTable.data(), n * sizeof(char*), hipMemcpyHostToDevice));
+      HIPCHECK(hipMalloc((void**)&mp->peerSFlagsDev, n * sizeof(uint64_t*)));
+      HIPCHECK(hipMemcpy(mp->peerSFlagsDev, flagTable.data(), n * sizeof(uint64_t*), hipMemcpyHostToDevice));
+    }
     HIPCHECK(hipDeviceSynchronize());   // zeroed and uploaded before any peer's first kernel
   }
   cl->ll = true;
-  info("clique of %d ranks: LL / LL128-sized calls run in-kernel (grid caps %u / %u)", n,
-       cl->comms[0]->lt->llGridCap, cl->comms[0]->lt->l128GridCap);
+  cl->simple = simple;
+  info("clique of %d ranks: LL / LL128%s-sized calls run in-kernel (grid caps %u / %u)", n,
+       simple ? " / Simple" : "", cl->comms[0]->lt->llGridCap, cl->comms[0]->lt->l128GridCap);
   return ncclSuccess;
 }
 
-// The protocol a clique collective runs with on the in-process transport, or
-// kMpSimple for the fold path. Decided once for all ranks.
-MpProto cliqueProtoOf(Clique* c, const std::vector<PendingColl>& parts) {
-  if (!c->ll || parts[0].count == 0 || !sameCollective(parts)) return kMpSimple;
+// Whether a clique collective runs in-kernel on the in-process transport
+// (one kernel per rank, its protocol chosen as on a multi-process
+// communicator) or on the event-ordered fold path. Decided once for all ranks.
+bool cliqueInKernel(Clique* c, const std::vector<PendingColl>& parts) {
+  if (!c->ll || parts[0].count == 0 || !sameCollective(parts)) return false;
   for (int r = 0; r < c->n; r++) {
-    if (c->comms[r] == nullptr || c->comms[r]->lt == nullptr) return kMpSimple;
+    if (c->comms[r] == nullptr || c->comms[r]->lt == nullptr) return false;
     for (int j = 0; j < r; j++)
-      if (parts[j].stream == parts[r].stream) return kMpSimple;   // one rank's kernel would queue behind another's
+      if (parts[j].stream == parts[r].stream) return false;   // one rank's kernel would queue behind another's
   }
-  return mpProtoOf(c->comms[0], parts[0]);
+  return c->simple || mpProtoOf(c->comms[0], parts[0]) != kMpSimple;
 }
-
-bool cliqueInKernel(Clique* c, const std::vector<PendingColl>& parts) { return cliqueProtoOf(c, parts) != kMpSimple; }
 
 // Consecutive in-kernel collectives [lo, hi): every rank runs them as a group
 // (runMpGroup cuts the same batched launches on every rank).

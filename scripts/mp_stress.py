@@ -5,7 +5,9 @@ same random plan from a shared seed — a sequence of AllReduce /
 ReduceScatter / Reduce calls of random datatype, op, size (spanning LL, LL128
 one- and two-shot and Simple), stream (two per rank, no caller ordering
 between them) and group boundaries (runs of calls inside ncclGroupStart/End,
-where compatible LL-sized calls become one launch) — issues it without host
+where runs of compatible LL / LL128 / Simple calls become one launch; a
+third of the calls repeat the previous call's kind / type / op so such runs
+occur) — issues it without host
 synchronisation, then checks every output exactly against torch on the GPU
 (small-integer inputs, so every fold order gives the same value; every rank
 regenerates every rank's input from the seed). Reports one JSON line per rank
@@ -34,11 +36,15 @@ def plan(rng, n):
         kind = rng.choice(["allreduce", "allreduce", "reducescatter", "reduce"])
         dt, tname = rng.choice(TYPES)
         op = rng.choice([0, 0, 2, 3])
+        root = rng.randrange(n)
+        if calls and rng.random() < 0.35:   # runs of one kind / type / op (/ root): what a group launch batches
+            p = calls[-1]
+            kind, dt, tname, op, root = p["kind"], p["dt"], p["t"], p["op"], p["root"]
         count = rng.choice(SIZES)
         if tname in ("float16", "bfloat16") and op == 0:
             count = min(count, 40000)
         calls.append({"kind": kind, "dt": dt, "t": tname, "op": op, "count": count, "stream": rng.randint(0, 1),
-                      "root": rng.randrange(n), "group": rng.random() < 0.5})
+                      "root": root, "group": rng.random() < 0.5})
     return calls
 
 

@@ -19,9 +19,13 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("ranks,seed", [("2,3", 21), ("4", 22)])
-def test_clique_in_kernel_transport_random_plans_exact(ranks, seed):
+@pytest.mark.parametrize("ranks,seed,simple", [("2,3", 21, "1"), ("4", 22, "1"), ("3", 23, "0")])
+def test_clique_in_kernel_transport_random_plans_exact(ranks, seed, simple):
+    """simple = 1 (default): Simple-sized calls run in-kernel too (the
+    multi-process Simple kernels over the clique's staging); 0: they keep the
+    event-ordered fold path."""
     env = {k: v for k, v in os.environ.items() if k not in ("GPU_MAX_HW_QUEUES", "NBX_CLIQUE_LL")}
+    env["NBX_CLIQUE_SIMPLE"] = simple
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "clique_stress.py"), ranks, "5", str(seed)],
                          capture_output=True, text=True, timeout=220, cwd=ROOT, env=env)
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

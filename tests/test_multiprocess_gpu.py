@@ -1029,7 +1029,20 @@ def _small_inputs(oracle, k, kind, dtype, count, n, r):
     return oracle.random_inputs(dtype, n, cnt, seed=5000 + 7 * k)[r]
 
 
-def _child_group_small(uid_bytes, rank, n, q):
+# Simple-sized groups (run with NCCL_PROTO=Simple): runs of one kind / type /
+# op become ONE Simple launch (SimpleSeg), cut at 16 calls, at kind / type /
+# op / root changes and where a call reads what an earlier one of the run
+# writes; sizes with partial slices, ragged blocks and one-element messages.
+GROUP_SIMPLE = ([("allreduce", 7, 0, c, 0) for c in (300000, 1, 40009, 1 << 20, 17, 70000)] +
+                [("allreduce", 7, 0, 5000 + i, i % 2) for i in range(20)] +
+                [("allreduce", 9, 0, c, 0) for c in (40000, 1023, 200001)] +
+                [("reducescatter", 2, 2, c, 0) for c in (100000, 3, 65536)] +
+                [("reduce", 4, 3, c, 0) for c in (77777, 1, 300000)] +
+                [("allreduce", 6, 4, c, 0) for c in (33333, 99999)])
+
+
+def _child_group_small(uid_bytes, rank, n, q, which="small"):
+    cases = GROUP_SIMPLE if which == "simple" else GROUP_SMALL
     try:
         import torch
         from tests.conftest import load_package
@@ -1043,7 +1056,7 @@ def _child_group_small(uid_bytes, rank, n, q):
         for it in range(2):
             live = []
             nbx.group_start()
-            for k, (kind, dtype, op, count, si) in enumerate(GROUP_SMALL):
+            for k, (kind, dtype, op, count, si) in enumerate(cases):
                 x = _small_inputs(oracle, k, kind, dtype, count, n, rank)
                 tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
                 ty = torch.full((count * x.itemsize,), 0xAB, dtype=torch.uint8, device="cuda")
@@ -1068,16 +1081,23 @@ def _child_group_small(uid_bytes, rank, n, q):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("n,batch", [(2, "1"), (3, "1"), (3, "0")])
-def test_multiprocess_grouped_small_calls_one_launch(nbx, oracle, n, batch, monkeypatch):
-    """Bit-exact vs the oracle in the direct schedule's order, batched into LL
-    group launches (NBX_GROUP_BATCH=1, default) and one kernel per call (0)."""
+@pytest.mark.parametrize("n,batch,which,algo", [(2, "1", "small", ""), (3, "1", "small", ""), (3, "0", "small", ""),
+                                                 (2, "1", "simple", ""), (3, "1", "simple", ""),
+                                                 (4, "1", "simple", "Ring"), (3, "0", "simple", "")])
+def test_multiprocess_grouped_small_calls_one_launch(nbx, oracle, n, batch, which, algo, monkeypatch):
+    """Bit-exact vs the oracle in the direct schedule's order, batched into
+    group launches (NBX_GROUP_BATCH=1, default) and one kernel per call (0):
+    LL / LL128 runs ("small"), and Simple runs ("simple", NCCL_PROTO=Simple;
+    direct and ring schedules — for the commutative ops tested the ring's
+    order gives the same bits)."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     monkeypatch.setenv("NBX_LL_MAX_GRID", "64")
     monkeypatch.setenv("NBX_GROUP_BATCH", batch)
-    res = _run_ranks(nbx, n, _child_group_small)
-    for k, (kind, dtype, op, count, si) in enumerate(GROUP_SMALL):
+    monkeypatch.setenv("NCCL_PROTO", "Simple" if which == "simple" else "")
+    monkeypatch.setenv("NCCL_ALGO", algo)
+    res = _run_ranks(nbx, n, _child_group_small, which)
+    for k, (kind, dtype, op, count, si) in enumerate(GROUP_SIMPLE if which == "simple" else GROUP_SMALL):
         xs = [_small_inputs(oracle, k, kind, dtype, count, n, r) for r in range(n)]
         devop, arg = oracle.host_to_dev_redop(op, dtype, n)
         st = oracle.NP_STORAGE[dtype]
