@@ -142,15 +142,21 @@ __device__ __forceinline__ SimpleSpan simpleSlice(const SimpleArgs& a, int b, ui
   SimpleSpan sp{(const char*)a.send, (char*)a.recv, 0, 0, a.blockElts};
   uint64_t total = a.total;
   if (a.nSegs > 0) {
-    int s = 0;
-    for (int q = 1; q < a.nSegs; q++)
-      if (v >= a.seg[q].sliceOff) s = q;
-    const SimpleSeg& sg = a.seg[s];
-    sp.send = (const char*)sg.send;
-    sp.recv = (char*)sg.recv;
-    sp.blockElts = sg.blockElts;
-    total = sg.total;
-    v -= sg.sliceOff;
+    // the last segment starting at or before v (sliceOff ascending); constant
+    // indices only, so the table stays in the kernel-argument segment (a
+    // run-time index copies the whole argument block to scratch)
+    uint64_t base = 0;
+#pragma unroll
+    for (int q = 0; q < kSimpleMaxSegs; q++) {
+      if (q < a.nSegs && v >= a.seg[q].sliceOff) {
+        sp.send = (const char*)a.seg[q].send;
+        sp.recv = (char*)a.seg[q].recv;
+        sp.blockElts = a.seg[q].blockElts;
+        total = a.seg[q].total;
+        base = a.seg[q].sliceOff;
+      }
+    }
+    v -= base;
   }
   uint64_t lo = (uint64_t)b * sp.blockElts;
   if (lo > total) lo = total;
