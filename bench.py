@@ -449,6 +449,30 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     # LL128 kept by every rank's creation-time probe (else LL / Simple carried those sizes)
     act = [r.get("ll128_active") for r in allres]
     out["ll128_active"] = None if any(a is None for a in act) else all(act)
+    out["hbm_model"] = simple_hbm_model(world, S)
+    return out
+
+
+def simple_hbm_model(world: int, msg_bytes: int):
+    """Per-rank byte model of a config-D Simple AllReduce (both schedules):
+    the user-visible bytes, the HBM bytes the staging design moves, and what
+    crosses xGMI each way, with the measured HBM / model ratio from the
+    committed PMC passes of the same kernels (profiles/r4/simple_traffic_pmc_r4j.json:
+    2 ranks on one GPU, one fused dispatch) — carried over, not measured here."""
+    n, M = world, msg_bytes
+    model = 2 * (M + 2 * (n - 1) * M // n)
+    out = {"algorithmic_bytes_per_rank": 2 * M, "staging_model_bytes_per_rank": model,
+           "xgmi_bytes_per_rank_each_way": 2 * (n - 1) * M // n,
+           "what": "staging model per rank = 2 x (M + 2 (n-1) M / n) HBM bytes (send block into peers' staging; "
+                   "fold of own input + n-1 slots into the output and peers' AG staging; gather of n-1 slots)"}
+    try:
+        with open(os.path.join(ROOT, "profiles", "r4", "simple_traffic_pmc_r4j.json")) as f:
+            d = json.load(f)
+        out["measured_over_model"] = {k: d[k]["hbm_over_model"] for k in ("direct", "ring")}
+        out["measured_provenance"] = ("profiles/r4/simple_traffic_pmc_r4j.json (rocprofv3 FETCH_SIZE / WRITE_SIZE "
+                                      "passes, 2 ranks on one GPU); not measured in this run")
+    except (OSError, ValueError, KeyError):
+        out["measured_over_model"] = None
     return out
 
 

@@ -28,3 +28,14 @@ def test_vs_rccl_missing_pieces():
     assert bench.vs_rccl({"allreduce_direct": None}, {"ok": False}) is None
     v = bench.vs_rccl({"allreduce_direct": None, "reduce_scatter": None}, {"ok": True})
     assert v["allreduce_1GiB"] is None and "sweep_best_protocol" not in v
+
+
+def test_simple_hbm_model():
+    m = bench.simple_hbm_model(2, 1 << 30)
+    assert m["algorithmic_bytes_per_rank"] == 2 << 30
+    assert m["staging_model_bytes_per_rank"] == 4 << 30      # n = 2: twice the user-visible bytes
+    assert m["xgmi_bytes_per_rank_each_way"] == 1 << 30
+    m8 = bench.simple_hbm_model(8, 1 << 30)
+    assert m8["staging_model_bytes_per_rank"] == 2 * ((1 << 30) + 2 * 7 * (1 << 30) // 8)
+    if m8["measured_over_model"] is not None:                 # the committed PMC summary
+        assert 0.95 < m8["measured_over_model"]["direct"] < 1.1
