@@ -337,13 +337,16 @@ def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 4
     if res is None:
         return None
     S = COUNT_D * 4
-    for name, fac in (("allreduce", 2 * (world - 1) / world), ("reduce_scatter", (world - 1) / world)):
+    for name, fac in (("allreduce", 2 * (world - 1) / world), ("reduce_scatter", (world - 1) / world),
+                      ("fold_allreduce", 2 * (world - 1) / world), ("fold_reduce_scatter", (world - 1) / world)):
         ms = res.get(name + "_ms")
         if ms:
             alg = S / (ms * 1e-3) / 1e9
             res[name] = {"ms": round(ms, 4), "algbw_GBs": round(alg, 2), "busbw_GBs": round(alg * fac, 2)}
     res["workload"] = ("config D through ncclCommInitAll (one process, every GPU of the run, no IPC), "
-                       "ncclSum fp32 1 GiB per rank, checked exactly")
+                       "ncclSum fp32 1 GiB per rank, checked exactly; allreduce / reduce_scatter with the clique's "
+                       "defaults (distinct GPUs: the in-kernel Simple transport over staging), fold_* on the "
+                       "event-ordered direct fold (NBX_CLIQUE_SIMPLE=0)")
     return res
 
 

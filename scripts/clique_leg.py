@@ -13,7 +13,11 @@ Spawned by bench.py rank 0 before it touches the GPU, idle until told:
 Inputs are small integers in fp32 (x_r[i] = (7 i + 13 r) mod 1024), so every
 fold order gives the exact sum and every rank's whole output is checked.
 Then 4 KiB / 64 KiB / 1 MiB AllReduces (the in-kernel LL / LL128 transport when
-the devices are distinct), each checked and timed per call.
+the devices are distinct), each checked and timed per call. Config D runs with
+the clique's defaults (distinct devices: Simple sizes in-kernel over staging),
+then again on a second clique with NBX_CLIQUE_SIMPLE=0 (the event-ordered
+direct fold that reads peers' buffers in place) — `fold_*` — so the driver's
+multi-GPU run measures both data paths over xGMI.
 """
 from __future__ import annotations
 
@@ -33,13 +37,17 @@ os.environ.setdefault("NBX_TIMEOUT_SEC", "30")   # before the library loads: a s
 
 
 def run(n: int, devs: list, count: int = COUNT) -> dict:
+    import ctypes
+
     import torch
     from __graft_entry__ import _load_package
     nbx = _load_package()
-    nbx.load_library()
+    lib = nbx.load_library()
     F32, SUM = 7, 0
     res = {"ok": True, "errors": [], "n_ranks": n, "devices": devs}
     comms = nbx.Communicator.init_all(devs)
+    vals = (ctypes.c_int64 * 9)()
+    res["simple_in_kernel"] = lib.nbxDebugCommSettings(comms[0].handle, vals, 9) == 9 and vals[4] > 0
     xs, ys, rs, streams, exps = [], [], [], [], []
     rc = count // n
     for r, d in enumerate(devs):
@@ -102,6 +110,28 @@ def run(n: int, devs: list, count: int = COUNT) -> dict:
             res["errors"].append(f"reduce_scatter rank {r}: {int((rs[r] != want).sum())} elements differ")
     res["reduce_scatter_ms"] = timed(reduce_scatter)
     small_calls(nbx, torch, comms, xs, ys, exps, streams, sync, res)
+    for c in comms:
+        c.destroy()
+    # the same config D on the event-ordered fold path (a second clique)
+    os.environ["NBX_CLIQUE_SIMPLE"] = "0"
+    try:
+        comms = nbx.Communicator.init_all(devs)
+    finally:
+        os.environ.pop("NBX_CLIQUE_SIMPLE", None)
+    for r in range(n):
+        with torch.cuda.device(ys[r].device):
+            ys[r].fill_(-1.0)
+            rs[r].fill_(-1.0)
+    sync()
+    allreduce()
+    reduce_scatter()
+    sync()
+    for r in range(n):
+        if not torch.equal(ys[r], exps[r]) or not torch.equal(rs[r], exps[r][r * rc:(r + 1) * rc]):
+            res["ok"] = False
+            res["errors"].append(f"fold path rank {r}: output differs")
+    res["fold_allreduce_ms"] = timed(allreduce)
+    res["fold_reduce_scatter_ms"] = timed(reduce_scatter)
     for c in comms:
         c.destroy()
     return res
