@@ -5,9 +5,11 @@ back to back after 2 warm-ups, for rocprofv3 kernel-trace / PMC passes
 probe_dtypes.py (fp8: random finite codes; floats: uniform [0, 1)), one
 output. Prints one JSON line: HIP-event device ms per launch, algorithmic
 bytes per launch (9 x input bytes), TB/s.
-usage: dtype_profile.py datatype redop eltbytes MiB_per_input iters
+usage: dtype_profile.py datatype redop eltbytes MiB_per_input iters [blocksPerCU variant]
   e.g. 10 0 1 128 10  (fp8 e4m3 sum, config E shape)
        7 0 4 128 10   (fp32 sum, same bytes)
+  blocksPerCU / variant: nbxSetLaunchConfig (0 = default; variant 1 small
+  tiles, 2 big tiles) for launch-shape A/B in separate processes.
 """
 import json
 import os
@@ -19,10 +21,13 @@ sys.path.insert(0, ROOT)
 
 def main():
     dt, redop, esz, mib, iters = (int(v) for v in sys.argv[1:6])
+    bpc, variant = (int(sys.argv[6]), int(sys.argv[7])) if len(sys.argv) > 7 else (0, 0)
     import torch
     from __graft_entry__ import _load_package
     nbx = _load_package()
-    nbx.load_library()
+    lib = nbx.load_library()
+    if lib.nbxSetLaunchConfig(bpc, variant) != 0:
+        raise SystemExit("bad launch config")
     torch.cuda.set_device(0)
     st = torch.cuda.current_stream()
     n = (mib << 20) // esz
@@ -52,6 +57,7 @@ def main():
     ms = e0.elapsed_time(e1) / iters
     alg = 9 * (mib << 20)
     print(json.dumps({"datatype": dt, "redop": redop, "MiB_per_input": mib, "n_srcs": 8, "launches": iters + 2,
+                      "blocks_per_cu": bpc, "variant": variant,
                       "ms": round(ms, 5), "alg_bytes": alg, "TBps": round(alg / (ms * 1e-3) / 1e12, 3)}), flush=True)
 
 

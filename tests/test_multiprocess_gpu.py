@@ -1375,3 +1375,66 @@ def test_multiprocess_comm_churn_verified_mappings(nbx, monkeypatch):
     for r in range(n):
         assert res[r]["wrong"] == [] and res[r]["exact"] == 3 * k, (r, res[r])
     print("re-exported connection buffers over", k, "communicators:", [res[r]["repairs"] for r in range(n)])
+
+
+def _child_abort_pending_init(uid_bytes, rank, q, evq):
+    """Rank 0 initialises non-blocking with the LL128 creation probe forced on,
+    rank 1 skips the probe (NBX_LL128_SELFTEST_ITERS=0), so rank 0's
+    background initialisation ends up in a probe kernel waiting for lines rank 1
+    never sends; ncclCommAbort must end that device wait (the communicator's
+    abort word is set before the init thread is joined) instead of waiting out
+    NBX_TIMEOUT_SEC."""
+    try:
+        import os
+        import time
+
+        import torch
+        from tests.conftest import load_package
+        os.environ["NBX_LL128_SELFTEST_ITERS"] = "8" if rank == 0 else "0"
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        uid = nbx.ncclUniqueId.from_buffer_copy(uid_bytes)
+        if rank == 1:
+            comm = nbx.Communicator.init_rank(2, uid, 1)
+            evq.get(timeout=240)   # rank 0 has aborted
+            comm.destroy()
+            q.put((rank, "ok", None))
+            return
+        comm, rc = nbx.Communicator.init_rank_config(2, uid, 0, blocking=0)
+        assert rc == int(nbx.ncclResult.ncclInProgress), rc
+        time.sleep(6.0)   # connection setup done; the probe's first kernel is waiting on rank 1
+        pending = comm.async_error()
+        t0 = time.perf_counter()
+        comm.abort()
+        dt = time.perf_counter() - t0
+        evq.put("done")
+        q.put((rank, "ok", {"pending": pending, "abort_s": dt}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_abort_ends_pending_init_device_wait(nbx, monkeypatch):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "120")
+    ctx = mp.get_context("spawn")
+    uid = nbx.get_unique_id()
+    q, evq = ctx.Queue(), ctx.Queue()
+    procs = [ctx.Process(target=_child_abort_pending_init, args=(bytes(uid), r, q, evq), daemon=True)
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            rank, status, payload = q.get(timeout=280)
+            assert status == "ok", f"rank {rank}:\n{payload}"
+            res[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+    assert res[0]["pending"] == int(nbx.ncclResult.ncclInProgress), res[0]   # still initialising
+    assert res[0]["abort_s"] < 20, res[0]                                      # not the 120 s timeout
