@@ -344,9 +344,9 @@ def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 4
             alg = S / (ms * 1e-3) / 1e9
             res[name] = {"ms": round(ms, 4), "algbw_GBs": round(alg, 2), "busbw_GBs": round(alg * fac, 2)}
     res["workload"] = ("config D through ncclCommInitAll (one process, every GPU of the run, no IPC), "
-                       "ncclSum fp32 1 GiB per rank, checked exactly; allreduce / reduce_scatter with the clique's "
-                       "defaults (distinct GPUs: the in-kernel Simple transport over staging), fold_* on the "
-                       "event-ordered direct fold (NBX_CLIQUE_SIMPLE=0)")
+                       "ncclSum fp32 1 GiB per rank, checked exactly; allreduce / reduce_scatter on the in-kernel Simple transport over staging "
+                       "(forced for every size), fold_* on the event-ordered direct fold (NBX_CLIQUE_SIMPLE=0; the "
+                       "clique's default above NBX_CLIQUE_SIMPLE_MAX_BYTES = 32 MiB)")
     return res
 
 

@@ -200,7 +200,8 @@ struct PendingColl {
 struct Clique {
   int n = 0;
   bool ll = false;       // LL / LL128-sized calls run in-kernel (every rank has comm->lt)
-  bool simple = false;   // and Simple-sized calls too (every rank's lt has Simple staging)
+  bool simple = false;   // and Simple-sized calls too (every rank's lt has Simple staging) ...
+  uint64_t simpleMaxBytes = 0;   // ... up to this many bytes per rank's send buffer (NBX_CLIQUE_SIMPLE_MAX_BYTES)
   std::vector<ncclComm*> comms;
   std::vector<int> devs;
   std::vector<hipEvent_t> evEnter, evReduced, evDone;   // one per rank
@@ -1860,6 +1861,11 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
   }
   cl->ll = true;
   cl->simple = simple;
+  // above this the direct fold (peers' buffers read in place, no staging copy)
+  // keeps large messages: on one GPU it wins from 64 MiB (the staging design
+  // moves twice the HBM bytes there) and loses up to 16 MiB to the
+  // event exchange; the xGMI crossover is for the first multi-GPU run to set
+  cl->simpleMaxBytes = (uint64_t)envLong("NBX_CLIQUE_SIMPLE_MAX_BYTES", 32 << 20);
   info("clique of %d ranks: LL / LL128%s-sized calls run in-kernel (grid caps %u / %u)", n,
        simple ? " / Simple" : "", cl->comms[0]->lt->llGridCap, cl->comms[0]->lt->l128GridCap);
   return ncclSuccess;
@@ -1875,7 +1881,11 @@ bool cliqueInKernel(Clique* c, const std::vector<PendingColl>& parts) {
     for (int j = 0; j < r; j++)
       if (parts[j].stream == parts[r].stream) return false;   // one rank's kernel would queue behind another's
   }
-  return c->simple || mpProtoOf(c->comms[0], parts[0]) != kMpSimple;
+  if (mpProtoOf(c->comms[0], parts[0]) != kMpSimple) return true;
+  const PendingColl& p0 = parts[0];
+  const uint64_t sendBytes =
+      (uint64_t)p0.count * (uint64_t)typeSize(p0.dt) * (p0.kind == kReduceScatter ? (uint64_t)c->n : 1u);
+  return c->simple && sendBytes <= c->simpleMaxBytes;
 }
 
 // Consecutive in-kernel collectives [lo, hi): every rank runs them as a group

@@ -13,11 +13,13 @@ Spawned by bench.py rank 0 before it touches the GPU, idle until told:
 Inputs are small integers in fp32 (x_r[i] = (7 i + 13 r) mod 1024), so every
 fold order gives the exact sum and every rank's whole output is checked.
 Then 4 KiB / 64 KiB / 1 MiB AllReduces (the in-kernel LL / LL128 transport when
-the devices are distinct), each checked and timed per call. Config D runs with
-the clique's defaults (distinct devices: Simple sizes in-kernel over staging),
-then again on a second clique with NBX_CLIQUE_SIMPLE=0 (the event-ordered
-direct fold that reads peers' buffers in place) — `fold_*` — so the driver's
-multi-GPU run measures both data paths over xGMI.
+the devices are distinct), each checked and timed per call. Config D runs in-kernel
+(distinct devices: the Simple kernels over staging, forced for every size with
+NBX_CLIQUE_SIMPLE_MAX_BYTES), then again on a second clique with
+NBX_CLIQUE_SIMPLE=0 (the event-ordered direct fold that reads peers' buffers in
+place) — `fold_*` — so the driver's multi-GPU run measures both data paths
+over xGMI (the clique's default switches from the first to the second above
+32 MiB).
 """
 from __future__ import annotations
 
@@ -45,7 +47,13 @@ def run(n: int, devs: list, count: int = COUNT) -> dict:
     lib = nbx.load_library()
     F32, SUM = 7, 0
     res = {"ok": True, "errors": [], "n_ranks": n, "devices": devs}
-    comms = nbx.Communicator.init_all(devs)
+    # config D in-kernel whatever its size (the default hands messages above
+    # NBX_CLIQUE_SIMPLE_MAX_BYTES to the fold), then on the fold below
+    os.environ["NBX_CLIQUE_SIMPLE_MAX_BYTES"] = str(1 << 62)
+    try:
+        comms = nbx.Communicator.init_all(devs)
+    finally:
+        os.environ.pop("NBX_CLIQUE_SIMPLE_MAX_BYTES", None)
     vals = (ctypes.c_int64 * 9)()
     res["simple_in_kernel"] = lib.nbxDebugCommSettings(comms[0].handle, vals, 9) == 9 and vals[4] > 0
     xs, ys, rs, streams, exps = [], [], [], [], []

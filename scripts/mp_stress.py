@@ -10,7 +10,8 @@ third of the calls repeat the previous call's kind / type / op so such runs
 occur) — issues it without host
 synchronisation, then checks every output exactly against torch on the GPU
 (small-integer inputs, so every fold order gives the same value; every rank
-regenerates every rank's input from the seed). Reports one JSON line per rank
+regenerates every rank's input from the seed). Some AllReduces read the
+previous AllReduce's output (same stream): a group run must be cut there. Reports one JSON line per rank
 count: iterations, calls, mismatches, first errors.
 usage: mp_stress.py [ranks list, default 2,3] [iterations, default 40] [seed]
 """
@@ -43,8 +44,16 @@ def plan(rng, n):
         count = rng.choice(SIZES)
         if tname in ("float16", "bfloat16") and op == 0:
             count = min(count, 40000)
+        dep = False
+        if (calls and calls[-1]["kind"] == "allreduce" and kind == "allreduce" and dt == calls[-1]["dt"] and
+                op == calls[-1]["op"] and (op in (2, 3) or tname in ("float32", "int32", "int64")) and
+                rng.random() < 0.5):
+            # reads the previous call's output: a run must be cut before it
+            dep, count = True, calls[-1]["count"]
         calls.append({"kind": kind, "dt": dt, "t": tname, "op": op, "count": count, "stream": rng.randint(0, 1),
-                      "root": root, "group": rng.random() < 0.5})
+                      "root": root, "group": rng.random() < 0.5, "dep": dep})
+        if dep:   # same stream as the call it reads (a caller orders its own streams)
+            calls[-1]["stream"] = calls[-2]["stream"]
     return calls
 
 
@@ -76,7 +85,7 @@ def rank_main(rank, n, iters, seed, uid, q):
             in_group = False
             torch.cuda.synchronize()
             for k, c in enumerate(calls):
-                x = _input(torch, c, rank, it, k, n, dev)
+                x = live[-1][3] if c.get("dep") else _input(torch, c, rank, it, k, n, dev)
                 y = torch.full((c["count"],), -3, device=dev, dtype=x.dtype)
                 torch.cuda.synchronize()
                 if c["group"] and not in_group:
@@ -97,12 +106,18 @@ def rank_main(rank, n, iters, seed, uid, q):
             if in_group:
                 nbx.group_end()
             torch.cuda.synchronize()
+            refs = []
             for k, c, _x, y in live:
                 ncalls += 1
-                xs = [_input(torch, c, r, it, k, n, dev) for r in range(n)]
-                st = torch.stack([t.to(torch.float64) for t in xs])
-                ref = st.sum(0) if c["op"] == 0 else (st.amax(0) if c["op"] == 2 else st.amin(0))
-                ref = ref.to(y.dtype)
+                if c.get("dep"):   # every rank's input is the previous call's (identical) output
+                    prev = refs[-1].to(torch.float64)
+                    ref = (prev * n if c["op"] == 0 else prev).to(y.dtype)
+                else:
+                    xs = [_input(torch, c, r, it, k, n, dev) for r in range(n)]
+                    st = torch.stack([t.to(torch.float64) for t in xs])
+                    ref = st.sum(0) if c["op"] == 0 else (st.amax(0) if c["op"] == 2 else st.amin(0))
+                    ref = ref.to(y.dtype)
+                refs.append(ref)
                 if c["kind"] == "reducescatter":
                     ref = ref[rank * c["count"]:(rank + 1) * c["count"]]
                 if c["kind"] == "reduce" and rank != c["root"]:
