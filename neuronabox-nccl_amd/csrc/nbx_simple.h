@@ -136,27 +136,27 @@ struct SimpleSpan {
   char* recv;
   uint64_t off, cnt, blockElts;
 };
+// `segs`: the launch's segment table, read through a pointer (into the
+// kernel-argument segment, or the fused rig's argument array) — never through
+// the by-value argument itself: a run-time index into that copies the whole
+// 824-byte argument block to scratch, and constant indices over 16 segments
+// load the table into SGPRs (3,600 SGPR spills in round 4's first build).
 template <class E>
-__device__ __forceinline__ SimpleSpan simpleSlice(const SimpleArgs& a, int b, uint64_t k, int g, int grid) {
+__device__ __forceinline__ SimpleSpan simpleSlice(const SimpleArgs& a, const SimpleSeg* segs, int b, uint64_t k,
+                                                  int g, int grid) {
   uint64_t v = k * (uint64_t)grid + (uint64_t)g;   // the launch's virtual slice of block b
   SimpleSpan sp{(const char*)a.send, (char*)a.recv, 0, 0, a.blockElts};
   uint64_t total = a.total;
   if (a.nSegs > 0) {
-    // the last segment starting at or before v (sliceOff ascending); constant
-    // indices only, so the table stays in the kernel-argument segment (a
-    // run-time index copies the whole argument block to scratch)
-    uint64_t base = 0;
-#pragma unroll
-    for (int q = 0; q < kSimpleMaxSegs; q++) {
-      if (q < a.nSegs && v >= a.seg[q].sliceOff) {
-        sp.send = (const char*)a.seg[q].send;
-        sp.recv = (char*)a.seg[q].recv;
-        sp.blockElts = a.seg[q].blockElts;
-        total = a.seg[q].total;
-        base = a.seg[q].sliceOff;
-      }
-    }
-    v -= base;
+    int s = 0;   // the last segment starting at or before v (sliceOff ascending)
+    for (int q = 1; q < a.nSegs; q++)
+      if (v >= segs[q].sliceOff) s = q;
+    const SimpleSeg sg = segs[s];
+    sp.send = (const char*)sg.send;
+    sp.recv = (char*)sg.recv;
+    sp.blockElts = sg.blockElts;
+    total = sg.total;
+    v -= sg.sliceOff;
   }
   uint64_t lo = (uint64_t)b * sp.blockElts;
   if (lo > total) lo = total;
@@ -334,7 +334,7 @@ __device__ __forceinline__ void simpleStoreCounters(const SimpleArgs& a, SimpleS
 // (kSimpleColl: the launch's own block index; kSimpleCollFused: one launch
 // running every rank of a one-process rig, for the PMC passes).
 template <class Fn>
-__device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, int g, int grid) {
+__device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const SimpleSeg* segs, int g, int grid) {
   using E = typename Fn::Elt;
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
   const int n = a.nRanks, me = a.rank, gm = a.gridMax, tid = (int)threadIdx.x;
@@ -360,7 +360,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, int g, int g
     if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
-      const SimpleSpan sp = simpleSlice<E>(a, j, k, g, grid);
+      const SimpleSpan sp = simpleSlice<E>(a, segs, j, k, g, grid);
       if (sp.cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
                                 sp.send + sp.off * sizeof(E), false, sp.cnt);
     }
@@ -380,7 +380,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, int g, int g
           !simpleWait(simpleFlag(myFlags, kFlAgCredit, n, tid, gm, g), sent + 1 - slots, a, tid, kDiagSimpleAgCredit))
         sh.fail = 1;
     }
-    const SimpleSpan sp = simpleSlice<E>(a, me, k, g, grid);
+    const SimpleSpan sp = simpleSlice<E>(a, segs, me, k, g, grid);
     const uint64_t off = sp.off, cnt = sp.cnt;
     // the output holds the whole message, except ReduceScatter's: block `me` only
     const uint64_t outOff = rs ? off - (uint64_t)me * sp.blockElts : off;
@@ -425,7 +425,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, int g, int g
     if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
-      const SimpleSpan sp = simpleSlice<E>(a, j, k, g, grid);
+      const SimpleSpan sp = simpleSlice<E>(a, segs, j, k, g, grid);
       if (sp.cnt) simpleCopy<E>(sp.recv + sp.off * sizeof(E), false, nullptr, false,
                                 simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, sp.cnt);
     }
@@ -454,9 +454,15 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, int g, int g
   mpArrive(a.order);
 }
 
+// The segment table of the launch's own kernel arguments (SimpleArgs is the
+// kernel's only parameter, at offset 0 of the kernel-argument segment).
+__device__ __forceinline__ const SimpleSeg* simpleKernargSegs() {
+  return (const SimpleSeg*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(SimpleArgs, seg));
+}
+
 template <class Fn>
 __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
-  simpleCollBody<Fn>(a, (int)blockIdx.x, (int)gridDim.x);
+  simpleCollBody<Fn>(a, simpleKernargSegs(), (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Ring schedule through the right neighbour's staging. AllReduce /
@@ -465,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
 // the ring (all_reduce.h:60-93). Reduce: the chain root+1 -> ... -> root over
 // the one block of the message (reduce.h:44-67).
 template <class Fn>
-__device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int grid) {
+__device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const SimpleSeg* segs, int g, int grid) {
   using E = typename Fn::Elt;
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
   const int n = a.nRanks, me = a.rank, gm = a.gridMax, tid = (int)threadIdx.x;
@@ -511,7 +517,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int g
     if (red) {
       // chain position: 0 = root+1 (sends its raw input), n-1 = the root
       const int pos = (me - a.root - 1 + 2 * n) % n;
-      const SimpleSpan sp = simpleSlice<E>(a, 0, k, g, grid);
+      const SimpleSpan sp = simpleSlice<E>(a, segs, 0, k, g, grid);
       const uint64_t off = sp.off, cnt = sp.cnt;
       const bool push = pos < n - 1;
       if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
@@ -534,7 +540,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int g
     }
     // send step: the raw chunk me-1 into the right neighbour's RS region
     {
-      const SimpleSpan sp = simpleSlice<E>(a, left, k, g, grid);
+      const SimpleSpan sp = simpleSlice<E>(a, segs, left, k, g, grid);
       if (!hopWait(-1, true, false)) return;
       if (sp.cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr,
                                 false, sp.send + sp.off * sizeof(E), false, sp.cnt);
@@ -545,7 +551,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int g
     for (int st = 0; st < n - 1; st++) {
       const int c = (me + 2 * n - 2 - st) % n;
       const bool last = st == n - 2;
-      const SimpleSpan sp = simpleSlice<E>(a, c, k, g, grid);
+      const SimpleSpan sp = simpleSlice<E>(a, segs, c, k, g, grid);
       const uint64_t off = sp.off, cnt = sp.cnt;
       if (!hopWait(0, !last, last && ar)) return;
       if (tid == 0) {
@@ -571,7 +577,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int g
     for (int st = 0; st < n - 1; st++) {
       const int c = (me + 2 * n - 1 - st) % n;
       const bool fwd = st < n - 2;
-      const SimpleSpan sp = simpleSlice<E>(a, c, k, g, grid);
+      const SimpleSpan sp = simpleSlice<E>(a, segs, c, k, g, grid);
       if (!hopWait(1, false, fwd)) return;
       if (sp.cnt)
         simpleCopy<E>(sp.recv + sp.off * sizeof(E), false,
@@ -587,7 +593,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, int g, int g
 
 template <class Fn>
 __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
-  simpleRingBody<Fn>(a, (int)blockIdx.x, (int)gridDim.x);
+  simpleRingBody<Fn>(a, simpleKernargSegs(), (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Every rank of a one-process rig in ONE launch (workgroup b runs rank
@@ -598,8 +604,8 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
 template <class Fn, bool RING>
 __global__ __launch_bounds__(kBlock) void kSimpleFused(const SimpleArgs* __restrict__ as, int grid) {
   const int r = (int)blockIdx.x / grid, g = (int)blockIdx.x % grid;
-  if (RING) simpleRingBody<Fn>(as[r], g, grid);
-  else simpleCollBody<Fn>(as[r], g, grid);
+  if (RING) simpleRingBody<Fn>(as[r], as[r].seg, g, grid);
+  else simpleCollBody<Fn>(as[r], as[r].seg, g, grid);
 }
 
 }  // namespace nbx

@@ -29,9 +29,9 @@ def _kernels(so_path, tmp):
         if r.returncode != 0 or not os.path.exists(e) or os.path.getsize(e) == 0:
             continue
         notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", e], capture_output=True, text=True).stdout
-        for m in re.finditer(r"\.name:\s+(\S+).*?\.private_segment_fixed_size:\s+(\d+).*?\.vgpr_count:\s+(\d+)",
-                             notes, re.S):
-            out.append((m.group(1), int(m.group(2)), int(m.group(3))))
+        for m in re.finditer(r"\.name:\s+(\S+).*?\.private_segment_fixed_size:\s+(\d+).*?\.sgpr_spill_count:\s+(\d+)"
+                             r".*?\.vgpr_count:\s+(\d+)", notes, re.S):
+            out.append((m.group(1), int(m.group(2)), int(m.group(4)), int(m.group(3))))
     return out
 
 
@@ -44,6 +44,7 @@ def kernels(nbx, tmp_path_factory):
 
 def test_all_kernels_present(kernels):
     names = [k[0] for k in kernels]
+    assert len(names) >= 42 * 47
     packs = [n for n in names if "kReducePacks" in n]
     elts = [n for n in names if "kReduceElts" in n]
     assert len(elts) == 42                 # one element kernel per distinct functor
@@ -55,9 +56,19 @@ def test_all_kernels_present(kernels):
 
 
 def test_no_scratch_and_vgpr_budget(kernels):
-    spills = [(n, p) for n, p, v in kernels if p > 0]
+    spills = [(n, p) for n, p, v, _ in kernels if p > 0]
     assert not spills, spills[:5]
-    assert max(v for _, _, v in kernels) <= 512
+    assert max(v for _, _, v, _ in kernels) <= 512
     # the config-B kernel keeps ~32 dwordx4 loads in flight in registers
-    k8 = [v for n, p, v in kernels if n == "_ZN3nbx12kReducePacksINS_6FnSumFINS_5TyF32EEELi8ELi4EEEvNS_5KArgsE"]
+    k8 = [v for n, p, v, _ in kernels if n == "_ZN3nbx12kReducePacksINS_6FnSumFINS_5TyF32EEELi8ELi4EEEvNS_5KArgsE"]
     assert k8 and 128 <= k8[0] <= 256
+
+
+def test_simple_kernels_sgpr_spills_bounded(kernels):
+    """The Simple collectives read their segment table through a pointer;
+    touching it through the by-value argument loaded it into SGPRs and spilled
+    them to VGPR lanes (~3,600 v_readlane per kernel, +5 us per call). Some
+    SGPR spilling is the compiler's normal state for these kernels (round 3:
+    at most 198 per kernel, mean 120; now at most 193, mean 102)."""
+    spilled = [(n, s) for n, _, _, s in kernels if ("kSimpleColl" in n or "kSimpleRing" in n) and s > 256]
+    assert not spilled, spilled[:5]
