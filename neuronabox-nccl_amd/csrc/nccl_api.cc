@@ -913,16 +913,17 @@ long ncclEnvMapped(const char* nbxName, const char* ncclName, long dflt, long nu
 // and its IPC handle taken at once.
 // The runtime rule behind the retry (scripts/probe_ipc_export.py: N processes
 // replaying communicator creation / destruction with the library's buffer
-// sizes, raw HIP, no libnbxccl; profiles/r4/probe_ipc_export_r4.jsonl):
-// hipIpcGetMemHandle refuses ('invalid argument') a new allocation placed at a
-// virtual address where an earlier allocation of the same process was
-// exported and then freed — 0-7 of 4,800 exports per run, every refusal at
-// such an address, the same pointer refused again on retry, a fresh
-// allocation (the refused one still held, so at another address) accepted
-// every time. So a refused allocation is held aside while the next one is
-// made (at most 4 tries), then freed. The same runtime condition also makes
-// a successful export name the wrong memory now and then (mpConnect, which
-// verifies every mapping and re-exports what is wrong).
+// sizes, raw HIP, no libnbxccl; profiles/r4/probe_ipc_export_r4*.jsonl):
+// once exported allocations are freed, hipIpcGetMemHandle now and then refuses
+// ('invalid argument') a new allocation — 25 of 62,400 exports, 20 of them at
+// an address whose earlier allocation had been exported and freed; the same
+// pointer was refused again on an immediate retry 23 times of 25, and a fresh
+// allocation (the refused one still held, so at another address) was
+// accepted 23 times of 23. With exported buffers never freed: 0 of 19,200. So
+// a refused allocation is held aside while the next one is made (at most 4
+// tries), then freed. The same runtime condition also makes a successful
+// export name the wrong memory now and then (mpConnect, which verifies every
+// mapping and re-exports what is wrong).
 hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle /* nullptr: in-process only */) {
   static const bool coarse = [] {
     const char* v = std::getenv("NBX_SYNC_MEM");
@@ -1046,11 +1047,12 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
 // on one GPU replaying communicator creation / destruction with this
 // library's buffer sizes and memory kinds) found IPC mappings that do not
 // show the exported allocation — an importer reads zeros or ANOTHER rank's
-// buffer through it, and its stores never reach the owner — in 12-20 of
-// 4,800 imports per run (uncached, 2 MiB-rounded: the library's buffers), the
-// same wrong bytes seen by every importer of that handle (so it is the
-// export, not one importer's mapping, that is wrong), at owner addresses that
-// an earlier, freed allocation of the owner had been exported from. Round 2's
+// buffer through it (89 canary reads), and its stores never reach the owner
+// (164), out of 62,400 imports, in the library's own memory kind as in plain
+// hipMalloc memory; the same wrong bytes are seen by every importer of that
+// handle (so it is the export, not one importer's mapping, that is wrong),
+// mostly at owner addresses that an earlier, freed allocation of the owner
+// had been exported from; with exported buffers never freed, none. Round 2's
 // wrong results (peers reading stale bytes through a mapping of a freshly
 // allocated buffer, their stores lost) are the same failure.
 // Check, per buffer and round (each with a fresh per-communicator nonce):
