@@ -28,6 +28,7 @@ enum DiagSite : uint64_t {
   kDiagSimpleAg = 10,    // Simple: a peer's AG-region slice (agReady)
   kDiagSimpleAgCredit = 11,  // Simple: a peer's credit for this rank's AG slot (agCredit)
   kDiagOrder = 12,       // a call on another stream: the previous call's done word (kMpWaitDone)
+  kDiagSimplePlan = 13,  // Simple: a peer's slice was cut by another plan (mismatched calls or group runs)
 };
 constexpr int kDiagWords = 6;
 constexpr int kDiagByteOffset = 16;   // from the start of the host words
@@ -46,6 +47,7 @@ inline const char* diagSiteName(uint64_t s) {
     case kDiagSimpleAg: return "Simple all-gather slice (peer's ready word)";
     case kDiagSimpleAgCredit: return "Simple all-gather slot credit";
     case kDiagOrder: return "previous call's completion (stream switch)";
+    case kDiagSimplePlan: return "Simple slice from a peer running a different plan (mismatched call or group cut)";
     default: return "unknown";
   }
 }

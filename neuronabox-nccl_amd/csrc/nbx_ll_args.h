@@ -96,6 +96,8 @@ struct LLArgs {
 // own user buffers and staging; peer traffic is stores into the peer's
 // staging plus flag words (waitPeer / postPeer of prims_simple.h:129-185).
 //   staging  [region 2: RS | AG][slot][source rank n][workgroup gridMax][stageSlice bytes]
+//            then, at hdrOff, one 16-byte plan header per slice cell in the same order
+//            ({plan signature, round}: written with the slice, checked by the consumer)
 //   flags    [kind 4][peer n][workgroup gridMax] u64      (written by the peer)
 //   counters [kind 4][peer n][workgroup gridMax] u64      (this rank's, device-resident)
 // Counter / flag kinds per (ordered pair, workgroup), monotonic over the
@@ -146,6 +148,8 @@ struct SimpleArgs {
   const volatile int* abortWord;
   volatile int* errWord;
   uint64_t timeoutTicks;
+  uint64_t planSig;            // simplePlanSig: the same on every rank iff the ranks cut the call alike
+  uint64_t hdrOff;             // byte offset of the plan headers in every rank's staging
   int32_t rank;
   int32_t nRanks;
   int32_t mode;                // SimpleMode
@@ -157,5 +161,39 @@ struct SimpleArgs {
   MpDone order;
   SimpleSeg seg[kSimpleMaxSegs];
 };
+
+// A launch's plan: everything that decides which elements go into which
+// staging slice in which round (never a pointer, never the rank), hashed
+// (FNV-1a). Ranks whose calls or group cuts differ get different signatures;
+// a consumer that finds a slice stamped with another signature fails the
+// launch (kDiagSimplePlan) instead of folding misplaced data.
+inline uint64_t simplePlanSig(const SimpleArgs& a, uint32_t grid, int32_t dtype, int32_t op) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&h](uint64_t v) {
+    for (int b = 0; b < 8; b++) {
+      h ^= (v >> (8 * b)) & 0xffu;
+      h *= 0x100000001b3ull;
+    }
+  };
+  mix((uint64_t)a.mode);
+  mix((uint64_t)(uint32_t)a.root);
+  mix((uint64_t)a.nRanks);
+  mix((uint64_t)(uint32_t)dtype);
+  mix((uint64_t)(uint32_t)op);
+  mix(grid);
+  mix(a.sliceBytes);
+  mix(a.nRounds);
+  mix((uint64_t)a.nSegs);
+  if (a.nSegs == 0) {
+    mix(a.total);
+    mix(a.blockElts);
+  }
+  for (int s = 0; s < a.nSegs; s++) {
+    mix(a.seg[s].total);
+    mix(a.seg[s].blockElts);
+    mix(a.seg[s].sliceOff);
+  }
+  return h | 1u;   // never 0: zeroed staging never matches
+}
 
 }  // namespace nbx

@@ -64,7 +64,8 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugSimpleRun(
   Rig rig;
   rig.n = n;
   const uint64_t cells = (uint64_t)n * (uint64_t)gridMax;
-  const uint64_t stageBytes = 2ull * (uint64_t)slots * cells * sliceBytes;
+  const uint64_t hdrOff = 2ull * (uint64_t)slots * cells * sliceBytes;   // then the plan headers (nbx_simple.h)
+  const uint64_t stageBytes = hdrOff + 2ull * (uint64_t)slots * cells * 16u;
   for (int r = 0; r < n; r++) {
     void *s = nullptr, *f = nullptr, *c = nullptr;
     if (hipExtMallocWithFlags(&s, stageBytes, hipDeviceMallocUncached) != hipSuccess ||
@@ -135,6 +136,8 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugSimpleRun(
     sa.slots = slots;
     sa.gridMax = gridMax;
     sa.prefetch = prefetch;
+    sa.hdrOff = hdrOff;
+    sa.planSig = nbx::simplePlanSig(sa, (uint32_t)grid, datatype, opFull.op);
   }
   // NBX_DEBUG_SIMPLE_FUSED=1: every rank's workgroups in ONE dispatch (fp32
   // sum), so a rocprofv3 PMC pass (which serializes dispatches) can count the

@@ -744,6 +744,7 @@ struct MpState {
   char* stage = nullptr;
   uint64_t stageBytes = 0;
   uint64_t llBytes = 0, sflagsBytes = 0;   // used bytes of the LL buffer and the Simple flag words
+  uint64_t stageHdrOff = 0;         // the Simple plan headers' offset in the staging (after the slices)
   int ipcRepairs = 0;               // connection buffers re-exported at init because a mapping was wrong (mpConnect)
   uint64_t* sflags = nullptr;
   uint64_t* scounters = nullptr;
@@ -1100,7 +1101,9 @@ void mpTransportSettings(MpState* mp, int minCus, int maxShare) {
 // `ipc`, with the check region mpConnect uses) and its counters.
 ncclResult_t mpAllocSimple(MpState* mp, int n, bool ipc) {
   const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
-  mp->stageBytes = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
+  // slices, then one 16-byte plan header per slice cell (nbx_simple.h simpleHdr)
+  mp->stageHdrOff = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
+  mp->stageBytes = mp->stageHdrOff + 2ull * (uint64_t)mp->slots * cells * 16u;
   HIPCHECK(allocSyncMem((void**)&mp->stage, connAllocBytes(mp->stageBytes, n), ipc ? &mp->stageHandle : nullptr));
   HIPCHECK(hipMemset(mp->stage, 0, connAllocBytes(mp->stageBytes, n)));
   mp->sflagsBytes = 4 * cells * sizeof(uint64_t);
@@ -1527,6 +1530,8 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc) {
   sa.slots = mp->slots;
   sa.gridMax = mp->simpleGrid;
   sa.prefetch = mp->simplePrefetch;
+  sa.hdrOff = mp->stageHdrOff;
+  sa.planSig = nbx::simplePlanSig(sa, (uint32_t)grid, (int32_t)c.dt, c.op.op);
   sa.order = mpOrderArgs(mp);
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
 }

@@ -1438,3 +1438,54 @@ def test_multiprocess_abort_ends_pending_init_device_wait(nbx, monkeypatch):
                 p.terminate()
     assert res[0]["pending"] == int(nbx.ncclResult.ncclInProgress), res[0]   # still initialising
     assert res[0]["abort_s"] < 20, res[0]                                      # not the 120 s timeout
+
+
+def _child_plan_mismatch(uid_bytes, rank, n, q, case):
+    """Ranks whose Simple launches are cut from different plans: every slice
+    carries its producer's plan signature, so the consumer fails the launch
+    (ncclRemoteError, the wait named "... different plan ...") instead of
+    folding misplaced data. case "count": the ranks pass different counts;
+    case "group": rank 0's group reads what its previous call wrote (cut into
+    two launches), rank 1's calls are independent (one launch)."""
+    try:
+        import ctypes
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        cnt = 300000
+        a = torch.ones(cnt + 8, device="cuda")
+        b = torch.zeros(cnt + 8, device="cuda")
+        c = torch.zeros(cnt + 8, device="cuda")
+        d = torch.ones(cnt + 8, device="cuda")
+        if case == "count":
+            comm.all_reduce(a.data_ptr(), b.data_ptr(), cnt + (3 if rank == 1 else 0), 7, 0, st)
+        else:
+            nbx.group_start()
+            comm.all_reduce(a.data_ptr(), b.data_ptr(), cnt, 7, 0, st)
+            comm.all_reduce((b if rank == 0 else d).data_ptr(), c.data_ptr(), cnt, 7, 0, st)
+            nbx.group_end()
+        torch.cuda.synchronize()
+        err = comm.async_error()
+        msg = (lib.ncclGetLastError(None) or b"").decode(errors="replace")
+        comm.abort()
+        q.put((rank, "ok", {"err": err, "msg": msg}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("case", ["count", "group"])
+def test_multiprocess_simple_plan_mismatch_fails_loudly(nbx, monkeypatch, case):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "5")
+    monkeypatch.setenv("NCCL_PROTO", "Simple")
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")
+    res = _run_ranks(nbx, 2, _child_plan_mismatch, case)
+    remote = int(nbx.ncclResult.ncclRemoteError)
+    assert all(res[r]["err"] == remote for r in range(2)), res
+    assert any("different plan" in res[r]["msg"] for r in range(2)), res
