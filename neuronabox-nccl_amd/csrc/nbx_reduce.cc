@@ -312,6 +312,15 @@ ncclResult_t launchPass(const KernelSet& ks, void* const* dsts, int nDsts, const
     static const bool envPerCU = envInt("NBX_BLOCKS_PER_CU", 0) > 0;
     if (big && !envPerCU && g_maxBlocksPerCU.load(std::memory_order_relaxed) == 0 && perCU < ks.bigBlocksPerCU)
       perCU = ks.bigBlocksPerCU;   // VALU-heavy functors: a second wave per SIMD
+    // Few big tiles per CU (config C's mid-size buckets): one tile per
+    // workgroup, up to NBX_MID_BLOCKS_PER_CU workgroups per CU, so every tile's
+    // loads are in flight at once instead of a workgroup's second tile waiting
+    // for its first tile's fold (scripts/steps/r4-o.txt, r4-p.txt)
+    static const int midPerCU = envInt("NBX_MID_BLOCKS_PER_CU", 4);
+    if (big && !envPerCU && g_maxBlocksPerCU.load(std::memory_order_relaxed) == 0 && midPerCU > 1) {
+      const size_t need = (tiles + (size_t)cus - 1) / (size_t)cus;
+      if (need > (size_t)perCU && need <= (size_t)midPerCU) perCU = (int)need;
+    }
     const size_t maxBlocks = (size_t)cus * (size_t)perCU;
     size_t grid = tiles < maxBlocks ? tiles : maxBlocks;
     if (grid == 0) grid = 1;
