@@ -8,7 +8,8 @@
 // so a timeout names the wait, the peer and how far it got (NCCL prints the
 // equivalent from its proxy / abort path, init.cc:2016, prims_simple.h:103-113).
 // Several waves may time out together; the record is the last writer's (the
-// site word is written last, after the fields).
+// site word is written last, after the fields), except that a failed plan
+// check is never replaced by a timeout.
 #pragma once
 #include <stdint.h>
 
@@ -29,9 +30,14 @@ enum DiagSite : uint64_t {
   kDiagSimpleAgCredit = 11,  // Simple: a peer's credit for this rank's AG slot (agCredit)
   kDiagOrder = 12,       // a call on another stream: the previous call's done word (kMpWaitDone)
   kDiagSimplePlan = 13,  // Simple: a peer's slice was cut by another plan (mismatched calls or group runs)
+  kDiagLLPlan = 14,      // LL family: a peer at the same call runs another plan
+  kDiagLLPlanWord = 15,  // LL family: a peer's plan word for this call (its lines had arrived)
 };
 constexpr int kDiagWords = 6;
 constexpr int kDiagByteOffset = 16;   // from the start of the host words
+
+// a site that records a failed consistency check, not a wait that gave up
+constexpr bool diagIsPlanCheck(uint64_t s) { return s == kDiagSimplePlan || s == kDiagLLPlan; }
 
 inline const char* diagSiteName(uint64_t s) {
   switch (s) {
@@ -48,6 +54,8 @@ inline const char* diagSiteName(uint64_t s) {
     case kDiagSimpleAgCredit: return "Simple all-gather slot credit";
     case kDiagOrder: return "previous call's completion (stream switch)";
     case kDiagSimplePlan: return "Simple slice from a peer running a different plan (mismatched call or group cut)";
+    case kDiagLLPlan: return "LL / LL128 lines from a peer running a different plan (mismatched call or group cut)";
+    case kDiagLLPlanWord: return "LL / LL128 plan word of a peer";
     default: return "unknown";
   }
 }
@@ -57,6 +65,9 @@ inline const char* diagSiteName(uint64_t s) {
 __device__ __forceinline__ void diagTimeout(volatile int* errWord, uint64_t site, int peer, uint64_t target,
                                             uint64_t observed, uint64_t ticks) {
   volatile uint64_t* d = (volatile uint64_t*)((volatile char*)errWord - 4 + kDiagByteOffset);
+  // a failed plan check names the cause; a later call's wait that then times
+  // out (the peers have diverged) does not replace it
+  if (!diagIsPlanCheck(site) && diagIsPlanCheck(d[0])) return;
   d[1] = (uint64_t)(int64_t)peer;
   d[2] = target;
   d[3] = observed;

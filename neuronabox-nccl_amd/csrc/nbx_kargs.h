@@ -116,6 +116,9 @@ struct KernelSet {
   const void* ll;                   // LL-protocol collectives (nbx_ll.h)
   const void* ll128;                // LL128-protocol collectives (nbx_ll.h)
   const void* ll128x2;              // LL128 two-shot AllReduce (nbx_ll.h)
+  const void* llChk;                // the same three with plan words (NBX_CHECK_PLANS)
+  const void* ll128Chk;
+  const void* ll128x2Chk;
   const void* simple;               // Simple protocol, direct schedule over init-mapped staging (nbx_simple.h)
   const void* simpleRing;           // Simple protocol, ring schedule over init-mapped staging (nbx_simple.h)
   const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]

@@ -670,9 +670,12 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.shifted = (const void*)&kReduceShifted<Fn>;
   const void* sn[] = {shiftedNFor<Fn, I + 1>()...};
   for (int i = 0; i < kMaxKSrcs; i++) ks.shiftedN[i] = sn[i];
-  ks.ll = (const void*)&kLLColl<Fn>;
-  ks.ll128 = (const void*)&kLL128Coll<Fn>;
-  ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn>;
+  ks.ll = (const void*)&kLLColl<Fn, false>;
+  ks.ll128 = (const void*)&kLL128Coll<Fn, false>;
+  ks.ll128x2 = (const void*)&kLL128AllReduce2<Fn, false>;
+  ks.llChk = (const void*)&kLLColl<Fn, true>;
+  ks.ll128Chk = (const void*)&kLL128Coll<Fn, true>;
+  ks.ll128x2Chk = (const void*)&kLL128AllReduce2<Fn, true>;
   ks.simple = (const void*)&kSimpleColl<Fn>;
   ks.simpleRing = (const void*)&kSimpleRing<Fn>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);

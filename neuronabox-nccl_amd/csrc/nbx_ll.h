@@ -31,6 +31,16 @@
 //        Reduce (root)  — ranks root+1, ..., root (reduce.h:44-67);
 //   3. stores the result; the last block to finish publishes this rank's
 //      done word (= seq) into every peer's buffer and advances the state.
+// Plan words (when the communicator checks plans, NBX_CHECK_PLANS: the
+// kernels' CHECK instantiation, LLArgs.planSig != 0; the default instantiation
+// carries none of this code): [parity 2][source n] after the done words. Every source
+// stamps {plan signature, flag} into each target's buffer, performed before
+// its lines go out (llPlanStamp), so a receiver can tell a peer that runs the
+// same call with another plan (mismatched counts / types / ops, a group cut
+// differently) and fail the launch naming it (kDiagLLPlan) — instead of timing
+// out on lines the peer never writes (every stuck line wait reads the plan
+// word in its slow path), or folding lines it cut differently (block 0's
+// threads j compare peer j's word after the fold, llPlanCheck).
 #pragma once
 #include "nbx_diag.h"
 #include "nbx_order.h"
@@ -110,6 +120,55 @@ __device__ __forceinline__ LLCall llBegin(const LLArgs& a) {
   return c;
 }
 
+// Plan word of source `src` for `parity` in the LL buffer at `base`.
+__device__ __forceinline__ uint64_t* llPlanWord(uint64_t* const base, const LLArgs& a, int parity, int src) {
+  return base + a.planOff + (uint64_t)(parity * a.nRanks + src);
+}
+
+// Block 0, thread j: this call's plan into target j's buffer. Stamped BEFORE
+// j's credit wait and drained after it: the word is performed at
+// j's memory before this thread's unit goes out, at no added latency (the
+// credit poll's round trip covers the write). So it can reach j while j still
+// runs the call two back on this parity; j's checks take a newer flag as
+// "moved on" (llPlanAge), never as a mismatch.
+__device__ __forceinline__ void llPlanStamp(const LLArgs& a, const LLCall& c, int j) {
+  __hip_atomic_store(llPlanWord(a.peerLL[j], a, c.parity, a.rank), ((uint64_t)c.flag << 32) | a.planSig,
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// plan word flag vs this call's: < 0 older (not stamped yet), 0 this call, > 0 newer
+__device__ __forceinline__ int32_t llPlanAge(uint64_t h, uint32_t flag) { return (int32_t)((uint32_t)(h >> 32) - flag); }
+
+// Slow path of a wait on peer j's lines: true (and the launch's error recorded)
+// if j is at this call with another plan. `w`: j's plan word; nullptr: none.
+__device__ __forceinline__ bool llPlanMismatch(const LLArgs& a, const uint64_t* w, uint32_t flag, int j, uint64_t t0,
+                                               bool record = true) {
+  if (w == nullptr) return false;
+  const uint64_t h = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((uint32_t)(h >> 32) != flag || (uint32_t)h == a.planSig) return false;
+  if (record) diagTimeout(a.errWord, kDiagLLPlan, j, a.planSig, (uint32_t)h, wall_clock64() - t0);
+  *a.errWord = 1;
+  return true;
+}
+
+// Block 0, thread j (a source of this rank), after the fold: peer j's plan
+// word for this call (bounded wait; already there in the common case, since j
+// performed it before pushing) must carry this rank's signature.
+__device__ __forceinline__ bool llPlanCheck(const LLArgs& a, const LLCall& c, int j, uint64_t t0) {
+  const uint64_t* w = llPlanWord(a.myLL, a, c.parity, j);
+  uint32_t spins = 0;
+  for (;;) {
+    const uint64_t h = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int32_t age = llPlanAge(h, c.flag);
+    if (age > 0) return true;
+    if (age == 0) return !llPlanMismatch(a, w, c.flag, j, t0);
+    if ((++spins & 1023u) == 0u && llExpired(a, t0)) {
+      llGiveUp(a, kDiagLLPlanWord, j, c.flag, (uint32_t)(h >> 32), t0);
+      return false;
+    }
+  }
+}
+
 // Every thread of every block, as the launch's last statement: the block's
 // memory operations complete, thread 0 arrives (nbx_order.h, per-XCD
 // counters), and the launch's last block publishes this rank's done word
@@ -150,7 +209,7 @@ __device__ __forceinline__ LLMsg llMsg(const LLArgs& a, uint64_t k) {
   return LLMsg{(const unsigned char*)g.send, (unsigned char*)g.recv, g.count * sizeof(E), k - g.packOff, g.blockElts};
 }
 
-template <class Fn>
+template <class Fn, bool CHECK>
 __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   using E = typename Fn::Elt;
   constexpr int EPK = 8 / (int)sizeof(E);   // elements per 8-byte pack
@@ -164,10 +223,14 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
 
-  // 0. credits: each target has finished reading this parity's previous use
+  // 0. plan words (checks on: block 0's thread j for target j, performed before
+  // the lines go out), credits: each target has finished reading this parity's previous use
+  const bool stamps = CHECK && blockIdx.x == 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x);
+  if (stamps) llPlanStamp(a, call, threadIdx.x);
   if (call.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
     if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0, (int)threadIdx.x)) sFailed = 1;
   }
+  if (stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   bool failed = sFailed != 0;
 
@@ -214,15 +277,20 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
         x.u = llLoadBytes(own, m.k * 8, m.bytes);
       } else {
         const uint64_t* line = a.myLL + ((uint64_t)(call.parity * n + j) * a.slotLines + 2 * k);
+        const uint64_t* pw = CHECK ? llPlanWord(a.myLL, a, call.parity, j) : nullptr;
         uint64_t l0 = 0, l1 = 0;
         uint32_t spins = 0;
         while (!failed) {
           l0 = __hip_atomic_load(line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           l1 = __hip_atomic_load(line + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((uint32_t)(l0 >> 32) == call.flag && (uint32_t)(l1 >> 32) == call.flag) break;
-          if ((++spins & 1023u) == 0u && llExpired(a, t0)) {
-            llGiveUp(a, kDiagLLLine, j, call.flag, (uint32_t)(l0 >> 32), t0);
-            failed = true;
+          if ((++spins & 1023u) == 0u) {
+            if (llPlanMismatch(a, pw, call.flag, j, t0)) {
+              failed = true;
+            } else if (llExpired(a, t0)) {
+              llGiveUp(a, kDiagLLLine, j, call.flag, (uint32_t)(l0 >> 32), t0);
+              failed = true;
+            }
           }
         }
         x.u = (l0 & 0xffffffffull) | (l1 << 32);
@@ -242,6 +310,8 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
     }
     llStoreBytes(m.recv, m.k * 8, m.bytes, acc.u);
   }
+  if (CHECK && receives && !failed && blockIdx.x == 0 && (int)threadIdx.x < n && (int)threadIdx.x != me)
+    (void)llPlanCheck(a, call, threadIdx.x, t0);
 
   // done word: after every block of this launch has consumed its lines
   llEnd(a, call);
@@ -340,11 +410,13 @@ __device__ __forceinline__ uint32_t l128FlagOf(const u32x4 (&v)[kL128MaxRanks], 
 }
 
 // Poll the chunks of the sources in `need` (slot byte offset slotOff(q)) until
-// every chunk of the line shows `flag`; false if the wait gave up.
+// every chunk of the line shows `flag`; false if the wait gave up, or if the
+// source's plan word (`plan` + q, or `plan` itself for a fixed `planPeer` >= 0;
+// nullptr: none) shows this call with another plan.
 template <class SlotOff>
 __device__ __forceinline__ bool l128Poll(const LLArgs& a, __amdgpu_buffer_rsrc_t rs, u32x4 (&v)[kL128MaxRanks],
                                          uint32_t need, uint32_t flag, uint64_t site, uint64_t t0, int t,
-                                         SlotOff slotOff) {
+                                         SlotOff slotOff, const uint64_t* plan, int planPeer) {
   uint32_t spins = 0;
   while (need != 0) {
 #pragma unroll
@@ -355,10 +427,14 @@ __device__ __forceinline__ bool l128Poll(const LLArgs& a, __amdgpu_buffer_rsrc_t
 #pragma unroll
     for (int q = 0; q < kL128MaxRanks; q++)
       if (((need >> q) & 1u) && l128LineReady(v[q].w == flag)) need &= ~(1u << q);
-    if (need != 0 && (++spins & 1023u) == 0u && llExpired(a, t0)) {
+    if (need != 0 && (++spins & 1023u) == 0u) {
       const int q = __builtin_ctz(need);
-      llGiveUp(a, site, q, flag, l128FlagOf(v, q), t0, t == 0);
-      return false;
+      const int peer = planPeer >= 0 ? planPeer : q;
+      if (plan != nullptr && llPlanMismatch(a, planPeer >= 0 ? plan : plan + q, flag, peer, t0, t == 0)) return false;
+      if (llExpired(a, t0)) {
+        llGiveUp(a, site, peer, flag, l128FlagOf(v, q), t0, t == 0);
+        return false;
+      }
     }
   }
   return true;
@@ -412,7 +488,7 @@ __device__ __forceinline__ void l128FoldLine(const Fn& fn, const LLArgs& a, cons
   }
 }
 
-template <class Fn>
+template <class Fn, bool CHECK>
 __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   using E = typename Fn::Elt;
   const Fn fn(llLoadArg<Fn>(a));
@@ -426,10 +502,13 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
 
-  // 0. credits (as kLLColl)
+  // 0. plan words, credits (as kLLColl)
+  const bool stamps = CHECK && blockIdx.x == 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x);
+  if (stamps) llPlanStamp(a, call, threadIdx.x);
   if (call.needDone != 0 && (int)threadIdx.x < n && llIsTarget(a, threadIdx.x)) {
     if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0, (int)threadIdx.x)) sFailed = 1;
   }
+  if (stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   bool failed = sFailed != 0;
 
@@ -454,6 +533,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.myL128, (short)0, (int)a.l128Bytes,
                                                                       0x00020000);
   const int fixedFirst = a.mode == kLLAllReduce ? -1 : ((a.mode == kLLReduce ? a.root : me) + 1) % n;
+  const uint64_t* const plan = CHECK ? llPlanWord(a.myLL, a, call.parity, 0) : nullptr;
   for (uint64_t i = g0; receives && !failed && i < a.nLines; i += groups) {
     const LLMsg m = llMsg<E>(a, i);
     const unsigned char* own = m.send + (a.mode == kLLReduceScatter ? (uint64_t)me * m.bytes : 0);
@@ -467,13 +547,16 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
         else need |= 1u << q;
       }
     }
-    failed = !l128Poll(a, rs, v, need, call.flag, kDiagLL128Line, t0, t, [&](int q) {
-      return (uint32_t)((((uint64_t)(call.parity * n + q)) * a.l128SlotLines + i) * kL128LineBytes);
-    });
+    failed = !l128Poll(
+        a, rs, v, need, call.flag, kDiagLL128Line, t0, t,
+        [&](int q) { return (uint32_t)((((uint64_t)(call.parity * n + q)) * a.l128SlotLines + i) * kL128LineBytes); },
+        plan, -1);
     l128FoldLine(fn, a, v, m.k, t, fixedFirst, m.blockElts, [&](int, uint64_t off, uint64_t w) {
       llStoreBytes(m.recv, off, m.bytes, w);
     });
   }
+  if (CHECK && receives && !failed && blockIdx.x == 0 && (int)threadIdx.x < n && (int)threadIdx.x != me)
+    (void)llPlanCheck(a, call, threadIdx.x, t0);
 
   // done word (as kLLColl)
   llEnd(a, call);
@@ -508,7 +591,7 @@ __device__ __forceinline__ void l128BlockRange(const LLArgs& a, int j, int eb, u
   *lenBytes = (hi - lo) * (uint64_t)eb;
 }
 
-template <class Fn>
+template <class Fn, bool CHECK>
 __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
   using E = typename Fn::Elt;
   constexpr int eb = (int)sizeof(E);
@@ -524,11 +607,16 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
   __shared__ int sFailed;
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
+  // plan words, credits (as kLLColl)
+  const bool stamps = CHECK && blockIdx.x == 0 && (int)threadIdx.x < n && (int)threadIdx.x != me;
+  if (stamps) llPlanStamp(a, call, threadIdx.x);
   if (call.needDone != 0 && (int)threadIdx.x < n && (int)threadIdx.x != me) {
     if (!llWait(a.myLL + a.doneOff + threadIdx.x, call.needDone, a, t0, (int)threadIdx.x)) sFailed = 1;
   }
+  if (stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   bool failed = sFailed != 0;
+  const uint64_t* const plan = CHECK ? llPlanWord(a.myLL, a, call.parity, 0) : nullptr;
   const unsigned char* send = (const unsigned char*)a.send;
   unsigned char* recv = (unsigned char*)a.recv;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.myL128, (short)0, (int)a.l128Bytes,
@@ -563,7 +651,7 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
         }
       }
       failed = !l128Poll(a, rs, v, need, call.flag, kDiagLL128RS, t0, t,
-                         [&](int q) { return (uint32_t)((subSlot(0, q) + i) * kL128LineBytes); });
+                         [&](int q) { return (uint32_t)((subSlot(0, q) + i) * kL128LineBytes); }, plan, -1);
       uint64_t w[2] = {0, 0};
       l128FoldLine(fn, a, v, i, t, first, a.blockElts, [&](int k, uint64_t o, uint64_t r) {
         w[k] = r;
@@ -589,12 +677,15 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
 #pragma unroll
       for (int q = 0; q < kL128MaxRanks; q++) v[q] = (u32x4){0, 0, 0, 0};
       failed = !l128Poll(a, rs, v, 1u, call.flag, kDiagLL128AG, t0, t,
-                         [&](int) { return (uint32_t)((subSlot(1, j) + i) * kL128LineBytes); });
+                         [&](int) { return (uint32_t)((subSlot(1, j) + i) * kL128LineBytes); }, plan ? plan + j : nullptr, j);
       const uint32_t pz = l128Partner(v[0].z);
       llStoreBytes(recv + off, l128WordOff(i, t), len, ((uint64_t)v[0].y << 32) | v[0].x);
       if (!(t & 1)) llStoreBytes(recv + off, l128PairOff(i, t) + 8, len, ((uint64_t)pz << 32) | v[0].z);
     }
   }
+  // every peer pushed its reduce-scatter lines here (both modes)
+  if (CHECK && !failed && blockIdx.x == 0 && (int)threadIdx.x < n && (int)threadIdx.x != me)
+    (void)llPlanCheck(a, call, threadIdx.x, t0);
   llEnd(a, call);
 }
 

@@ -63,6 +63,7 @@ struct LLArgs {
   uint64_t* myLL;
   uint64_t slotLines;      // lines per (parity, source) slot = 2 * max packs
   uint64_t doneOff;        // line index of the done words (one per writer rank) in every LL buffer
+  uint64_t planOff;        // line index of the plan words [parity 2][source n] in every LL buffer
   LLState* state;          // this rank's sequencing state (device memory)
   uint64_t blockElts;      // AllReduce: direct-schedule block size (elements) -> fold order
   uint64_t arg;            // functor scalar (by value)
@@ -84,8 +85,42 @@ struct LLArgs {
   MpDone order;
   int32_t nSegs;           // kLLColl group launch: segments in seg[] (0: one message)
   uint32_t gridCap;        // the communicator's workgroup cap (ranks sharing a GPU split it), 0: none
+  uint32_t planSig;        // llPlanSig: the same on every rank iff the ranks cut the call alike; 0: no plan checks
+  uint32_t pad;
   LLSeg seg[kLLMaxSegs];
 };
+
+// An LL-family launch's plan: what decides which line of a slot carries which
+// bytes and how a receiver folds them (protocol, kind, type, op, root, ranks,
+// message sizes and blocks, a group's cut; never a pointer, the rank or the
+// grid), hashed (FNV-1a, folded to 32 bits). Every source stamps it with the
+// call's flag into its plan word in each target's buffer (nbx_ll.h llPlanStamp).
+inline uint32_t llPlanSig(const LLArgs& a, int32_t proto, int32_t dtype, int32_t op) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&h](uint64_t v) {
+    for (int b = 0; b < 8; b++) {
+      h ^= (v >> (8 * b)) & 0xffu;
+      h *= 0x100000001b3ull;
+    }
+  };
+  mix((uint64_t)(uint32_t)proto);
+  mix((uint64_t)(uint32_t)a.mode);
+  mix((uint64_t)(uint32_t)a.root);
+  mix((uint64_t)(uint32_t)a.nRanks);
+  mix((uint64_t)(uint32_t)dtype);
+  mix((uint64_t)(uint32_t)op);
+  mix(a.count);
+  mix(a.nPacks);
+  mix(a.nLines);
+  mix(a.blockElts);
+  mix((uint64_t)(uint32_t)a.nSegs);
+  for (int s = 0; s < a.nSegs; s++) {
+    mix(a.seg[s].count);
+    mix(a.seg[s].packOff);
+    mix(a.seg[s].blockElts);
+  }
+  return (uint32_t)(h ^ (h >> 32)) | 1u;   // never 0 (0: checks off)
+}
 
 // ---------------------------------------------------------------------------
 // Simple protocol over init-mapped staging (nbx_simple.h). Peers never touch
@@ -148,7 +183,7 @@ struct SimpleArgs {
   const volatile int* abortWord;
   volatile int* errWord;
   uint64_t timeoutTicks;
-  uint64_t planSig;            // simplePlanSig: the same on every rank iff the ranks cut the call alike
+  uint64_t planSig;            // simplePlanSig: the same on every rank iff the ranks cut the call alike; 0: no checks
   uint64_t hdrOff;             // byte offset of the plan headers in every rank's staging
   int32_t rank;
   int32_t nRanks;

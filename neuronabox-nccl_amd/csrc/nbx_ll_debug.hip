@@ -44,7 +44,7 @@ __global__ __launch_bounds__(64) void kL128TearReader(LLArgs a, uint32_t flag, u
   u32x4 v[kL128MaxRanks];
 #pragma unroll
   for (int q = 0; q < kL128MaxRanks; q++) v[q] = (u32x4){0, 0, 0, 0};
-  const bool ok = l128Poll(a, rs, v, 2u, flag, kDiagLL128Line, wall_clock64(), t, [](int) { return 0u; });
+  const bool ok = l128Poll(a, rs, v, 2u, flag, kDiagLL128Line, wall_clock64(), t, [](int) { return 0u; }, nullptr, -1);
   if (t == 0) stamp[1] = ok ? wall_clock64() : 0;
   l128FoldLine(fn, a, v, 0, t, 1, a.blockElts, [&](int, uint64_t off, uint64_t w) { llStoreBytes(out, off, kL128DataBytes, w); });
 }

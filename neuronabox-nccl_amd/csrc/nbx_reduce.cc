@@ -450,7 +450,7 @@ size_t gridCapFromEnv(const char* name, long dflt) {
 ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
-  if (!ks.valid || ks.ll == nullptr) return ncclInvalidArgument;
+  if (!ks.valid || ks.ll == nullptr || ks.llChk == nullptr) return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
   // one 8-byte pack per thread; NBX_LL_MAX_GRID caps the workgroups (default
@@ -462,7 +462,7 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
   if (grid > maxGrid) grid = maxGrid;
   if (a.gridCap != 0 && grid > a.gridCap) grid = a.gridCap;
   void* args[] = {&a};
-  hipError_t e = hipLaunchKernel(ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);
+  hipError_t e = hipLaunchKernel(a.planSig != 0 ? ks.llChk : ks.ll, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
   return ncclSuccess;
 }
@@ -470,7 +470,7 @@ ncclResult_t launchLLColl(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& 
 ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& a, hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
-  if (!ks.valid || ks.ll128 == nullptr) return ncclInvalidArgument;
+  if (!ks.valid || ks.ll128 == nullptr || ks.ll128Chk == nullptr) return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
   // 64 lines (4 lanes each) per 256-thread workgroup, at most one workgroup per
@@ -484,7 +484,7 @@ ncclResult_t launchLL128Coll(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArg
   if (grid > maxGrid) grid = maxGrid;
   if (a.gridCap != 0 && grid > a.gridCap) grid = a.gridCap;
   void* args[] = {&a};
-  hipError_t e = hipLaunchKernel(ks.ll128, dim3((unsigned)grid), dim3(256), args, 0, stream);
+  hipError_t e = hipLaunchKernel(a.planSig != 0 ? ks.ll128Chk : ks.ll128, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
   return ncclSuccess;
 }
@@ -509,7 +509,7 @@ ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op,
                                    hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
-  if (!ks.valid || ks.ll128x2 == nullptr) return ncclInvalidArgument;
+  if (!ks.valid || ks.ll128x2 == nullptr || ks.ll128x2Chk == nullptr) return ncclInvalidArgument;
   a.arg = op.scalarArgIsPtr ? 0 : op.scalarArg;
   a.argPtr = op.scalarArgIsPtr ? (const void*)(uintptr_t)op.scalarArg : nullptr;
   static const size_t maxGrid = gridCapFromEnv("NBX_LL128_MAX_GRID", 256);
@@ -519,7 +519,7 @@ ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op,
   if (grid > maxGrid) grid = maxGrid;
   if (a.gridCap != 0 && grid > a.gridCap) grid = a.gridCap;
   void* args[] = {&a};
-  hipError_t e = hipLaunchKernel(ks.ll128x2, dim3((unsigned)grid), dim3(256), args, 0, stream);
+  hipError_t e = hipLaunchKernel(a.planSig != 0 ? ks.ll128x2Chk : ks.ll128x2, dim3((unsigned)grid), dim3(256), args, 0, stream);
   if (e != hipSuccess) return ncclUnhandledCudaError;
   return ncclSuccess;
 }

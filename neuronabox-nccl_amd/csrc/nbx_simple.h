@@ -127,27 +127,58 @@ __device__ __forceinline__ char* simpleStage(const SimpleArgs& a, int owner, int
   return a.peerStage[owner] + idx * a.stageSlice;
 }
 
-// The 16-byte plan header of slot `slot` of (region, source src, workgroup g)
-// in rank `owner`'s staging: {plan signature, round}, stamped by the producer
-// with the slice (published by the same drain and flag) and checked by the
-// consumer before it reads the slice. Ranks that cut a call or a group run
-// differently (or issue different calls) have different signatures, and the
-// consumer fails the launch (kDiagSimplePlan) instead of folding data of
-// another plan.
+// The plan header (when the communicator checks plans: SimpleArgs.planSig != 0,
+// NBX_CHECK_PLANS) of slot `slot` of (region, source src, workgroup g) in rank
+// `owner`'s staging (16-byte cell, the first 8 bytes used): {plan signature
+// (low 32 bits), the producer's count for this slot use (high 32 bits) = the
+// value its ready flag announces}, ONE 64-bit store before the drain that
+// publishes the slice. Ranks that cut a call or a group run differently (or
+// issue different calls) have different signatures, and the consumer fails the
+// launch (kDiagSimplePlan) instead of folding data of another plan. The count
+// makes a header fresh or stale without any ordering against the flag, so the
+// consumer loads it in the same poll as the flag (simpleWaitSlice): no extra
+// round trip per hand-off.
 __device__ __forceinline__ uint64_t* simpleHdr(const SimpleArgs& a, int owner, int region, uint64_t slot, int src,
                                                int g) {
   const uint64_t idx = (((uint64_t)region * a.slots + slot) * a.nRanks + src) * a.gridMax + g;
   return (uint64_t*)(a.peerStage[owner] + a.hdrOff + idx * 16);
 }
-__device__ __forceinline__ void simpleStamp(uint64_t* h, const SimpleArgs& a, uint64_t k) {
-  __hip_atomic_store(h, a.planSig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(h + 1, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ void simpleStamp(uint64_t* h, const SimpleArgs& a, uint64_t count) {
+  if (a.planSig == 0) return;   // plan checks off (NBX_CHECK_PLANS)
+  __hip_atomic_store(h, ((uint64_t)(uint32_t)count << 32) | (uint32_t)a.planSig, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ bool simpleCheck(const uint64_t* h, const SimpleArgs& a, uint64_t k, int peer) {
-  const uint64_t sig = __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const uint64_t round = __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (sig == a.planSig && round == k) return true;
-  diagTimeout(a.errWord, kDiagSimplePlan, peer, a.planSig, sig, round);
+
+// Bounded spin until the ready flag *w >= target, with slice header h (of the
+// slot that use `target` fills) loaded in the same poll; then the header must
+// carry `target` (reloaded if that poll's copy was older — the producer stored
+// it before the flag) and this launch's signature. False on timeout, abort or
+// a plan mismatch.
+__device__ __forceinline__ bool simpleWaitSlice(const uint64_t* w, uint64_t target, const uint64_t* h,
+                                                const SimpleArgs& a, int peer, uint64_t site) {
+  const uint64_t t0 = wall_clock64();
+  const bool chk = a.planSig != 0;   // plan checks on (NBX_CHECK_PLANS)
+  uint32_t spins = 0;
+  uint64_t hv = 0;
+  for (;;) {
+    const uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (chk) hv = __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+    if ((++spins & 255u) == 0u && (*a.abortWord != 0 || wall_clock64() - t0 > a.timeoutTicks)) {
+      const bool aborted = *a.abortWord != 0;
+      if (!aborted) diagTimeout(a.errWord, site, peer, target, v, wall_clock64() - t0);
+      *a.errWord = aborted ? 2 : 1;
+      return false;
+    }
+  }
+  if (!chk) return true;
+  while ((uint32_t)(hv >> 32) != (uint32_t)target) {
+    hv = __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((++spins & 255u) == 0u && wall_clock64() - t0 > a.timeoutTicks) break;
+  }
+  if (hv == (((uint64_t)(uint32_t)target << 32) | (uint32_t)a.planSig)) return true;
+  diagTimeout(a.errWord, kDiagSimplePlan, peer, (uint32_t)a.planSig, (uint32_t)hv, hv >> 32);
   *a.errWord = 1;
   return false;
 }
@@ -389,7 +420,8 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
       if (sp.cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
                                 sp.send + sp.off * sizeof(E), false, sp.cnt);
     }
-    if (tid < n && tid != me) simpleStamp(simpleHdr(a, tid, 0, sh.cnt[kCtRsSent][tid] % slots, me, g), a, k);
+    if (tid < n && tid != me)
+      simpleStamp(simpleHdr(a, tid, 0, sh.cnt[kCtRsSent][tid] % slots, me, g), a, sh.cnt[kCtRsSent][tid] + 1);
     simpleDrain();
     if (tid < n && tid != me) simplePost(simpleFlag(a.peerFlags[tid], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][tid]);
     __syncthreads();
@@ -398,9 +430,8 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
   auto phaseB = [&](uint64_t k) -> bool {
     // ---- B: fold block `me` (own input + the n-1 RS slots), store, push to the AG targets
     if (tid < n && tid != me) {
-      if (!simpleWait(simpleFlag(myFlags, kFlRsReady, n, tid, gm, g), sh.cnt[kCtRsRecv][tid] + 1, a, tid,
-                      kDiagSimpleRs) ||
-          !simpleCheck(simpleHdr(a, me, 0, sh.cnt[kCtRsRecv][tid] % slots, tid, g), a, k, tid))
+      if (!simpleWaitSlice(simpleFlag(myFlags, kFlRsReady, n, tid, gm, g), sh.cnt[kCtRsRecv][tid] + 1,
+                           simpleHdr(a, me, 0, sh.cnt[kCtRsRecv][tid] % slots, tid, g), a, tid, kDiagSimpleRs))
         sh.fail = 1;
       const uint64_t sent = sh.cnt[kCtAgSent][tid];
       if (pushTarget(tid) && sent + 1 > slots &&
@@ -434,7 +465,8 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
       const uint64_t sysSrc = ~(1ull << ((me - first + n) % n));
       simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
     }
-    if (tid < n && pushTarget(tid)) simpleStamp(simpleHdr(a, tid, 1, sh.cnt[kCtAgSent][tid] % slots, me, g), a, k);
+    if (tid < n && pushTarget(tid))
+      simpleStamp(simpleHdr(a, tid, 1, sh.cnt[kCtAgSent][tid] % slots, me, g), a, sh.cnt[kCtAgSent][tid] + 1);
     simpleDrain();
     if (tid < n && tid != me) {
       simplePost(simpleFlag(a.peerFlags[tid], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][tid]);
@@ -446,9 +478,8 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
   auto phaseC = [&](uint64_t k) -> bool {
     // ---- C: the peers' finished blocks from the AG region into the output
     if (tid < n && tid != me &&
-        (!simpleWait(simpleFlag(myFlags, kFlAgReady, n, tid, gm, g), sh.cnt[kCtAgRecv][tid] + 1, a, tid,
-                     kDiagSimpleAg) ||
-         !simpleCheck(simpleHdr(a, me, 1, sh.cnt[kCtAgRecv][tid] % slots, tid, g), a, k, tid)))
+        !simpleWaitSlice(simpleFlag(myFlags, kFlAgReady, n, tid, gm, g), sh.cnt[kCtAgRecv][tid] + 1,
+                         simpleHdr(a, me, 1, sh.cnt[kCtAgRecv][tid] % slots, tid, g), a, tid, kDiagSimpleAg))
       sh.fail = 1;
     __syncthreads();
     if (sh.fail) return false;
@@ -512,14 +543,14 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
   const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
   // thread 0 waits for what a hop needs: the left neighbour's slice (recvFrom)
   // and free slots at the right neighbour (RS region: pushRs, AG region: pushAg)
-  auto hopWait = [&](int recvRegion, bool pushRs, bool pushAg, uint64_t k) {
+  auto hopWait = [&](int recvRegion, bool pushRs, bool pushAg) {
     if (tid == 0) {
       if (recvRegion >= 0) {
         const int fl = recvRegion == 0 ? kFlRsReady : kFlAgReady;
         const int ct = recvRegion == 0 ? kCtRsRecv : kCtAgRecv;
-        if (!simpleWait(simpleFlag(myFlags, fl, n, left, gm, g), sh.cnt[ct][left] + 1, a, left,
-                        recvRegion == 0 ? kDiagSimpleRs : kDiagSimpleAg) ||
-            !simpleCheck(simpleHdr(a, me, recvRegion, sh.cnt[ct][left] % slots, left, g), a, k, left))
+        if (!simpleWaitSlice(simpleFlag(myFlags, fl, n, left, gm, g), sh.cnt[ct][left] + 1,
+                             simpleHdr(a, me, recvRegion, sh.cnt[ct][left] % slots, left, g), a, left,
+                             recvRegion == 0 ? kDiagSimpleRs : kDiagSimpleAg))
           sh.fail = 1;
       }
       const uint64_t rsS = sh.cnt[kCtRsSent][right], agS = sh.cnt[kCtAgSent][right];
@@ -534,10 +565,12 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
     return sh.fail == 0;
   };
   // the plan headers of this hop's pushes, before the drain that publishes them
-  auto hopStamp = [&](bool pushRs, bool pushAg, uint64_t k) {
+  auto hopStamp = [&](bool pushRs, bool pushAg) {
     if (tid == 0) {
-      if (pushRs) simpleStamp(simpleHdr(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), a, k);
-      if (pushAg) simpleStamp(simpleHdr(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g), a, k);
+      if (pushRs)
+        simpleStamp(simpleHdr(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), a, sh.cnt[kCtRsSent][right] + 1);
+      if (pushAg)
+        simpleStamp(simpleHdr(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g), a, sh.cnt[kCtAgSent][right] + 1);
     }
   };
   auto hopPost = [&](int recvRegion, bool pushRs, bool pushAg) {
@@ -557,7 +590,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       const SimpleSpan sp = simpleSlice<E>(a, segs, 0, k, g, grid);
       const uint64_t off = sp.off, cnt = sp.cnt;
       const bool push = pos < n - 1;
-      if (!hopWait(pos == 0 ? -1 : 0, push, false, k)) return;
+      if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
       char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : sp.recv + off * sizeof(E);
       if (pos == 0) {
         if (cnt) simpleCopy<E>(out, push, nullptr, false, sp.send + off * sizeof(E), false, cnt);
@@ -571,7 +604,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
         const bool aligned = simpleAligned(sp.send + off * sizeof(E)) && simpleAligned(out);
         simpleFold<Fn>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned);
       }
-      hopStamp(push, false, k);
+      hopStamp(push, false);
       simpleDrain();
       hopPost(pos == 0 ? -1 : 0, push, false);
       continue;
@@ -579,10 +612,10 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
     // send step: the raw chunk me-1 into the right neighbour's RS region
     {
       const SimpleSpan sp = simpleSlice<E>(a, segs, left, k, g, grid);
-      if (!hopWait(-1, true, false, k)) return;
+      if (!hopWait(-1, true, false)) return;
       if (sp.cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr,
                                 false, sp.send + sp.off * sizeof(E), false, sp.cnt);
-      hopStamp(true, false, k);
+      hopStamp(true, false);
       simpleDrain();
       hopPost(-1, true, false);
     }
@@ -592,7 +625,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       const bool last = st == n - 2;
       const SimpleSpan sp = simpleSlice<E>(a, segs, c, k, g, grid);
       const uint64_t off = sp.off, cnt = sp.cnt;
-      if (!hopWait(0, !last, last && ar, k)) return;
+      if (!hopWait(0, !last, last && ar)) return;
       if (tid == 0) {
         sh.src[0] = sp.send + off * sizeof(E);
         sh.src[1] = simpleStage(a, me, 0, sh.cnt[kCtRsRecv][left] % slots, left, g);
@@ -608,7 +641,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
         simpleFold<Fn>(fn, sh.src, 2, 2ull, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, last ? 2ull : 1ull,
                        cnt, aligned);
       }
-      hopStamp(!last, last && ar, k);
+      hopStamp(!last, last && ar);
       simpleDrain();
       hopPost(0, !last, last && ar);
     }
@@ -618,12 +651,12 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       const int c = (me + 2 * n - 1 - st) % n;
       const bool fwd = st < n - 2;
       const SimpleSpan sp = simpleSlice<E>(a, segs, c, k, g, grid);
-      if (!hopWait(1, false, fwd, k)) return;
+      if (!hopWait(1, false, fwd)) return;
       if (sp.cnt)
         simpleCopy<E>(sp.recv + sp.off * sizeof(E), false,
                       fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr, true,
                       simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, sp.cnt);
-      hopStamp(false, fwd, k);
+      hopStamp(false, fwd);
       simpleDrain();
       hopPost(1, false, fwd);
     }

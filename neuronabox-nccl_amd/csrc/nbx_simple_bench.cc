@@ -137,7 +137,8 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugSimpleRun(
     sa.gridMax = gridMax;
     sa.prefetch = prefetch;
     sa.hdrOff = hdrOff;
-    sa.planSig = nbx::simplePlanSig(sa, (uint32_t)grid, datatype, opFull.op);
+    const char* cp = std::getenv("NBX_CHECK_PLANS");   // as the communicator's default: off
+    sa.planSig = (cp && std::atoi(cp) != 0) ? nbx::simplePlanSig(sa, (uint32_t)grid, datatype, opFull.op) : 0;
   }
   // NBX_DEBUG_SIMPLE_FUSED=1: every rank's workgroups in ONE dispatch (fp32
   // sum), so a rocprofv3 PMC pass (which serializes dispatches) can count the

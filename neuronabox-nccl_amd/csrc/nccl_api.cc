@@ -727,6 +727,7 @@ struct MpState {
   uint64_t llMaxBytes = 0;
   uint64_t llSlotLines = 0;
   uint64_t llDoneOff = 0;
+  uint64_t llPlanOff = 0;   // plan words [parity 2][source n] (nbx_ll.h)
   nbx::LLState* llState = nullptr;  // device-resident LL-family sequencing (nbx_ll_args.h)
   // LL128 protocol (nbx_ll.h kLL128Coll): own buffer [2][n][l128SlotLines] 64-B lines;
   // shares the LL buffer's done words and parity credits
@@ -769,6 +770,7 @@ struct MpState {
   bool launched = false;            // the call being launched put a kernel on its stream
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
   bool groupBatch = true;           // NBX_GROUP_BATCH=0: every grouped call its own kernel
+  bool checkPlans = false;          // NBX_CHECK_PLANS (default NCCL_CHECK_POINTERS): plan words / headers
   std::vector<hipEvent_t> groupEvents;   // fan-in / fan-out of a group launch over several streams
   // clique ranks only: the previous call ran on the event-ordered fold path
   // (runCliqueColl / runCliqueBatch) on extStream; it is complete once every
@@ -807,6 +809,7 @@ struct MpInitInfo {
   int32_t slots;
   int32_t simpleGrid;
   int32_t groupBatch;      // NBX_GROUP_BATCH: one launch per run of grouped calls, or one per call
+  int32_t checkPlans;      // NBX_CHECK_PLANS: every launch stamps / checks its plan (or none does)
 };
 
 // NCCL_PROTO (tuning.cc:254-259, parseList): a comma-separated list of the
@@ -967,6 +970,13 @@ void mpReportDeviceError(ncclComm* c) {
     warn("comm %p rank %d: a device wait was aborted (ncclCommAbort)", (void*)c, c->rank);
     return;
   }
+  if (nbx::diagIsPlanCheck(rec[0])) {
+    warn("comm %p rank %d: device check failed after %.3f s: %s: peer %lld, our plan %llx, its plan %llx "
+         "(workgroup %llu)", (void*)c, c->rank, (double)rec[5] * 1e-8, nbx::diagSiteName(rec[0]),
+         (long long)(int64_t)rec[1], (unsigned long long)rec[2], (unsigned long long)rec[3],
+         (unsigned long long)rec[4]);
+    return;
+  }
   warn("comm %p rank %d: device wait timed out after %.3f s: %s of peer %lld, waited for %llu, last saw %llu "
        "(workgroup %llu)", (void*)c, c->rank, (double)rec[5] * 1e-8, nbx::diagSiteName(rec[0]),
        (long long)(int64_t)rec[1], (unsigned long long)rec[2], (unsigned long long)rec[3],
@@ -1003,6 +1013,13 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
   mp->protoMask = protoFromEnv();
   mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
   mp->groupBatch = envLong("NBX_GROUP_BATCH", 1) != 0;
+  // Plan checks (nbx_ll.h plan words, nbx_simple.h slice headers): a launch
+  // fails, naming the peer, when ranks issue mismatched calls or cut a group
+  // differently — instead of a timeout or folded misplaced data. Off unless
+  // asked for (NBX_CHECK_PLANS=1, or the reference's own argument-checking
+  // knob NCCL_CHECK_POINTERS=1): they cost 0.7-1.9 us per small call on the
+  // shared-GPU rig, and the reference does not check this either.
+  mp->checkPlans = envLong("NBX_CHECK_PLANS", comm->checkPointers ? 1 : 0) != 0;
   HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
   HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
@@ -1018,7 +1035,8 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
     mp->llMaxBytes = mx;
     mp->llSlotLines = 2 * (mx / 8);
     mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
-    mp->llBytes = (mp->llDoneOff + (uint64_t)n + 1) * sizeof(uint64_t);
+    mp->llPlanOff = mp->llDoneOff + (uint64_t)n + 1;
+    mp->llBytes = (mp->llPlanOff + 2 * (uint64_t)n) * sizeof(uint64_t);
     const uint64_t llAlloc = connAllocBytes(mp->llBytes, n);
     HIPCHECK(allocSyncMem((void**)&mp->ll, llAlloc, ipc ? &mp->llHandle : nullptr));
     HIPCHECK(hipMemset(mp->ll, 0, llAlloc));
@@ -1298,6 +1316,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.slots = mp->slots;
   mine.simpleGrid = mp->simpleGrid;
   mine.groupBatch = mp->groupBatch;
+  mine.checkPlans = mp->checkPlans;
   mine.nonce = std::random_device{}() * 0x100000001ull ^ (uint64_t)std::random_device{}() ^
                ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)mp;
   mine.llHandle = mp->llHandle;
@@ -1324,6 +1343,11 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     // advances the device-resident sequence by one: ranks must cut alike
     if (all[j].groupBatch != mine.groupBatch) {
       warn("ncclCommInitRank : NBX_GROUP_BATCH differs across ranks");
+      return ncclInvalidUsage;
+    }
+    // a checking rank would wait for plan words a non-checking peer never stamps
+    if (all[j].checkPlans != mine.checkPlans) {
+      warn("ncclCommInitRank : NBX_CHECK_PLANS / NCCL_CHECK_POINTERS differ across ranks");
       return ncclInvalidUsage;
     }
     if (j == me || all[j].device == c->device) continue;
@@ -1406,6 +1430,7 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
   la.myLL = mp->ll;
   la.slotLines = mp->llSlotLines;
   la.doneOff = mp->llDoneOff;
+  la.planOff = mp->llPlanOff;
   la.state = mp->llState;
   la.blockElts = per > 0 ? per : 1;
   la.abortWord = mp->hostWordsDev;
@@ -1444,12 +1469,15 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
       la.nLines = mp->l128SlotLines / 2;   // sub-slot lines: [parity][RS|AG][source]
       const uint64_t blockLines =
           ((uint64_t)per * (uint64_t)eb + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+      la.planSig = mp->checkPlans ? nbx::llPlanSig(la, (int32_t)proto, (int32_t)c.dt, c.op.op) : 0;
       return nbx::launchLL128AllReduce2(c.dt, c.op, la, blockLines, c.stream);
     }
     la.nLines = nSegs > 1 ? units : (slotBytes + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost;
+    la.planSig = mp->checkPlans ? nbx::llPlanSig(la, (int32_t)proto, (int32_t)c.dt, c.op.op) : 0;
     return nbx::launchLL128Coll(c.dt, c.op, la, c.stream);
   }
   if (nSegs > 1) la.nPacks = units;
+  la.planSig = mp->checkPlans ? nbx::llPlanSig(la, (int32_t)proto, (int32_t)c.dt, c.op.op) : 0;
   return nbx::launchLLColl(c.dt, c.op, la, c.stream);
 }
 
@@ -1531,7 +1559,7 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc) {
   sa.gridMax = mp->simpleGrid;
   sa.prefetch = mp->simplePrefetch;
   sa.hdrOff = mp->stageHdrOff;
-  sa.planSig = nbx::simplePlanSig(sa, (uint32_t)grid, (int32_t)c.dt, c.op.op);
+  sa.planSig = mp->checkPlans ? nbx::simplePlanSig(sa, (uint32_t)grid, (int32_t)c.dt, c.op.op) : 0;
   sa.order = mpOrderArgs(mp);
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
 }
@@ -2506,7 +2534,8 @@ NBX_EXPORT int nbxDebugCommProtoMask(ncclComm_t comm) {
 // rank's in-process transport's): out[0] LL max bytes, [1] LL128 max bytes,
 // [2] Simple slice bytes, [3] Simple slots, [4] Simple grid, [5] LL grid cap,
 // [6] LL128 grid cap, [7] group batching, [8] connection buffers re-exported
-// at creation because a peer's mapping of them was wrong (mpConnect). Returns
+// at creation because a peer's mapping of them was wrong (mpConnect), [9] plan
+// checks on (NBX_CHECK_PLANS / NCCL_CHECK_POINTERS). Returns
 // how many were written, -1
 // for a bad handle or a communicator without that transport.
 NBX_EXPORT int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut) {
@@ -2514,11 +2543,11 @@ NBX_EXPORT int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut) {
   if (comm->asyncError.load() != ncclSuccess) return -1;
   const MpState* mp = mpOf(comm);
   if (mp == nullptr) return -1;
-  const int64_t v[9] = {(int64_t)mp->llMaxBytes, (int64_t)mp->l128MaxBytes, (int64_t)mp->sliceBytes, mp->slots,
-                        mp->simpleGrid,          (int64_t)mp->llGridCap,    (int64_t)mp->l128GridCap, mp->groupBatch,
-                        mp->ipcRepairs};
+  const int64_t v[10] = {(int64_t)mp->llMaxBytes, (int64_t)mp->l128MaxBytes, (int64_t)mp->sliceBytes, mp->slots,
+                         mp->simpleGrid,          (int64_t)mp->llGridCap,    (int64_t)mp->l128GridCap, mp->groupBatch,
+                         mp->ipcRepairs,          mp->checkPlans};
   int k = 0;
-  for (; k < nOut && k < 9; k++) out[k] = v[k];
+  for (; k < nOut && k < 10; k++) out[k] = v[k];
   return k;
 }
 

@@ -1216,8 +1216,8 @@ def _child_knobs(uid_bytes, rank, n, q, env):
         except nbx.NcclError as e:
             q.put((rank, "ok", {"init": int(e.code)}))
             return
-        vals = (ctypes.c_int64 * 9)()
-        got = lib.nbxDebugCommSettings(comm.handle, vals, 9)
+        vals = (ctypes.c_int64 * 10)()
+        got = lib.nbxDebugCommSettings(comm.handle, vals, 10)
         out = {"init": 0, "settings": list(vals)[:got]}
         st = torch.cuda.current_stream().cuda_stream
         for cnt in (2048, 131072, 1 << 20):   # 8 KiB (LL), 512 KiB (LL128), 4 MiB (Simple) of fp32
@@ -1253,6 +1253,20 @@ def test_multiprocess_reference_knobs(nbx, monkeypatch):
         ll, l128, slice_, slots, grid, llcap, l128cap, batch = res[r]["settings"][:8]
         assert (ll, l128, slice_, slots, grid) == (32768, 786432, 131072, 2, 16), res[r]["settings"]
         assert llcap <= 16 and l128cap <= 16 and batch == 1
+        assert res[r]["settings"][9] == 0   # plan checks off by default
+        assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
+
+
+@pytest.mark.parametrize("name", ["NCCL_CHECK_POINTERS", "NBX_CHECK_PLANS"])
+def test_multiprocess_plan_checks_on_exact(nbx, monkeypatch, name):
+    """The reference's argument-checking knob (or NBX_CHECK_PLANS) turns the
+    plan words / slice headers on; LL, LL128 and Simple results stay exact."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.delenv("NBX_CHECK_PLANS", raising=False)
+    res = _run_ranks(nbx, 2, _child_knobs, {name: ["1", "1"]})
+    for r in range(2):
+        assert res[r]["init"] == 0 and res[r]["settings"][9] == 1, res[r]
         assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
 
 
@@ -1270,14 +1284,14 @@ def test_multiprocess_nbx_override_wins(nbx, monkeypatch):
 
 
 @pytest.mark.parametrize("name,vals", [("NCCL_BUFFSIZE", ["262144", "131072"]), ("NBX_GROUP_BATCH", ["1", "0"]),
-                                       ("NCCL_LL_BUFFSIZE", ["65536", "32768"])])
+                                       ("NCCL_LL_BUFFSIZE", ["65536", "32768"]), ("NBX_CHECK_PLANS", ["1", "0"])])
 def test_multiprocess_settings_must_agree(nbx, monkeypatch, name, vals):
     """Settings that decide a call's protocol, grid, staging layout or launch
     cut must be equal on every rank: ncclCommInitRank fails with
     ncclInvalidUsage on every rank instead of the ranks' kernels disagreeing."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
-    for k in ("NBX_SIMPLE_SLICE_BYTES", "NBX_LL_MAX_BYTES", "NBX_GROUP_BATCH"):
+    for k in ("NBX_SIMPLE_SLICE_BYTES", "NBX_LL_MAX_BYTES", "NBX_GROUP_BATCH", "NBX_CHECK_PLANS"):
         monkeypatch.delenv(k, raising=False)
     res = _run_ranks(nbx, 2, _child_knobs, {name: vals})
     for r in range(2):
@@ -1440,13 +1454,15 @@ def test_multiprocess_abort_ends_pending_init_device_wait(nbx, monkeypatch):
     assert res[0]["abort_s"] < 20, res[0]                                      # not the 120 s timeout
 
 
-def _child_plan_mismatch(uid_bytes, rank, n, q, case):
-    """Ranks whose Simple launches are cut from different plans: every slice
-    carries its producer's plan signature, so the consumer fails the launch
-    (ncclRemoteError, the wait named "... different plan ...") instead of
-    folding misplaced data. case "count": the ranks pass different counts;
-    case "group": rank 0's group reads what its previous call wrote (cut into
-    two launches), rank 1's calls are independent (one launch)."""
+def _child_plan_mismatch(uid_bytes, rank, n, q, case, cnt=300000):
+    """Ranks whose launches are cut from different plans: every Simple slice
+    carries its producer's plan signature, every LL / LL128 source stamps its
+    plan word, so the consumer fails the launch (ncclRemoteError, the check
+    named "... different plan ...") instead of folding misplaced data or
+    timing out. case "count": the ranks pass different counts; "op": the same
+    count, rank 1 reduces with max (its lines do arrive); "group": rank 0's
+    group reads what its previous call wrote (cut into two launches), rank 1's
+    calls are independent (one launch)."""
     try:
         import ctypes
 
@@ -1457,13 +1473,14 @@ def _child_plan_mismatch(uid_bytes, rank, n, q, case):
         torch.cuda.set_device(0)
         comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
         st = torch.cuda.current_stream().cuda_stream
-        cnt = 300000
         a = torch.ones(cnt + 8, device="cuda")
         b = torch.zeros(cnt + 8, device="cuda")
         c = torch.zeros(cnt + 8, device="cuda")
         d = torch.ones(cnt + 8, device="cuda")
         if case == "count":
             comm.all_reduce(a.data_ptr(), b.data_ptr(), cnt + (3 if rank == 1 else 0), 7, 0, st)
+        elif case == "op":
+            comm.all_reduce(a.data_ptr(), b.data_ptr(), cnt, 7, 2 if rank == 1 else 0, st)
         else:
             nbx.group_start()
             comm.all_reduce(a.data_ptr(), b.data_ptr(), cnt, 7, 0, st)
@@ -1481,6 +1498,7 @@ def _child_plan_mismatch(uid_bytes, rank, n, q, case):
 
 @pytest.mark.parametrize("case", ["count", "group"])
 def test_multiprocess_simple_plan_mismatch_fails_loudly(nbx, monkeypatch, case):
+    monkeypatch.setenv("NCCL_CHECK_POINTERS", "1")   # turns the plan checks on (NBX_CHECK_PLANS default)
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "5")
     monkeypatch.setenv("NCCL_PROTO", "Simple")
@@ -1489,3 +1507,21 @@ def test_multiprocess_simple_plan_mismatch_fails_loudly(nbx, monkeypatch, case):
     remote = int(nbx.ncclResult.ncclRemoteError)
     assert all(res[r]["err"] == remote for r in range(2)), res
     assert any("different plan" in res[r]["msg"] for r in range(2)), res
+
+
+# LL (4 KiB), LL128 one-shot (80 KB) and two-shot (1.2 MB): a peer that runs the
+# same call with another plan is named by its plan word well before the 5 s
+# timeout (a timeout would read "timed out", not "different plan")
+@pytest.mark.parametrize("proto,cnt,case", [("LL", 1000, "count"), ("LL", 1000, "op"), ("LL", 1000, "group"),
+                                            ("LL128", 20000, "count"), ("LL128", 20000, "op"),
+                                            ("LL128", 300000, "count"), ("LL128", 300000, "op")])
+def test_multiprocess_ll_plan_mismatch_fails_loudly(nbx, monkeypatch, proto, cnt, case):
+    monkeypatch.setenv("NBX_CHECK_PLANS", "1")
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "5")
+    monkeypatch.setenv("NCCL_PROTO", proto)
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")
+    res = _run_ranks(nbx, 2, _child_plan_mismatch, case, cnt)
+    remote = int(nbx.ncclResult.ncclRemoteError)
+    assert all(res[r]["err"] == remote for r in range(2)), res
+    assert all("different plan" in res[r]["msg"] for r in range(2)), res
