@@ -816,7 +816,7 @@ struct MpInitInfo {
 // enabled protocols among LL, LL128, Simple, or "^list" for all but those.
 // Per message (per-rank block for ReduceScatter) the first enabled protocol
 // whose buffer holds it is used: LL up to NBX_LL_MAX_BYTES (64 KiB), LL128 up
-// to NBX_LL128_MAX_BYTES (4 MiB; n <= 8 ranks), else Simple (also the
+// to NBX_LL128_MAX_BYTES (1 MiB; n <= 8 ranks), else Simple (also the
 // fallback when Simple is disabled and nothing else fits).
 // Read when the communicator is created (as NCCL reads its tuning env at init).
 enum { kProtoLL = 1, kProtoLL128 = 2, kProtoSimple = 4, kProtoAll = 7 };
@@ -840,12 +840,12 @@ int protoFromString(const char* v) {
 }
 int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
 
-// Per message: LL up to the LL max; LL128 one-shot (every rank pushes the
-// whole message to every target) up to the LL128 max — for AllReduce / Reduce
-// with more than 2 ranks only up to the one-shot max; above that the LL128
-// two-shot AllReduce / Reduce (reduce-scatter + gather hops) while a rank's
-// block fits half an LL128 slot; else Simple. ReduceScatter is one hop by
-// nature: one-shot up to the LL128 max.
+// Per message: LL up to the LL max; LL128 up to the LL128 max: one-shot (every
+// rank pushes the whole message to every target), for AllReduce / Reduce with
+// more than 2 ranks only up to the one-shot max and the two-shot AllReduce /
+// Reduce (reduce-scatter + gather hops, a rank's block in half an LL128 slot)
+// above it; else Simple. ReduceScatter is one hop by nature: one-shot up to
+// the LL128 max.
 enum MpProto : int { kMpLL = 0, kMpLL128 = 1, kMpSimple = 2, kMpLL128x2 = 3 };
 // Lines per (parity, source) slot: holds maxBytes one-shot, and each half (a
 // two-shot sub-slot) holds maxBytes / 2.
@@ -860,7 +860,7 @@ MpProto chooseProtoFor(int mask, bool twoShotKind, uint64_t slotBytes, uint64_t 
   if ((mask & kProtoLL128) && l128Max != 0 && n <= nbx::kL128MaxRanksHost) {
     if (!twoShotKind || n <= 2 || slotBytes <= oneShotMax) {
       if (slotBytes <= l128Max) return kMpLL128;
-    } else if (blockBytes <= (l128SlotLinesFor(l128Max) / 2) * nbx::kL128DataBytesHost) {
+    } else if (slotBytes <= l128Max && blockBytes <= (l128SlotLinesFor(l128Max) / 2) * nbx::kL128DataBytesHost) {
       return kMpLL128x2;
     }
   }
@@ -1043,7 +1043,10 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
   }
   // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
   if (n <= nbx::kL128MaxRanksHost) {
-    uint64_t mx = (uint64_t)ncclEnvMapped("NBX_LL128_MAX_BYTES", "NCCL_LL128_BUFFSIZE", 4 << 20, 3, 4);
+    // 1 MiB: where Simple overtakes LL128 (48 payload bytes per 64-byte line) on
+    // the shared-GPU rig — 2 ranks: 1 MiB 15.4 vs 15.6 us, 2 MiB 25.8 vs 16.4,
+    // 4 MiB 43.8 vs 18.7; 4 ranks: 2 MiB 34.5 vs 25.4 (profiles/r4/proto_sweep_r4z)
+    uint64_t mx = (uint64_t)ncclEnvMapped("NBX_LL128_MAX_BYTES", "NCCL_LL128_BUFFSIZE", 1 << 20, 3, 4);
     mp->l128OneShotMax = (uint64_t)envLong("NBX_LL128_ONESHOT_MAX", 256 << 10);
     if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
     if (mx != 0) {

@@ -318,10 +318,10 @@ def test_multiprocess_ring_fifo_reduce_scatter_and_reduce(nbx, oracle, n, grid, 
 
 
 # (kind, dtype, op, count, byte offset of send/recv). By default slots
-# <= 64 KiB take the LL protocol; LL128 one-shot up to 4 MiB (AllReduce with
-# > 2 ranks: up to 256 KiB), LL128 two-shot AllReduce above that while a rank's
-# block fits 2 MiB; the rest the direct (Simple) path. With NCCL_PROTO=LL128
-# every message takes LL128. Reduce to a changing root back to back exercises
+# <= 64 KiB take the LL protocol; LL128 up to 1 MiB: one-shot (AllReduce with
+# > 2 ranks: up to 256 KiB), LL128 two-shot AllReduce above that; the rest the
+# direct (Simple) path. With NCCL_PROTO=LL128 (and a 4 MiB LL128 max) every
+# message up to 4 MiB takes LL128. Reduce to a changing root back to back exercises
 # the done-word credits (a non-root never waits for data, so only the credits
 # stop it from overwriting a slot the root has not read yet).
 LL_CASES = [
@@ -338,7 +338,7 @@ LL_CASES = [
     ("ar", 7, 4, 262144, 0), ("ar", 9, 0, 300001, 0), ("ar", 11, 0, 600001, 1), ("ar", 7, 0, 300000, 4),
     ("ar", 2, 2, 1000003, 0), ("ar", 8, 0, 200001, 0), ("red", 7, 0, 300001, 0), ("red", 9, 4, 200003, 2),
     ("red", 2, 3, 500000, 0),
-    # direct (Simple) path interleaved: > 4 MiB per slot
+    # direct (Simple) path interleaved: > 4 MiB per slot (> 1 MiB by default)
     ("ar", 7, 0, 1100000, 0), ("rs", 7, 4, 1048577, 0),
 ]
 
@@ -358,6 +358,7 @@ def _child_ll(uid_bytes, rank, n, q, proto):
         import os
         if proto:
             os.environ["NCCL_PROTO"] = proto
+            os.environ["NBX_LL128_MAX_BYTES"] = str(4 << 20)   # the 1-4 MiB cases through both LL128 shapes too
         import time
 
         import torch
@@ -470,7 +471,7 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
 
 # fp32 counts -> protocol by default (2-3 ranks): LL, LL128 one-shot, LL128
 # two-shot (3 ranks; one-shot at 2), Simple
-GRAPH_CASES = [(1000, "LL"), (50003, "LL128"), (300001, "LL128 two-shot"), (1500000, "Simple"),
+GRAPH_CASES = [(1000, "LL"), (50003, "LL128"), (200001, "LL128 two-shot"), (1500000, "Simple"),
                # one ncclGroupStart/End: two LL-sized calls and two LL128 one-shot calls -> two group launches
                (777, "LL group"), (4099, "LL group"), (20000, "LL128 group"), (30001, "LL128 group")]
 

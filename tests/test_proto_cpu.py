@@ -1,8 +1,8 @@
 """Protocol selection of the multi-process communicator, on the CPU through
 the library's debug hooks (include/nbx_debug.h): NCCL_PROTO parsing in NCCL's
 list syntax (tuning.cc:254-259: "LL,LL128", "^Simple", case-insensitive) and
-the per-message choice LL (<= LL max) -> LL128 one-shot (<= LL128 max, <= 8
-ranks; AllReduce with > 2 ranks only up to the one-shot max) -> LL128 two-shot
+the per-message choice LL (<= LL max) -> LL128 (<= LL128 max, <= 8 ranks):
+one-shot (AllReduce with > 2 ranks only up to the one-shot max), else two-shot
 AllReduce / Reduce (a rank's block fits half an LL128 slot) -> Simple;
 ReduceScatter (one hop by nature) one-shot up to the LL128 max."""
 import ctypes
@@ -45,9 +45,9 @@ def _block(nbytes, n, eb=4):
 
 @pytest.mark.parametrize("mask,ar,nbytes,n,want", [
     (ALL, 1, 4, 2, P_LL), (ALL, 1, 64 * K, 8, P_LL), (ALL, 1, 64 * K + 4, 8, P_LL128), (ALL, 1, 256 * K, 8, P_LL128),
-    (ALL, 1, 256 * K + 4, 8, P_LL128X2), (ALL, 1, 16 * M, 8, P_LL128X2), (ALL, 1, 16 * M + 1024, 8, P_SIMPLE),
+    (ALL, 1, 256 * K + 4, 8, P_LL128X2), (ALL, 1, 4 * M, 8, P_LL128X2), (ALL, 1, 4 * M + 1024, 8, P_SIMPLE),
     (ALL, 1, 4 * M, 2, P_LL128), (ALL, 1, 4 * M + 4, 2, P_SIMPLE),      # 2 ranks: one-shot only
-    (ALL, 1, 6 * M, 3, P_LL128X2), (ALL, 1, 8 * M, 3, P_SIMPLE),
+    (ALL, 1, 4 * M, 3, P_LL128X2), (ALL, 1, 6 * M, 3, P_SIMPLE),      # the slot bounds both shapes
     (ALL, 0, 4 * M, 8, P_LL128), (ALL, 0, 4 * M + 4, 8, P_SIMPLE),      # RS: one-shot up to the max
     (ALL, 1, 256 * K, 9, P_SIMPLE), (ALL, 1, 4 * K, 9, P_LL),           # LL128 only up to 8 ranks
     (ALL, 1, 0, 4, P_SIMPLE), (ALL, 1, 4 * K, 65, P_SIMPLE),
