@@ -641,6 +641,18 @@ def main():
         assert torch.equal(out[idx], ref), "bench output differs from the left-fold reference"
 
     achieved = ALG_BYTES / (kern_avg_ms * 1e-3) / 1e9
+    # median and best per launch too — a separate pass after the
+    # timed region, one event pair per launch (the timed region brackets all K
+    # launches with one pair: an event between launches costs ~1.5 %)
+    per = []
+    for _ in range(max(args.steps, 5)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        step()
+        e1.record(stream)
+        per.append((e0, e1))
+    torch.cuda.synchronize()
+    per_ms = sorted(a.elapsed_time(b) for a, b in per)
     traffic, traffic_src = _pmc_traffic()
     ceil = None
     if os.environ.get("NBX_BENCH_CEILING", "1") != "0":
@@ -670,6 +682,9 @@ def main():
                      "tile_schedule": "static" if os.environ.get("NBX_DYNAMIC_TILES", "1") == "0"
                      else "dynamic (per-stream tile counter)",
                      "kernel_avg_ms": round(kern_avg_ms, 5),
+                     "kernel_ms_median": round(per_ms[len(per_ms) // 2], 5),
+                     "kernel_ms_best": round(per_ms[0], 5),
+                     "per_launch_what": f"{len(per_ms)} launches after the timed region, one event pair each",
                      "alg_bytes_per_launch": ALG_BYTES},
         "cpu_baseline": None,
         "collective": None,
