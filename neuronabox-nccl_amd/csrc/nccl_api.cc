@@ -1062,33 +1062,6 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
   return ncclSuccess;
 }
 
-// Opens every peer's connection buffers and checks every mapping before first
-// use, re-exporting any buffer whose mapping is wrong (the reference maps its
-// peers' buffers once at connection time, transport/p2p.cc:290-330 p2pMap).
-// Why the check is needed: scripts/probe_ipc_export.py (raw HIP, N processes
-// on one GPU replaying communicator creation / destruction with this
-// library's buffer sizes and memory kinds) found IPC mappings that do not
-// show the exported allocation — an importer reads zeros or ANOTHER rank's
-// buffer through it (89 canary reads), and its stores never reach the owner
-// (164), out of 62,400 imports, in the library's own memory kind as in plain
-// hipMalloc memory; the same wrong bytes are seen by every importer of that
-// handle (so it is the export, not one importer's mapping, that is wrong),
-// mostly at owner addresses that an earlier, freed allocation of the owner
-// had been exported from; with exported buffers never freed, none. Round 2's
-// wrong results (peers reading stale bytes through a mapping of a freshly
-// allocated buffer, their stores lost) are the same failure.
-// Check, per buffer and round (each with a fresh per-communicator nonce):
-// every rank stores a 16-byte word through its mapping of every peer's buffer
-// (slot = its rank) and its own word into its own buffer (slot n), all in the
-// check region after the used bytes; after a bootstrap barrier every rank
-// checks the words its peers stored into its buffers and reads every peer's
-// own word through its mappings. A wrong (owner, buffer) seen by anyone —
-// agreed by an allgather — is re-exported: its owner allocates a new buffer
-// (the old one held until the end, so the new one lands elsewhere), every
-// peer closes the wrong mapping and opens the new handle, and the round
-// repeats (at most 4). Only then does ncclCommInitRank fail (ncclSystemError).
-// NBX_IPC_VERIFY_FAIL=<rank>:<buffer> (test hook) makes round 0 report that
-// rank's buffer (0 LL, 1 LL128, 2 staging, 3 flags) wrong.
 // Grid caps and Simple settings of one rank's transport. Simple grid: one
 // workgroup per CU, all co-resident (workgroup g of a rank waits on workgroup
 // g of its peers); ranks sharing a GPU split its CUs, and so do the LL
@@ -1135,6 +1108,33 @@ ncclResult_t mpAllocSimple(MpState* mp, int n, bool ipc) {
   return ncclSuccess;
 }
 
+// Opens every peer's connection buffers and checks every mapping before first
+// use, re-exporting any buffer whose mapping is wrong (the reference maps its
+// peers' buffers once at connection time, transport/p2p.cc:290-330 p2pMap).
+// Why the check is needed: scripts/probe_ipc_export.py (raw HIP, N processes
+// on one GPU replaying communicator creation / destruction with this
+// library's buffer sizes and memory kinds) found IPC mappings that do not
+// show the exported allocation — an importer reads zeros or ANOTHER rank's
+// buffer through it (89 canary reads), and its stores never reach the owner
+// (164), out of 62,400 imports, in the library's own memory kind as in plain
+// hipMalloc memory; the same wrong bytes are seen by every importer of that
+// handle (so it is the export, not one importer's mapping, that is wrong),
+// mostly at owner addresses that an earlier, freed allocation of the owner
+// had been exported from; with exported buffers never freed, none. Round 2's
+// wrong results (peers reading stale bytes through a mapping of a freshly
+// allocated buffer, their stores lost) are the same failure.
+// Check, per buffer and round (each with a fresh per-communicator nonce):
+// every rank stores a 16-byte word through its mapping of every peer's buffer
+// (slot = its rank) and its own word into its own buffer (slot n), all in the
+// check region after the used bytes; after a bootstrap barrier every rank
+// checks the words its peers stored into its buffers and reads every peer's
+// own word through its mappings. A wrong (owner, buffer) seen by anyone —
+// agreed by an allgather — is re-exported: its owner allocates a new buffer
+// (the old one held until the end, so the new one lands elsewhere), every
+// peer closes the wrong mapping and opens the new handle, and the round
+// repeats (at most 4). Only then does ncclCommInitRank fail (ncclSystemError).
+// NBX_IPC_VERIFY_FAIL=<rank>:<buffer> (test hook) makes round 0 report that
+// rank's buffer (0 LL, 1 LL128, 2 staging, 3 flags) wrong.
 ncclResult_t mpConnect(ncclComm* c, const std::vector<MpInitInfo>& all) {
   MpState* mp = c->mp;
   const int n = c->nRanks, me = c->rank;
