@@ -111,11 +111,16 @@ struct LLCall {
   uint32_t flag;
 };
 
+// The three state words are loaded together (one round trip, not two: the
+// previous launch on this stream wrote all of them before it completed).
 __device__ __forceinline__ LLCall llBegin(const LLArgs& a) {
   LLCall c;
-  c.seq = __hip_atomic_load(&a.state->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const uint64_t s = __hip_atomic_load(&a.state->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t l0 = __hip_atomic_load(&a.state->lastSeq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t l1 = __hip_atomic_load(&a.state->lastSeq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  c.seq = s + 1;
   c.parity = (int)(c.seq & 1u);
-  c.needDone = __hip_atomic_load(&a.state->lastSeq[c.parity], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  c.needDone = c.parity ? l1 : l0;
   c.flag = (uint32_t)c.seq;
   return c;
 }
@@ -219,6 +224,15 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
   const uint64_t flagHi = (uint64_t)call.flag << 32;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = wall_clock64();
+  // this thread's first pack of the caller's input, loaded while the credits
+  // are checked (AllReduce / Reduce: one pack for every target)
+  const uint64_t k0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool pre = a.mode != kLLReduceScatter && k0 < a.nPacks;
+  uint64_t first = 0;
+  if (pre) {
+    const LLMsg m0 = llMsg<E>(a, k0);
+    first = llLoadBytes(m0.send, m0.k * 8, m0.bytes);
+  }
   __shared__ int sFailed;
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
@@ -239,7 +253,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.nPacks; k += stride) {
       const LLMsg m = llMsg<E>(a, k);
       uint64_t whole = 0;
-      if (a.mode != kLLReduceScatter) whole = llLoadBytes(m.send, m.k * 8, m.bytes);
+      if (a.mode != kLLReduceScatter) whole = (pre && k == k0) ? first : llLoadBytes(m.send, m.k * 8, m.bytes);
       for (int j = 0; j < n; j++) {
         if (!llIsTarget(a, j)) continue;
         const uint64_t v = a.mode == kLLReduceScatter ? llLoadBytes(m.send + (uint64_t)j * m.bytes, m.k * 8, m.bytes)
@@ -498,6 +512,13 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
   const uint64_t g0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / kL128Lanes;
   const uint64_t t0 = wall_clock64();
   const LLCall call = llBegin(a);
+  // this lane's chunk of its first line, loaded while the credits are checked
+  const bool pre = a.mode != kLLReduceScatter && g0 < a.nLines;
+  u32x4 first = {0, 0, 0, 0};
+  if (pre) {
+    const LLMsg m0 = llMsg<E>(a, g0);
+    first = l128Chunk(m0.send, m0.bytes, m0.k, t, call.flag);
+  }
   __shared__ int sFailed;
   if (threadIdx.x == 0) sFailed = 0;
   __syncthreads();
@@ -517,7 +538,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
     for (uint64_t i = g0; i < a.nLines; i += groups) {
       const LLMsg m = llMsg<E>(a, i);
       u32x4 whole = {0, 0, 0, 0};
-      if (a.mode != kLLReduceScatter) whole = l128Chunk(m.send, m.bytes, m.k, t, call.flag);
+      if (a.mode != kLLReduceScatter) whole = (pre && i == g0) ? first : l128Chunk(m.send, m.bytes, m.k, t, call.flag);
       for (int j = 0; j < n; j++) {
         if (!llIsTarget(a, j)) continue;
         const u32x4 v = a.mode == kLLReduceScatter ? l128Chunk(m.send + (uint64_t)j * m.bytes, m.bytes, m.k, t, call.flag)
