@@ -16,7 +16,8 @@
 //   0. waits until every peer it pushes to has finished reading the last LL
 //      call that used this parity (that peer's done word >= needDone) — the
 //      credit that makes a slot reusable even when a rank never waits for
-//      data (Reduce non-roots);
+//      data (Reduce non-roots); implied, and skipped, when the previous call
+//      took lines from every peer (llBegin);
 //   1. pushes its message, 8 bytes per thread, as two lines into slot
 //      [seq & 1][r] of each target's buffer (remote stores over xGMI):
 //        AllReduce      — the whole message to every peer
@@ -111,16 +112,24 @@ struct LLCall {
   uint32_t flag;
 };
 
-// The three state words are loaded together (one round trip, not two: the
-// previous launch on this stream wrote all of them before it completed).
+// The state words are loaded together (one round trip, not two: the previous
+// launch on this stream wrote all of them before it completed).
+// Implied credits: if the previous call took lines from every peer, each peer
+// had started ITS previous call, so (a communicator's calls run in order on
+// every rank) each peer had finished the call before that — the last one that
+// used this call's parity — and with it every read of the slots this call
+// overwrites. The explicit wait on the done words (needDone != 0) is then
+// skipped: one uncached round trip less per call in a run of AllReduce /
+// ReduceScatter calls. A Reduce non-root (it takes no lines) keeps the wait.
 __device__ __forceinline__ LLCall llBegin(const LLArgs& a) {
   LLCall c;
   const uint64_t s = __hip_atomic_load(&a.state->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t l0 = __hip_atomic_load(&a.state->lastSeq[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t l1 = __hip_atomic_load(&a.state->lastSeq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t ra = __hip_atomic_load(&a.state->recvAllSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   c.seq = s + 1;
   c.parity = (int)(c.seq & 1u);
-  c.needDone = c.parity ? l1 : l0;
+  c.needDone = (s != 0 && ra == s) ? 0 : (c.parity ? l1 : l0);
   c.flag = (uint32_t)c.seq;
   return c;
 }
@@ -179,13 +188,16 @@ __device__ __forceinline__ bool llPlanCheck(const LLArgs& a, const LLCall& c, in
 // counters), and the launch's last block publishes this rank's done word
 // (= seq) in every peer's buffer, advances the state for the next launch and
 // publishes the call's completion number (MpDone).
-__device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c) {
+// `receivedAll`: this launch took lines from every peer (llBegin's implied credits).
+__device__ __forceinline__ void llEnd(const LLArgs& a, const LLCall& c, bool receivedAll) {
   mpDrain();
   if (threadIdx.x != 0 || !mpLastBlock(a.order.arrive)) return;
   for (int j = 0; j < a.nRanks; j++) {
     if (j == a.rank) continue;
     __hip_atomic_store(a.peerLL[j] + a.doneOff + a.rank, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if (receivedAll)   // (after a failed call the communicator is broken until aborted, as in the reference)
+    __hip_atomic_store(&a.state->recvAllSeq, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&a.state->lastSeq[c.parity], c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&a.state->seq, c.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (nbx_order.h)
   mpPublish(a.order);
@@ -328,7 +340,7 @@ __global__ __launch_bounds__(256) void kLLColl(LLArgs a) {
     (void)llPlanCheck(a, call, threadIdx.x, t0);
 
   // done word: after every block of this launch has consumed its lines
-  llEnd(a, call);
+  llEnd(a, call, receives);
 }
 
 
@@ -580,7 +592,7 @@ __global__ __launch_bounds__(256) void kLL128Coll(LLArgs a) {
     (void)llPlanCheck(a, call, threadIdx.x, t0);
 
   // done word (as kLLColl)
-  llEnd(a, call);
+  llEnd(a, call, receives);
 }
 
 
@@ -707,7 +719,9 @@ __global__ __launch_bounds__(256) void kLL128AllReduce2(LLArgs a) {
   // every peer pushed its reduce-scatter lines here (both modes)
   if (CHECK && !failed && blockIdx.x == 0 && (int)threadIdx.x < n && (int)threadIdx.x != me)
     (void)llPlanCheck(a, call, threadIdx.x, t0);
-  llEnd(a, call);
+  uint64_t myOff, myLen;   // every peer pushes lines of a non-empty own block here
+  l128BlockRange(a, me, eb, &myOff, &myLen);
+  llEnd(a, call, myLen > 0);
 }
 
 }  // namespace nbx

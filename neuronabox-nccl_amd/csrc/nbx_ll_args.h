@@ -20,7 +20,7 @@ constexpr int kL128LanesHost = 4;       // lanes (16 bytes each) per LL128 line
 struct LLState {
   uint64_t seq;         // last completed LL-family call (the pending one is seq + 1)
   uint64_t lastSeq[2];  // last call that used each parity's slots (credit target)
-  uint64_t unused;
+  uint64_t recvAllSeq;  // last call in which this rank took lines from every peer
 };
 
 // Cross-stream order of one communicator's calls (nccl_api.cc runMpColl):
