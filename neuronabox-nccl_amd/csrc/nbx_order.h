@@ -26,10 +26,11 @@ namespace nbx {
 // signals). Caller buffers are the caller's to order across streams, as with
 // any kernel. A release here was an L2 write-back (`buffer_wbl2 sc1`) per
 // block and per step of the chain — four in the last block's path.
-// A one-block launch (a small Simple call) needs no arrival at all.
+// (A shortcut for one-block launches sped small Simple calls up but slowed the
+// LL kernels, which share this function, by ~0.5 us at 2 ranks: not taken,
+// profiles/r4/arrive_r4aj/.)
 __device__ __forceinline__ bool mpLastBlock(uint32_t* arrive) {
   const unsigned g = gridDim.x, x = blockIdx.x & 7u;
-  if (g == 1u) return true;
   const unsigned inGroup = (g - x + 7u) >> 3;   // blocks b < g with b % 8 == x
   const unsigned groups = g < 8u ? g : 8u;
   uint32_t* const mine = arrive + (size_t)x * kMpArriveStride;
