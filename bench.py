@@ -37,6 +37,17 @@ Extra JSON fields:
                  same shapes in the bench process, as the vendor reference.
                  NBX_BENCH_COLLECTIVE=0 skips all three, NBX_BENCH_CLIQUE=0 the
                  clique part, NBX_BENCH_RCCL=0 the RCCL part.
+
+The N > 1 legs share ONE wall budget, NBX_BENCH_LEG_BUDGET_S (default 240 s,
+so an 8-rank run stays well inside a 600 s driver limit): every leg's wait is
+drawn from what is left of it (rank 0's clock, broadcast, so every rank makes
+the same skip decision), a leg that no longer fits is skipped with the reason
+recorded, a leg that times out reports the last partial result its child
+printed, and a watchdog ends every rank at the budget (+ a grace) even if a
+leg hangs inside this process (RCCL). At N > 1 rank 0 prints the headline line
+(value, roofline) BEFORE the legs start and again, with `collective` filled
+in, when they end (or when the watchdog fires): a stall in never-on-xGMI code
+can cost the collective evidence, never the headline value.
 """
 from __future__ import annotations
 
@@ -47,11 +58,20 @@ import select
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+COLLECTIVE_SCRIPT = os.path.join(ROOT, "scripts", "collective_leg.py")
+CLIQUE_SCRIPT = os.path.join(ROOT, "scripts", "clique_leg.py")
+LEG_BUDGET_S = 240.0     # NBX_BENCH_LEG_BUDGET_S: every N > 1 leg together
+# a leg is skipped when less than this is left (and each leg keeps this much
+# for every leg after it); the watchdog fires this long after the budget
+LEG_MIN_S = float(os.environ.get("NBX_BENCH_LEG_MIN_S", "15"))
+WATCHDOG_GRACE_S = float(os.environ.get("NBX_BENCH_WATCHDOG_GRACE_S", "20"))
 
 N_SRCS = 8
 COUNT = 64 << 20                    # fp32 elements per 256 MiB input
@@ -113,6 +133,119 @@ def max_over_ranks(value: float, world: int) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class LegBudget:
+    """One wall budget shared by every N > 1 leg (NBX_BENCH_LEG_BUDGET_S)."""
+
+    def __init__(self, total: float | None = None, clock=time.monotonic):
+        if total is None:
+            total = float(os.environ.get("NBX_BENCH_LEG_BUDGET_S", LEG_BUDGET_S))
+        self.total = float(total)
+        self.clock = clock
+        self.t0 = clock()
+
+    def left(self) -> float:
+        return max(0.0, self.total - (self.clock() - self.t0))
+
+    def agreed_left(self, world: int) -> float:
+        """Rank 0's remaining budget, the same on every rank (one broadcast):
+        every rank then skips, or bounds, a leg alike."""
+        left = self.left()
+        if world > 1:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                box = [left]
+                dist.broadcast_object_list(box, src=0)
+                left = float(box[0])
+        return left
+
+
+def leg_timeout(default: float, left: float, reserve: float = 0.0) -> float:
+    """A leg's wait: its own default, capped by what is left of the budget
+    after `reserve` seconds kept for the legs that follow it."""
+    return max(0.0, min(default, left - reserve))
+
+
+def skipped_leg(left: float, what: str) -> dict:
+    return {"ok": False, "skipped": f"{what} skipped: {left:.0f} s of the leg budget left "
+                                    f"(NBX_BENCH_LEG_BUDGET_S), under the {LEG_MIN_S:.0f} s minimum"}
+
+
+class Emitter:
+    """Rank 0's JSON lines. The final line is printed once, by the main
+    thread when the legs end or by the watchdog when the budget runs out."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+        self.lock = threading.Lock()
+        self.final_done = False
+        self.result = None      # the headline result, once measured
+        self.coll = None        # the collective summary built so far
+        self.leg = None         # the leg running now (for the watchdog's reason)
+
+    def preliminary(self, result: dict) -> None:
+        if self.rank != 0:
+            return
+        line = dict(result)
+        line["collective"] = {"ok": None, "status": "pending: the N > 1 legs run after this line; "
+                                                    "the final line (same value) follows"}
+        with self.lock:
+            print(json.dumps(line), flush=True)
+
+    def final(self, result: dict, reason: str | None = None) -> None:
+        with self.lock:
+            if self.final_done:
+                return
+            self.final_done = True
+            if self.rank != 0:
+                return
+            line = dict(result)
+            if reason is not None:
+                coll = dict(self.coll or {})
+                coll["ok"] = False
+                coll.setdefault("errors", []).append(reason)
+                coll["incomplete"] = reason
+                line["collective"] = coll
+            print(json.dumps(line), flush=True)
+
+
+class Watchdog:
+    """Ends this rank when the leg budget (+ grace) is spent: rank 0 prints the
+    final line with what the legs produced so far and the reason, every rank
+    kills its own leg children (by PID) and exits 0 — the headline value
+    stands; `collective.ok` is false."""
+
+    def __init__(self, seconds: float, emitter: Emitter, children, exit_fn=None):
+        self.emitter = emitter
+        self.children = [c for c in children if c is not None]
+        self.exit_fn = exit_fn or (lambda: os._exit(0))
+        self.cancelled = threading.Event()
+        self.seconds = seconds
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        if self.cancelled.wait(self.seconds):
+            return
+        leg = self.emitter.leg or "the legs"
+        print(f"[bench rank {self.emitter.rank}] leg budget spent during {leg}; ending the run", file=sys.stderr,
+              flush=True)
+        if self.emitter.result is not None:
+            self.emitter.final(self.emitter.result,
+                               f"leg budget ({self.seconds:.0f} s incl. grace) spent during {leg}; "
+                               "the run was ended by the watchdog")
+        for c in self.children:
+            try:
+                c.kill()   # this rank's own child, by PID
+            except OSError:
+                pass
+        sys.stdout.flush()
+        sys.stderr.flush()
+        self.exit_fn()
+
+    def cancel(self):
+        self.cancelled.set()
 
 
 def _pmc_traffic():
@@ -281,7 +414,7 @@ def _spawn_collective_leg(world: int, script: str | None = None):
     """Start this rank's collective-leg child before the parent touches the GPU."""
     if world <= 1 or os.environ.get("NBX_BENCH_COLLECTIVE", "1") == "0":
         return None
-    script = script or os.path.join(ROOT, "scripts", "collective_leg.py")
+    script = script or COLLECTIVE_SCRIPT
     log = tempfile.NamedTemporaryFile(prefix=f"nbx_coll_leg_r{os.environ.get('RANK', '0')}_", suffix=".log",
                                       delete=False)
     child = subprocess.Popen([sys.executable, script],
@@ -297,28 +430,57 @@ def _spawn_clique_leg(world: int, rank: int, script: str | None = None):
     if (world <= 1 or rank != 0 or os.environ.get("NBX_BENCH_COLLECTIVE", "1") == "0"
             or os.environ.get("NBX_BENCH_CLIQUE", "1") == "0"):
         return None
-    return _spawn_collective_leg(world, script or os.path.join(ROOT, "scripts", "clique_leg.py"))
+    return _spawn_collective_leg(world, script or CLIQUE_SCRIPT)
 
 
-def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 400.0):
+def _close_child(child):
+    if child is None:
+        return
+    try:
+        child.stdin.close()
+    except OSError:
+        pass
+    try:
+        child.wait(timeout=5)
+    except subprocess.TimeoutExpired:
+        child.kill()   # this rank's own child, by PID
+        child.wait()
+
+
+def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 400.0,
+               budget: LegBudget | None = None):
     """Config D through ncclCommInitAll over every rank's GPU, run by rank 0's
     child while the other ranks wait on the host (the process group's store:
-    no RCCL kernel of theirs occupies a GPU meanwhile). Rank 0 gets the result."""
+    no RCCL kernel of theirs occupies a GPU meanwhile). Rank 0 gets the result.
+    With a budget the wait is capped by what is left of it (rank 0's clock)."""
     import datetime
     import torch.distributed as dist
+    if budget is not None:
+        left = budget.agreed_left(world)
+        if left < LEG_MIN_S:
+            if rank == 0:
+                _close_child(child)
+                return skipped_leg(left, "the clique leg")
+            return None
+        result_timeout = leg_timeout(result_timeout, left, reserve=LEG_MIN_S)
     devs = [None] * world
     dist.all_gather_object(devs, dev)
     store = dist.distributed_c10d._get_default_store()
     key = "nbx_clique_leg_done"
     if rank != 0:
-        store.wait([key], datetime.timedelta(seconds=result_timeout + 120))
+        try:
+            store.wait([key], datetime.timedelta(seconds=result_timeout + 10))
+        except Exception as e:   # rank 0 never set the key: its wait is bounded too; go on
+            print(f"[bench rank {rank}] clique leg: no completion from rank 0 ({type(e).__name__})",
+                  file=sys.stderr, flush=True)
         return None
     res = None
+    partial = None
     if child is not None:
         try:
             child.stdin.write(f"RUN {world} {','.join(str(d) for d in devs)}\n")
             child.stdin.flush()
-            line = _read_line(child, "RESULT", result_timeout)
+            line, partial = _read_line(child, "RESULT", result_timeout, partial=True)
             res = json.loads(line) if line else None
         except (OSError, ValueError):
             res = None
@@ -332,7 +494,8 @@ def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 4
             child.kill()   # rank 0's own child, by PID
             child.wait()
         if res is None:
-            res = {"ok": False, "errors": ["no result from the clique leg: " + _log_tail(child)]}
+            res = _partial_or_error(partial, f"no result from the clique leg within {result_timeout:.0f} s: "
+                                    + _log_tail(child))
     store.set(key, "1")
     if res is None:
         return None
@@ -343,6 +506,18 @@ def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 4
         if ms:
             alg = S / (ms * 1e-3) / 1e9
             res[name] = {"ms": round(ms, 4), "algbw_GBs": round(alg, 2), "busbw_GBs": round(alg * fac, 2)}
+    n, M = world, S
+    # local HBM rate per GPU: in-kernel entries on the staging
+    # model of the multi-process kernels (same kernels); the direct fold reads
+    # every rank's block in place (M) and writes its block into every output
+    # (M) / its own output (M / n) — model bytes, no PMC ratio measured
+    for name, model in (("allreduce", 2 * (M + 2 * (n - 1) * M // n)),
+                        ("reduce_scatter", 2 * (n - 1) * M // n + M + M // n),
+                        ("fold_allreduce", 2 * M), ("fold_reduce_scatter", M + M // n)):
+        e = res.get(name)
+        if isinstance(e, dict) and e.get("ms"):
+            e["hbm_model_bytes_per_rank"] = model
+            e["hbm_GBs_per_rank"] = round(model / (e["ms"] * 1e-3) / 1e9, 1)
     res["workload"] = ("config D through ncclCommInitAll (one process, every GPU of the run, no IPC), "
                        "ncclSum fp32 1 GiB per rank, checked exactly; allreduce / reduce_scatter on the in-kernel Simple transport over staging "
                        "(forced for every size), fold_* on the event-ordered direct fold (NBX_CLIQUE_SIMPLE=0; the "
@@ -350,11 +525,15 @@ def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 4
     return res
 
 
-def _read_line(child, prefix: str, timeout: float):
+def _read_line(child, prefix: str, timeout: float, partial: bool = False):
     """Next line of the child's stdout starting with `prefix`; a heartbeat goes
-    to stderr every 30 s while waiting (a long leg never looks hung)."""
+    to stderr every 30 s while waiting (a long leg never looks hung). With
+    `partial`, returns (line, last PARTIAL json the child printed meanwhile):
+    the legs print their results so far after every stage."""
     deadline = time.monotonic() + timeout
     t0 = time.monotonic()
+    last = None
+    found = None
     while time.monotonic() < deadline:
         r, _, _ = select.select([child.stdout], [], [], max(0.0, min(30.0, deadline - time.monotonic())))
         if not r:
@@ -365,10 +544,27 @@ def _read_line(child, prefix: str, timeout: float):
             break
         line = child.stdout.readline()
         if not line:
-            return None   # child exited
+            break   # child exited
+        if line.startswith("PARTIAL "):
+            try:
+                last = json.loads(line[len("PARTIAL "):])
+            except ValueError:
+                pass
+            continue
         if line.startswith(prefix + " "):
-            return line[len(prefix) + 1:].strip()
-    return None
+            found = line[len(prefix) + 1:].strip()
+            break
+    return (found, last) if partial else found
+
+
+def _partial_or_error(partial, reason: str) -> dict:
+    """A leg that gave no final result: its last partial result (if any),
+    marked failed, with the reason."""
+    res = dict(partial) if isinstance(partial, dict) else {}
+    res["ok"] = False
+    res["errors"] = list(res.get("errors") or []) + [reason]
+    res["incomplete"] = True
+    return res
 
 
 def _log_tail(child, n=5):
@@ -379,26 +575,39 @@ def _log_tail(child, n=5):
         return ""
 
 
-def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
-    """Drive the child through config D; every rank returns; rank 0 gets the summary."""
+def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0, budget: LegBudget | None = None,
+                   reserve: float = 0.0):
+    """Drive the child through config D; every rank returns; rank 0 gets the
+    summary. With a budget, the ID handshake and the run wait at most what is
+    left of it (rank 0's clock) minus `reserve` for the legs after this one."""
     import torch.distributed as dist
+    id_timeout = 180.0
+    if budget is not None:
+        left = budget.agreed_left(world)
+        if left - reserve < LEG_MIN_S:
+            _close_child(child)
+            return skipped_leg(left, "the collective leg") if rank == 0 else None
+        id_timeout = leg_timeout(id_timeout, left, reserve=reserve + LEG_MIN_S)
     ids = None
     if rank == 0:
         try:
             child.stdin.write("ID\n")
             child.stdin.flush()
-            ids = _read_line(child, "ID", 180)
+            ids = _read_line(child, "ID", id_timeout)
         except OSError:
             ids = None
     box = [ids]
     dist.broadcast_object_list(box, src=0)
     ids = box[0]
+    if budget is not None:
+        result_timeout = leg_timeout(result_timeout, budget.agreed_left(world), reserve=reserve)
     res = None
+    partial = None
     if ids is not None:
         try:
             child.stdin.write(f"RUN {ids}\n")
             child.stdin.flush()
-            line = _read_line(child, "RESULT", result_timeout)
+            line, partial = _read_line(child, "RESULT", result_timeout, partial=True)
             res = json.loads(line) if line else None
         except (OSError, ValueError):
             res = None
@@ -413,7 +622,10 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
         child.kill()   # this rank's own child, by PID
         child.wait()
     if not got:
-        res = {"rank": rank, "ok": False, "errors": ["no result from the collective leg: " + _log_tail(child)]}
+        why = ("no unique ids from rank 0's collective-leg child" if ids is None else
+               f"no result from the collective leg within {result_timeout:.0f} s")
+        res = _partial_or_error(partial, why + ": " + _log_tail(child))
+        res["rank"] = rank
     allres = [None] * world
     dist.all_gather_object(allres, res)
     if rank != 0:
@@ -422,6 +634,8 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     out = {"workload": "config D: 1 GiB fp32 per rank, ncclSum, one process per GPU, libnbxccl multi-process "
                        "communicator (TCP bootstrap, hipIpc peer buffers, device flags)",
            "n_ranks": world, "ok": all(r.get("ok") for r in allres),
+           # every rank pinned to one GPU (NBX_BENCH_DEVICE: a rehearsal, not xGMI)
+           "shared_gpu": "NBX_BENCH_DEVICE" in os.environ,
            "check": "exact (small-integer fp32 inputs), whole output, every rank"}
     errs = [f"rank {r.get('rank')}: {e}" for r in allres for e in r.get("errors", [])]
     if errs:
@@ -453,7 +667,50 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0):
     act = [r.get("ll128_active") for r in allres]
     out["ll128_active"] = None if any(a is None for a in act) else all(act)
     out["hbm_model"] = simple_hbm_model(world, S)
+    out["transport_allreduce"] = agg("transport_allreduce_ms", 2 * (world - 1) / world, S)
+    add_hbm_rates(out, world, S)
+    # LL128 forced across the fabric (NCCL_PROTO=LL128): every call checked
+    fc = [r.get("ll128_forced_checked_calls") for r in allres]
+    fm = [r.get("ll128_forced_mismatched_calls") for r in allres]
+    out["ll128_forced"] = (None if any(v is None for v in fc + fm) else
+                           {"checked_calls": sum(fc), "mismatched_calls": sum(fm), "per_rank_mismatched": fm,
+                            "what": "AllReduces on the NCCL_PROTO=LL128 communicator, one-shot 96 KiB and (n > 2) "
+                                    "two-shot 1 MiB, inputs changing per call, every output compared exactly"})
+    # connection buffers re-exported at creation (a wrong IPC mapping, verified before first use)
+    rep = [r.get("ipc_repairs") for r in allres]
+    out["ipc_repairs"] = (None if any(v is None for v in rep) else
+                          {k: sum((v.get(k) or 0) for v in rep) for k in ("direct", "ring")})
     return out
+
+
+def add_hbm_rates(out: dict, world: int, msg_bytes: int) -> None:
+    """the local HBM rate per GPU of each libnbxccl
+    entry = the staging design's HBM bytes per rank (simple_hbm_model; for
+    ReduceScatter and the transport-only call their own model) x the measured
+    HBM / model ratio of the same kernels (committed PMC passes; 1.0 where none
+    was measured) / the call's time. A model-derived rate, stated as such."""
+    n, M = world, msg_bytes
+    hm = out.get("hbm_model") or simple_hbm_model(world, msg_bytes)
+    ratio = hm.get("measured_over_model") or {}
+    models = {
+        # push (n-1) blocks + fold M + store and push the block n times + gather (n-1) blocks
+        "allreduce_direct": (2 * (M + 2 * (n - 1) * M // n), "direct"),
+        "allreduce_ring": (2 * (M + 2 * (n - 1) * M // n), "ring"),
+        # push (n-1) blocks, fold M, store one block
+        "reduce_scatter": (2 * (n - 1) * M // n + M + M // n, "direct"),
+        # as allreduce_direct without reading the n-1 staging slots of the fold
+        "transport_allreduce": (4 * (n - 1) * M // n + M // n + M, None),
+    }
+    for key, (model, rkey) in models.items():
+        e = out.get(key)
+        if not e or not e.get("ms"):
+            continue
+        r = ratio.get(rkey) if rkey else None
+        e["hbm_model_bytes_per_rank"] = model
+        e["hbm_over_model_applied"] = r if r else 1.0
+        e["hbm_GBs_per_rank"] = round(model * (r if r else 1.0) / (e["ms"] * 1e-3) / 1e9, 1)
+    out["hbm_rate_what"] = ("hbm_GBs_per_rank = staging-model HBM bytes per rank x measured HBM/model ratio "
+                            "(profiles/r4/simple_traffic_pmc_r4j.json; 1.0 where unmeasured) / call time")
 
 
 def simple_hbm_model(world: int, msg_bytes: int):
@@ -565,7 +822,7 @@ COUNT_D = 256 << 20   # config D: fp32 elements per rank (1 GiB)
 SWEEP_BYTES = [4 << 10, 32 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]   # = collective_leg.SWEEP_BYTES
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -573,14 +830,15 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--check", action="store_true", help="verify step output against the oracle (sampled)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    child = _spawn_collective_leg(int(os.environ.get("WORLD_SIZE", "1")))
-    clique_child = _spawn_clique_leg(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")))
+
+def headline(args, world: int, rank: int, local: int) -> dict:
+    """The timed region (config B on this rank's GPU), the roofline fields,
+    the same-process stream ceilings and, at N = 1, the host end-to-end leg.
+    Returns the result dict (collective / cpu_baseline still None); every
+    device buffer of this function is freed when it returns."""
     import torch
-    world, rank, local = _dist_init()
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     nbx = _load_package()
     nbx.load_library()
     dev = torch.device("cuda", local)
@@ -633,7 +891,6 @@ def main():
     value = world * ALG_BYTES / (wall / args.steps) / 2**30
 
     if args.check:
-        import numpy as np
         idx = torch.randint(0, COUNT, (1 << 16,), device=dev)
         ref = srcs[0][idx].clone()
         for s in srcs[1:]:
@@ -699,26 +956,59 @@ def main():
                               "frac_of_read_ceiling = achieved / max(read, copy)")
     if world == 1 and os.environ.get("NBX_BENCH_E2E", "1") != "0" and not args.no_cpu_baseline:
         result["host_e2e"] = host_e2e_leg(torch, nbx, srcs, out, stream, op)
+    del srcs, out
+    torch.cuda.empty_cache()
+    return result
+
+
+def run_legs(result: dict, world: int, rank: int, local: int, child, clique_child, emitter: Emitter,
+             budget: LegBudget) -> dict | None:
+    """The N > 1 legs inside one wall budget (module docstring); rank 0
+    returns the collective summary, the other ranks None."""
+    emitter.leg = "the collective leg"
+    # the multi-process leg may use what the clique and RCCL legs do not need
+    coll = collective_leg(child, world, rank, budget=budget, reserve=2 * LEG_MIN_S)
+    emitter.coll = coll
+    if os.environ.get("NBX_BENCH_CLIQUE", "1") != "0":
+        emitter.leg = "the clique leg"
+        cl = clique_leg(clique_child, world, rank, local, budget=budget)
+        if coll is not None:
+            coll["clique"] = cl
+    if os.environ.get("NBX_BENCH_RCCL", "1") != "0":
+        emitter.leg = "the RCCL leg"
+        left = budget.agreed_left(world)
+        rccl = rccl_leg(world) if left >= LEG_MIN_S else skipped_leg(left, "the RCCL leg")
+        if coll is not None:
+            coll["rccl"] = rccl
+            coll["vs_rccl"] = vs_rccl(coll, rccl)
+    emitter.leg = None
+    if coll is not None:
+        coll["leg_budget"] = {"budget_s": budget.total, "used_s": round(budget.total - budget.left(), 1)}
+    return coll
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    child = _spawn_collective_leg(env_world)
+    clique_child = _spawn_clique_leg(env_world, int(os.environ.get("RANK", "0")))
+    import torch
+    world, rank, local = _dist_init()
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    emitter = Emitter(rank)
+    result = headline(args, world, rank, local)
+    emitter.result = result
     if child is not None:
-        del srcs, out
-        torch.cuda.empty_cache()
-        coll = collective_leg(child, world, rank)
-        if os.environ.get("NBX_BENCH_CLIQUE", "1") != "0":
-            cl = clique_leg(clique_child, world, rank, local)
-            if coll is not None:
-                coll["clique"] = cl
-        if os.environ.get("NBX_BENCH_RCCL", "1") != "0":
-            rccl = rccl_leg(world)
-            if coll is not None:
-                coll["rccl"] = rccl
-                coll["vs_rccl"] = vs_rccl(coll, rccl)
-        result["collective"] = coll
+        # the headline first: whatever the legs do, the value is on stdout
+        emitter.preliminary(result)
+        budget = LegBudget()
+        wd = Watchdog(budget.total + WATCHDOG_GRACE_S, emitter, [child, clique_child])
+        result["collective"] = run_legs(result, world, rank, local, child, clique_child, emitter, budget)
+        wd.cancel()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if child is None:
-            del srcs, out
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    emitter.final(result)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

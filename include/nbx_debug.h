@@ -43,10 +43,19 @@ int nbxDebugProtoMask(const char* ncclProto);
 int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
                         uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax);
 
+/* The protocol set a communicator starts from for NCCL_PROTO = ncclProto
+ * (NULL: unset) when its ranks span more than one GPU (multiGpu = 1) or share
+ * one: across GPUs LL128 is left out unless NCCL_PROTO names it (not in a
+ * "^list") or NBX_LL128_ACROSS_GPUS=1 — the reference enables LL128 by default
+ * only on validated fabrics (tuning.cc:287-297). NBX_DEBUG_ASSUME_MULTI_GPU=1
+ * (test hook) applies the gate to ranks sharing a GPU. */
+int nbxDebugGatedProtoMask(const char* ncclProto, int multiGpu);
+
 /* The protocol set a communicator runs with (bits as nbxDebugProtoMask): its
- * NCCL_PROTO at creation, minus LL128 if the creation-time LL128 self-test
- * failed (multi-process communicators; -1 for others or a bad handle).
- * NBX_LL128_SELFTEST_FAIL=1 makes that self-test report a failure (test hook). */
+ * NCCL_PROTO at creation gated as nbxDebugGatedProtoMask, minus LL128 if the
+ * creation-time LL128 self-test failed (multi-rank communicators and clique
+ * ranks; -1 for others or a bad handle). NBX_LL128_SELFTEST_FAIL=1 makes that
+ * self-test report a failure (test hook). */
 int nbxDebugCommProtoMask(ncclComm_t comm);
 
 /* The transport settings a communicator runs with (after NCCL_BUFFSIZE /
@@ -55,10 +64,20 @@ int nbxDebugCommProtoMask(ncclComm_t comm);
  * out[0] LL max bytes, [1] LL128 max bytes, [2] Simple slice bytes, [3] Simple
  * slots, [4] Simple grid, [5] LL grid cap, [6] LL128 grid cap, [7] group
  * batching, [8] connection buffers re-exported at creation because a peer's
- * IPC mapping of them showed other memory (verified before first use). Writes
- * min(nOut, 9) values and returns that count; -1 for a bad handle or a
+ * IPC mapping of them showed other memory (verified before first use), [9]
+ * plan checks on (NBX_CHECK_PLANS / NCCL_CHECK_POINTERS). Writes
+ * min(nOut, 10) values and returns that count; -1 for a bad handle or a
  * communicator without a multi-rank transport. */
 int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut);
+
+/* Config D's xGMI transport alone, on a multi-process
+ * communicator: an AllReduce-shaped call of the direct Simple schedule (forced
+ * for any size and NCCL_ALGO) that moves every byte an AllReduce of `count`
+ * elements moves between the ranks, with the fold reduced to a copy of the
+ * own input; recvbuff receives junk. Collective (every rank, same count and
+ * datatype), stream-ordered like ncclAllReduce. Measurement only. */
+ncclResult_t nbxDebugTransportAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                        ncclComm_t comm, ncclStream_t stream);
 
 /* Stream ceilings in the caller's process (SURVEY §8(d) "a measured stream
  * ceiling"): kind 0 reads nSrcs == 8 buffers of `bytes` each with the hot

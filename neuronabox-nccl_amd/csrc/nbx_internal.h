@@ -53,6 +53,7 @@ ncclResult_t launchMpWaitDone(const uint64_t* done, uint64_t target, const volat
 // Every rank of the one-process Simple rig in one dispatch (fp32 sum; PMC
 // measurement only, nbx_simple_bench.cc): n x grid workgroups, argsDev[n].
 ncclResult_t launchSimpleFusedF32Sum(const SimpleArgs* argsDev, int n, unsigned grid, bool ring, hipStream_t stream);
+int simpleFusedMaxResident(bool ring);   // workgroups of kSimpleFused resident at once (-1: HIP error)
 // LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
                                    hipStream_t stream);

@@ -141,7 +141,12 @@ inline uint32_t llPlanSig(const LLArgs& a, int32_t proto, int32_t dtype, int32_t
 //   rsRecv  / flag rsCredit : RS-region slices this rank consumed from the peer / the peer consumed from here
 //   agSent  / flag agReady  : the same for the AG region
 //   agRecv  / flag agCredit
-enum SimpleMode : int32_t { kSimpleAllReduce = 0, kSimpleReduceScatter = 1, kSimpleReduce = 2 };
+// kSimpleTransport (measurement only, nbxDebugTransportAllReduce): the direct
+// AllReduce schedule moving every byte it moves across the peers (pushes,
+// gather) with the fold reduced to a copy of the own input — the staging
+// slots are waited for and credited, not read — so its time is the xGMI
+// transport alone; its output is not the sum.
+enum SimpleMode : int32_t { kSimpleAllReduce = 0, kSimpleReduceScatter = 1, kSimpleReduce = 2, kSimpleTransport = 3 };
 enum SimpleAlgo : int32_t { kSimpleAlgoDirect = 0, kSimpleAlgoRing = 1 };
 // flag words (written by the peer named by their index)
 enum SimpleFlag : int32_t { kFlRsReady = 0, kFlRsCredit = 1, kFlAgReady = 2, kFlAgCredit = 3 };

@@ -63,6 +63,20 @@ ncclResult_t launchSimpleFusedF32Sum(const SimpleArgs* argsDev, int n, unsigned 
                        argsDev, (int)grid);
   return hipGetLastError() == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
 }
+
+// Workgroups of the fused Simple kernel the current device holds at once
+// (occupancy x CUs): workgroup g of one rank spins on workgroup g of its
+// peers, so a fused grid larger than this would wait for workgroups that are
+// never scheduled; -1 on a HIP error.
+int simpleFusedMaxResident(bool ring) {
+  int dev = 0, cus = 0, perCu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1;
+  const void* fn = ring ? (const void*)&kSimpleFused<FnSumF<TyF32>, true> : (const void*)&kSimpleFused<FnSumF<TyF32>, false>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, fn, kBlock, 0) != hipSuccess) return -1;
+  return perCu * cus;
+}
 }  // namespace nbx
 
 extern "C" __attribute__((visibility("default"))) int nbxDebugLL128TearTest(int delayUs, int tear,

@@ -398,7 +398,9 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
   __shared__ SimpleShared sh;
   simpleLoadCounters(a, sh, g);
   uint64_t* const myFlags = a.peerFlags[me];
-  const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce, rs = a.mode == kSimpleReduceScatter;
+  const bool xport = a.mode == kSimpleTransport;   // AllReduce traffic, no fold (measurement)
+  const bool ar = a.mode == kSimpleAllReduce || xport, red = a.mode == kSimpleReduce,
+             rs = a.mode == kSimpleReduceScatter;
   const bool storeLocal = !red || me == a.root;        // B writes this rank's output block
   const bool gathers = ar || (red && me == a.root);    // C runs here
   const int first = ((red ? a.root : me) + 1) % n;      // fold order of block `me`
@@ -462,8 +464,10 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
       // destination 0 is the caller's output unless a Reduce non-root pushes to the root
       const uint64_t sysMask = storeLocal ? ~1ull : ~0ull;
       // every source but the own input (at fold position (me - first) mod n) is staging
-      const uint64_t sysSrc = ~(1ull << ((me - first + n) % n));
-      simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
+      const int ownPos = (me - first + n) % n;
+      const uint64_t sysSrc = ~(1ull << ownPos);
+      if (xport) simpleFold<Fn>(fn, sh.src + ownPos, 1, 0ull, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
+      else simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
     }
     if (tid < n && pushTarget(tid))
       simpleStamp(simpleHdr(a, tid, 1, sh.cnt[kCtAgSent][tid] % slots, me, g), a, sh.cnt[kCtAgSent][tid] + 1);

@@ -149,6 +149,9 @@ extern "C" __attribute__((visibility("default"))) int nbxDebugSimpleRun(
   nbx::SimpleArgs* argsDev = nullptr;
   if (fused) {
     if (datatype != 7 || opFull.op != nbxDevSum || (uint64_t)n * grid > 2048) return ncclInvalidArgument;
+    // every workgroup of the one dispatch must be resident at once (they wait on each other)
+    const int resident = nbx::simpleFusedMaxResident(ring != 0);
+    if (resident < 0 || (uint64_t)n * grid > (uint64_t)resident) return ncclInvalidArgument;
     for (auto& sa : args) {
       sa.arg = 0;
       sa.argPtr = nullptr;

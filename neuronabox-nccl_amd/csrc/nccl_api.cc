@@ -840,6 +840,28 @@ int protoFromString(const char* v) {
 }
 int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
 
+// LL128 across GPUs is enabled by default only where it was validated — the
+// reference's rule (tuning.cc:250-297: protoEnable[LL128] = 2 "default", and
+// parseList turns it into 1 only when NCCL_PROTO lists LL128; a "^list"
+// leaves it at 2). LL128 trusts a 64-byte line written by one store to arrive
+// whole; within one GPU that was stress-tested, over xGMI it has
+// not been, so ranks on different GPUs drop LL128 from the default set until a
+// node run validates it (DESIGN §6 states the flip rule). It stays on when
+// NCCL_PROTO names it explicitly, or with NBX_LL128_ACROSS_GPUS=1.
+// NBX_DEBUG_ASSUME_MULTI_GPU=1 (test hook) applies this gate to ranks that
+// share a GPU, and nothing else of the multi-GPU settings.
+long envLong(const char* name, long dflt);
+bool protoLL128Explicit(const char* v) {
+  if (v == nullptr || *v == 0 || v[0] == '^') return false;
+  return (protoFromString(v) & kProtoLL128) != 0;
+}
+int protoGateAcrossGpus(int mask, bool multiGpu, const char* ncclProto) {
+  const bool assume = envLong("NBX_DEBUG_ASSUME_MULTI_GPU", 0) != 0;
+  if (!(multiGpu || assume) || protoLL128Explicit(ncclProto)) return mask;
+  if (envLong("NBX_LL128_ACROSS_GPUS", 0) != 0) return mask;
+  return mask & ~kProtoLL128;
+}
+
 // Per message: LL up to the LL max; LL128 up to the LL128 max: one-shot (every
 // rank pushes the whole message to every target), for AllReduce / Reduce with
 // more than 2 ranks only up to the one-shot max and the two-shot AllReduce /
@@ -887,7 +909,8 @@ long envLong(const char* name, long dflt) {
 //   NCCL_BUFFSIZE       Simple connection buffer per (peer, channel): the
 //                       Simple staging per (peer, workgroup, region) is
 //                       slots x slice, so slice = NCCL_BUFFSIZE / slots
-//                       (NBX_SIMPLE_SLICE_BYTES);
+//                       (NBX_SIMPLE_SLICE_BYTES) — only below the 64 KiB
+//                       default (mpTransportSettings);
 //   NCCL_LL_BUFFSIZE    LL buffer: half of every 8-byte line is flag, so LL
 //                       carries messages up to NCCL_LL_BUFFSIZE / 2 (NBX_LL_MAX_BYTES);
 //   NCCL_LL128_BUFFSIZE LL128 buffer: 48 payload bytes per 64-byte line, so
@@ -1083,7 +1106,20 @@ void mpTransportSettings(MpState* mp, int minCus, int maxShare) {
   }
   mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
   mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
-  long sl = ncclEnvMapped("NBX_SIMPLE_SLICE_BYTES", "NCCL_BUFFSIZE", 64 << 10, 1, mp->slots);
+  // NCCL_BUFFSIZE is the reference's buffer per (peer, channel) and its own
+  // default is 4 MiB, which job scripts often set explicitly; here it would
+  // become a 1 MiB slice per (peer, workgroup, region, slot) — 4 GiB of staging
+  // at 8 ranks. So it is honoured only where it LOWERS the slice
+  // below the 64 KiB default (a memory cap, its use in the reference); an
+  // explicit NBX_SIMPLE_SLICE_BYTES sets the slice (16 B .. 1 MiB) as asked.
+  long sl = envLong("NBX_SIMPLE_SLICE_BYTES", 0);
+  if (sl <= 0) {
+    sl = 64 << 10;
+    const long bs = envLong("NCCL_BUFFSIZE", 0);
+    if (bs > 0 && bs / mp->slots < sl) sl = bs / mp->slots;
+    else if (bs > 0)
+      info("NCCL_BUFFSIZE=%ld ignored: the Simple slice stays %ld bytes (only smaller buffers are honoured)", bs, sl);
+  }
   sl = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(sl, 1 << 20));
   mp->sliceBytes = (uint64_t)(sl + 15) & ~(uint64_t)15;
   if (const char* nt = std::getenv("NCCL_NTHREADS"); nt && *nt && std::atol(nt) != 256)
@@ -1304,6 +1340,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   }
   mpTransportSettings(mp, minCus, maxShare);
   NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true, c));
+  mp->protoMask = protoGateAcrossGpus(mp->protoMask, mp->multiGpu, std::getenv("NCCL_PROTO"));   // before the settings are compared
   NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/true));
   HIPCHECK(hipDeviceSynchronize());   // zeroed before any peer can map and write them
 
@@ -1493,7 +1530,7 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
 // numbers from the same arguments. Several calls of one group (nc > 1, same
 // kind / type / op / root) run as ONE launch: block b of the launch is block
 // b of every message in turn (SimpleSeg), cut into the launch's slices.
-ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc) {
+ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc, bool transport = false) {
   MpState* mp = mpOf(comm);
   const MpCall& c = calls[0];
   const int n = comm->nRanks, me = comm->rank;
@@ -1554,7 +1591,8 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc) {
   sa.timeoutTicks = (uint64_t)(mp->timeoutSec * 1.0e8);
   sa.rank = me;
   sa.nRanks = n;
-  sa.mode = c.kind == kAllReduce ? nbx::kSimpleAllReduce
+  sa.mode = transport                  ? nbx::kSimpleTransport
+            : c.kind == kAllReduce     ? nbx::kSimpleAllReduce
             : c.kind == kReduceScatter ? nbx::kSimpleReduceScatter
                                        : nbx::kSimpleReduce;
   sa.root = c.root;
@@ -1564,7 +1602,7 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc) {
   sa.hdrOff = mp->stageHdrOff;
   sa.planSig = mp->checkPlans ? nbx::simplePlanSig(sa, (uint32_t)grid, (int32_t)c.dt, c.op.op) : 0;
   sa.order = mpOrderArgs(mp);
-  return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring, c.stream);
+  return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring && !transport, c.stream);
 }
 
 // One call of a multi-process communicator, ordered after the previous one:
@@ -1751,16 +1789,20 @@ thread_local std::vector<ncclComm*> t_groupMpComms;
 // segments of one launch run concurrently, so such a chain (AllReduce a->b,
 // then b->c) must stay separate launches, in order. That cut looks at this
 // rank's own buffers; the ranks of an SPMD program alias alike and cut alike.
-// A group whose calls alias differently on different ranks is outside what
-// the batching supports (LL / LL128 ranks then time out waiting for lines
-// that never come; Simple ranks could fold misplaced slices):
+// A Reduce never joins a run: its recv buffer is written on the root only (a
+// non-root may even pass NULL), so a cut that looked at it would split the
+// root's run where the non-roots batch theirs — every rank runs
+// each grouped Reduce as its own launch instead, a rule every rank evaluates
+// alike. A group whose AllReduce / ReduceScatter calls alias differently on
+// different ranks is outside what the batching supports (LL / LL128 ranks then
+// time out waiting for lines that never come; Simple ranks could fold
+// misplaced slices; NBX_CHECK_PLANS=1 makes both fail loudly, naming the peer):
 // NBX_GROUP_BATCH=0 runs every grouped call as its own kernel, in order.
-void mpCallSpans(const MpCall& c, int n, int rank, std::vector<Span>* out) {
+void mpCallSpans(const MpCall& c, int n, std::vector<Span>* out) {
   const size_t eb = (size_t)typeSize(c.dt);
   const size_t sendBytes = (c.kind == kReduceScatter ? c.count * (size_t)n : c.count) * eb;
   out->push_back({(uintptr_t)c.send, (uintptr_t)c.send + sendBytes, false});
-  if (c.recv != nullptr && (c.kind != kReduce || rank == c.root))
-    out->push_back({(uintptr_t)c.recv, (uintptr_t)c.recv + c.count * eb, true});
+  if (c.recv != nullptr) out->push_back({(uintptr_t)c.recv, (uintptr_t)c.recv + c.count * eb, true});
 }
 
 ncclResult_t runMpGroup(ncclComm* comm) {
@@ -1787,14 +1829,14 @@ ncclResult_t runMpGroup(ncclComm* comm) {
       size_t j = i + 1;
       const MpProto p = calls[i].count > 0 ? mpProtoOf(comm, calls[i]) : kMpSimple;
       const size_t maxSegs = p == kMpSimple ? (size_t)nbx::kSimpleMaxSegs : (size_t)nbx::kLLMaxSegs;
-      if (mp->groupBatch && (p == kMpLL || p == kMpLL128 || p == kMpSimple)) {
+      if (mp->groupBatch && calls[i].kind != kReduce && (p == kMpLL || p == kMpLL128 || p == kMpSimple)) {
         uint64_t used = p == kMpSimple ? 0 : unitsOf(calls[i], p);
         std::vector<Span> spans, sj;
-        mpCallSpans(calls[i], comm->nRanks, comm->rank, &spans);
+        mpCallSpans(calls[i], comm->nRanks, &spans);
         while (j < calls.size() && j - i < maxSegs && calls[j].count > 0 && sameOp(calls[i], calls[j]) &&
                mpProtoOf(comm, calls[j]) == p && (p == kMpSimple || used + unitsOf(calls[j], p) <= capOf(p))) {
           sj.clear();
-          mpCallSpans(calls[j], comm->nRanks, comm->rank, &sj);
+          mpCallSpans(calls[j], comm->nRanks, &sj);
           if (spansConflict(spans, sj)) break;
           spans.insert(spans.end(), sj.begin(), sj.end());
           if (p != kMpSimple) used += unitsOf(calls[j], p);
@@ -1867,6 +1909,7 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
     cl->comms[r]->lt = mp;
     NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/false, cl->comms[r]));
     mp->multiGpu = distinct;
+    mp->protoMask = protoGateAcrossGpus(mp->protoMask, mp->multiGpu, std::getenv("NCCL_PROTO"));
     mp->ring = algoRingFromEnv();
     mpTransportSettings(mp, minCus, maxShare);   // co-resident grids, as mpInit
     if (simple) NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/false));
@@ -2528,6 +2571,13 @@ NBX_API(ncclResult_t, ncclGroupEnd) {
 
 NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
 
+// The protocol set a communicator starts from (before its LL128 self-test):
+// NCCL_PROTO = ncclProto, its ranks on more than one GPU or not (the LL128
+// gate above; NBX_LL128_ACROSS_GPUS and NBX_DEBUG_ASSUME_MULTI_GPU apply).
+NBX_EXPORT int nbxDebugGatedProtoMask(const char* ncclProto, int multiGpu) {
+  return protoGateAcrossGpus(protoFromString(ncclProto), multiGpu != 0, ncclProto);
+}
+
 NBX_EXPORT int nbxDebugCommProtoMask(ncclComm_t comm) {
   if (comm == nullptr || comm->magic != kCommMagic || mpOf(comm) == nullptr) return -1;
   return mpOf(comm)->protoMask;   // a clique rank: its in-process transport's
@@ -2552,6 +2602,29 @@ NBX_EXPORT int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut) {
   int k = 0;
   for (; k < nOut && k < 10; k++) out[k] = v[k];
   return k;
+}
+
+// Config D's transport alone: an AllReduce-shaped call of the
+// direct Simple schedule on a multi-process communicator that moves every
+// byte the AllReduce moves between the ranks (pushes into the peers' staging,
+// the finished blocks into theirs, the gather) with the fold reduced to a copy
+// of the own input (kSimpleTransport). Collective: every rank calls it with
+// the same count and datatype. recvbuff receives junk. Measurement only.
+NBX_EXPORT ncclResult_t nbxDebugTransportAllReduce(const void* sendbuff, void* recvbuff, size_t count,
+                                                  ncclDataType_t datatype, ncclComm_t comm, ncclStream_t stream) {
+  NCCLCHECK(commCheck(comm, "TransportAllReduce"));
+  NCCLCHECK(commEnsureReady(comm));
+  if (comm->mp == nullptr || typeSize(datatype) < 0 || count == 0 || sendbuff == nullptr || recvbuff == nullptr)
+    return ncclInvalidArgument;
+  DevGuard g(comm->device);
+  const MpCall call{kAllReduce, sendbuff, recvbuff, count, datatype, nbxDevRedOpFull{nbxDevSum, 0, 0}, 0,
+                    (hipStream_t)stream};
+  try {
+    return runMpOrdered(comm, call.stream, [&]() { return mpLaunchSimple(comm, &call, 1, /*transport=*/true); });
+  } catch (const std::exception& e) {
+    warn("internal exception: %s", e.what());
+    return ncclInternalError;
+  }
 }
 
 NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,

@@ -13,6 +13,9 @@ talks over stdin/stdout:
   child  -> parent  "ID <hex> x6\\n"      ncclUniqueIds: direct, ring, and the LL / LL128 /
                                          LL128-one-shot / Simple comms of the protocol sweep
   parent -> child   "RUN <hex> x6\\n"     (every rank, after the parent's broadcast)
+  child  -> parent  "PARTIAL <json>\\n"    (after every stage: the results so far; the
+                                         parent reports the last one if the leg runs out
+                                         of its time budget)
   child  -> parent  "RESULT <json>\\n"
 
 Inputs are small integers in fp32 (x_r[i] = (7 i + 13 r) mod 1024), so every
@@ -47,9 +50,21 @@ def _emit(line: str) -> None:
     sys.stdout.flush()
 
 
-def _progress(msg: str) -> None:   # to this rank's leg log (stderr); its tail is reported on failure
+def _progress(msg: str, res: dict | None = None) -> None:
+    """To this rank's leg log (stderr; its tail is reported on failure) and,
+    with `res`, the results so far to the parent (a PARTIAL line)."""
     sys.stderr.write(f"[leg {time.strftime('%H:%M:%S')}] {msg}\n")
     sys.stderr.flush()
+    if res is not None:
+        _emit("PARTIAL " + json.dumps(dict(res, stage=msg)))
+
+
+def _ipc_repairs(lib, comm) -> int | None:
+    """Connection buffers this communicator re-exported at creation because a
+    peer's IPC mapping of them showed other memory (nbxDebugCommSettings[8])."""
+    import ctypes
+    vals = (ctypes.c_int64 * 10)()
+    return int(vals[8]) if lib.nbxDebugCommSettings(comm.handle, vals, 10) >= 9 else None
 
 
 def _pkg():
@@ -134,10 +149,47 @@ def protocol_sweep(ids, rank, world, st, shared_gpu, res):
             times.append(round(1e3 * _time_calls(lambda: c.all_reduce(x.data_ptr(), y.data_ptr(), n, 7, 0, st),
                                                  iters), 2))
         res["sweep_" + name + "_us"] = times
+        if name == "LL128":
+            ll128_stress(c, rank, world, st, res)
         if c.async_error() != 0:
             res["ok"] = False
             res["errors"].append(f"sweep {name}: async error")
         c.destroy()
+
+
+LL128_STRESS_CALLS = 1000   # per size: one-shot and (n > 2) two-shot -> >= 2000 calls
+
+
+def ll128_stress(c, rank, world, st, res):
+    """The 64-byte LL128 line across the fabric (LL128 is off by
+    default across GPUs until a node run shows it whole): LL128_STRESS_CALLS
+    AllReduces per size on the NCCL_PROTO=LL128 communicator (LL128 forced, its
+    creation-time probe passed), inputs changing every call, every output
+    compared exactly on the GPU. Sizes: 96 KiB (one-shot) and, with more than 2
+    ranks, 1 MiB (two-shot above the 256 KiB one-shot limit); at 2 ranks 1 MiB
+    is one-shot too. A torn line would show as a wrong element."""
+    import torch
+    calls = bad = 0
+    sizes = {"oneshot": 24 << 10, "twoshot" if world > 2 else "oneshot_1MiB": 256 << 10}
+    for label, n in sizes.items():
+        idx = torch.arange(n, dtype=torch.int32, device="cuda")
+        base = ((idx * 11 + 5 * rank) % 1000).to(torch.float32)
+        want0 = sum(((idx * 11 + 5 * r) % 1000).to(torch.float32) for r in range(world))
+        y = torch.empty(n, dtype=torch.float32, device="cuda")
+        wrong = 0
+        for it in range(LL128_STRESS_CALLS):
+            k = float(it % 113)
+            xi = base + k
+            c.all_reduce(xi.data_ptr(), y.data_ptr(), n, 7, 0, st)
+            if not torch.equal(y, want0 + world * k):
+                wrong += 1
+        calls += LL128_STRESS_CALLS
+        bad += wrong
+        if wrong:
+            res["ok"] = False
+            res["errors"].append(f"ll128 forced stress {label} ({4 * n} B): {wrong} of {LL128_STRESS_CALLS} calls wrong")
+    res["ll128_forced_checked_calls"] = calls
+    res["ll128_forced_mismatched_calls"] = bad
 
 
 def run(ids, rank, world, dev):
@@ -170,14 +222,20 @@ def run(ids, rank, world, dev):
             bad = int((got != want).sum().item())
             res["errors"].append(f"{name}: {bad} elements differ")
 
-    _progress("communicators ready")
-    # LL128 survives the creation-time probe on this fabric (bit 1 of the comm's protocol set)
+    # LL128 in the default protocol set (bit 1): off by default across GPUs
+    # (nccl_api.cc protoGateAcrossGpus), and dropped by the creation-time probe
+    # if it saw a torn line
     import ctypes
     lib = nbx.load_library()
     lib.nbxDebugCommProtoMask.argtypes = [ctypes.c_void_p]
     lib.nbxDebugCommProtoMask.restype = ctypes.c_int
+    lib.nbxDebugCommSettings.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    lib.nbxDebugTransportAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                               ctypes.c_void_p, ctypes.c_void_p]
     res["proto_mask"] = int(lib.nbxDebugCommProtoMask(comm.handle))
     res["ll128_active"] = bool(res["proto_mask"] & 2)
+    res["ipc_repairs"] = {"direct": _ipc_repairs(lib, comm), "ring": _ipc_repairs(lib, comm_ring)}
+    _progress("communicators ready", res)
     for name, c in (("allreduce_direct", comm), ("allreduce_ring", comm_ring)):
         y.zero_()
         c.all_reduce(x.data_ptr(), y.data_ptr(), COUNT, F32, SUM, st)
@@ -196,6 +254,17 @@ def run(ids, rank, world, dev):
         comm.reduce_scatter(x.data_ptr(), yr.data_ptr(), rc, F32, SUM, st)
     res["reduce_scatter_ms"] = _time_calls(lambda: comm.reduce_scatter(x.data_ptr(), yr.data_ptr(), rc, F32, SUM, st),
                                            ITERS)
+    # the xGMI transport alone — the direct AllReduce schedule's
+    # pushes and gather of the same 1 GiB with the fold reduced to a copy
+    # (nbxDebugTransportAllReduce); its output is junk, y is rewritten below
+    def xport():
+        rc_ = lib.nbxDebugTransportAllReduce(x.data_ptr(), y.data_ptr(), COUNT, F32, comm.handle, st)
+        if rc_ != 0:
+            raise RuntimeError(f"nbxDebugTransportAllReduce: {rc_}")
+    xport()
+    torch.cuda.synchronize()
+    res["transport_allreduce_ms"] = _time_calls(xport, ITERS)
+    _progress("config D timed", res)
 
     # Simple path with inputs that change every call (direct and ring schedules,
     # 32 MiB): catches any stale peer data a cache could serve across calls
@@ -214,10 +283,12 @@ def run(ids, rank, world, dev):
             res["errors"].append(f"simple_{name}_stress: {bad} of {SIMPLE_STRESS_ITERS} calls wrong")
     res["simple_stress_checked_calls"] = 2 * SIMPLE_STRESS_ITERS
     del xs_, es_, ys_
-    _progress("config D done")
-    # LL128 (1 MiB): exact on every one of LL128_ITERS calls with inputs that
-    # change per call (a torn line or a stale slot would show up as a
-    # wrong value), then the per-call latency
+    _progress("config D done", res)
+    # 1 MiB on the default protocol set (LL128 on one GPU; across GPUs LL128
+    # is off by default, so Simple carries it there): exact on every one of
+    # LL128_ITERS calls with inputs that change per call (a torn line or a
+    # stale slot would show up as a wrong value), then the per-call latency
+    # (LL128 forced across GPUs: ll128_stress in the protocol sweep)
     x1 = x[:LL128_COUNT].clone()
     e1 = exp[:LL128_COUNT]
     y1 = torch.empty(LL128_COUNT, dtype=torch.float32, device="cuda")
@@ -246,11 +317,11 @@ def run(ids, rank, world, dev):
 
     del x, y, yr, exp, x1, e1, y1, xs, ys
     torch.cuda.empty_cache()
-    _progress("LL / LL128 done")
+    _progress("LL / LL128 done", res)
     config_e(comm, rank, world, st, res)
-    _progress("config E done")
+    _progress("config E done", res)
     protocol_sweep(ids[2:6], rank, world, st, "NBX_BENCH_DEVICE" in os.environ, res)
-    _progress("protocol sweep done")
+    _progress("protocol sweep done", res)
 
     torch.cuda.synchronize()
     if comm.async_error() != 0 or comm_ring.async_error() != 0:

@@ -706,6 +706,29 @@ def test_multiprocess_ll128_selftest(nbx, monkeypatch, n, fail):
         assert mask == (5 if fail else 7), (r, mask)   # LL|Simple after a failed probe, else all three
 
 
+@pytest.mark.parametrize("proto,override,want", [("", "", 5), ("LL128,LL,Simple", "", 7), ("", "1", 7)])
+def test_multiprocess_ll128_gate_across_gpus(nbx, monkeypatch, proto, override, want):
+    """Ranks that report different GPUs (NBX_DEBUG_ASSUME_MULTI_GPU=1: the gate
+    only, not the grid split) start without LL128, as the reference enables
+    LL128 by default only on validated fabrics (tuning.cc:287-297): the
+    LL128-sized calls run on Simple, exact. NCCL_PROTO naming LL128, or
+    NBX_LL128_ACROSS_GPUS=1, keeps it (and its creation-time probe runs)."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
+    monkeypatch.setenv("NBX_DEBUG_ASSUME_MULTI_GPU", "1")
+    monkeypatch.setenv("NCCL_PROTO", proto)
+    monkeypatch.setenv("NBX_LL128_ACROSS_GPUS", override)
+    monkeypatch.setenv("NBX_LL128_SELFTEST_ITERS", "4")
+    monkeypatch.delenv("NCCL_ALGO", raising=False)
+    monkeypatch.delenv("NBX_LL128_SELFTEST_FAIL", raising=False)
+    res = _run_ranks(nbx, 3, _child_selftest)
+    for r in range(3):
+        mask, bad = res[r]
+        assert bad == 0, (r, bad)
+        assert mask == want, (r, mask)
+
+
 def _child_abort(uid_bytes, rank, q, evq):
     try:
         import threading
@@ -1126,6 +1149,80 @@ def test_multiprocess_grouped_small_calls_one_launch(nbx, oracle, n, batch, whic
                 assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, k, kind, dtype, op, count, r)
 
 
+REDUCE_CHAIN_COUNTS = (1000, 30000, 300000)   # LL, LL128 one-shot, Simple (defaults, one GPU)
+
+
+def _child_reduce_chain(uid_bytes, rank, n, q, null_recv):
+    """a group whose second Reduce reads what the first one writes
+    on the root (x -> y, then y -> z; and one buffer reduced in place twice).
+    The root's recv is written, a non-root's is not, so a cut that looked at
+    each rank's own writes split the root's run and batched the non-roots'.
+    Non-roots pass the same pointers as the root, or NULL recv buffers
+    (`null_recv`; then the chain reads y, which only the root has)."""
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        s = torch.cuda.current_stream().cuda_stream
+        I32, SUM = 2, 0
+        out = {}
+        for count in REDUCE_CHAIN_COUNTS:
+            i = torch.arange(count, dtype=torch.int32, device="cuda")
+            x = (i * 3 + rank * 7) % 101
+            y = rank * 1000 + i % 13
+            z = torch.full_like(i, -1)
+            w = (i * 5 + rank) % 89   # reduced in place twice
+            torch.cuda.synchronize()
+            recv_y = y.data_ptr() if (rank == 0 or not null_recv) else 0
+            recv_z = z.data_ptr() if (rank == 0 or not null_recv) else 0
+            nbx.group_start()
+            comm.reduce(x.data_ptr(), recv_y, count, I32, SUM, 0, s)
+            comm.reduce(y.data_ptr(), recv_z, count, I32, SUM, 0, s)
+            comm.reduce(w.data_ptr(), w.data_ptr(), count, I32, SUM, 0, s)
+            comm.reduce(w.data_ptr(), w.data_ptr(), count, I32, SUM, 0, s)
+            nbx.group_end()
+            torch.cuda.synchronize()
+            out[count] = (y.cpu().numpy().copy(), z.cpu().numpy().copy(), w.cpu().numpy().copy())
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n,null_recv", [(2, False), (3, False), (3, True)])
+def test_multiprocess_grouped_reduce_chain_root_and_nonroot(nbx, n, null_recv, monkeypatch):
+    """Grouped Reduce chains cut alike on the root and the non-roots (a
+    Reduce never shares a launch with another call of its group), at LL,
+    LL128 and Simple sizes: exact int32 sums, every rank's buffers as NCCL
+    leaves them (a non-root's recv untouched)."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "30")
+    monkeypatch.setenv("NBX_LL_MAX_GRID", "64")
+    res = _run_ranks(nbx, n, _child_reduce_chain, null_recv)
+    for count in REDUCE_CHAIN_COUNTS:
+        i = np.arange(count, dtype=np.int64)
+        xs = [(i * 3 + r * 7) % 101 for r in range(n)]
+        ys = [r * 1000 + i % 13 for r in range(n)]
+        ws = [(i * 5 + r) % 89 for r in range(n)]
+        S = sum(xs)
+        Z = S + sum(ys[1:])        # the root's y is S by then; a non-root's y is its own
+        W1 = sum(ws)
+        W2 = W1 + sum(ws[1:])
+        y0, z0, w0 = res[0][count]
+        assert np.array_equal(y0, S.astype(np.int32)), count
+        assert np.array_equal(z0, Z.astype(np.int32)), count
+        assert np.array_equal(w0, W2.astype(np.int32)), count
+        for r in range(1, n):
+            yr, zr, wr = res[r][count]
+            assert np.array_equal(yr, ys[r].astype(np.int32)) and np.array_equal(wr, ws[r].astype(np.int32))
+            assert (zr == -1).all()
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;
@@ -1237,22 +1334,26 @@ def _child_knobs(uid_bytes, rank, n, q, env):
         q.put((rank, "error", traceback.format_exc()))
 
 
-def test_multiprocess_reference_knobs(nbx, monkeypatch):
-    """NCCL_BUFFSIZE 256 KiB -> 128 KiB Simple slices (2 slots), NCCL_LL_BUFFSIZE
-    64 KiB -> LL up to 32 KiB, NCCL_LL128_BUFFSIZE 1 MiB -> LL128 up to 768 KiB,
-    NCCL_MAX_NCHANNELS 16 -> every grid capped at 16 workgroups; results exact."""
+@pytest.mark.parametrize("buffsize,slice_want", [("65536", 32768), ("4194304", 65536)])
+def test_multiprocess_reference_knobs(nbx, monkeypatch, buffsize, slice_want):
+    """NCCL_BUFFSIZE 64 KiB -> 32 KiB Simple slices (2 slots), while the
+    reference's own 4 MiB default, set explicitly, leaves the 64 KiB slice (only
+    smaller buffers are honoured: ADVICE r4, 1 MiB slices would be 4 GiB of
+    staging at 8 ranks); NCCL_LL_BUFFSIZE 64 KiB -> LL up to 32 KiB,
+    NCCL_LL128_BUFFSIZE 1 MiB -> LL128 up to 768 KiB, NCCL_MAX_NCHANNELS 16 ->
+    every grid capped at 16 workgroups; results exact."""
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     for k in ("NBX_SIMPLE_SLICE_BYTES", "NBX_SIMPLE_MAX_GRID", "NBX_LL_MAX_BYTES", "NBX_LL128_MAX_BYTES"):
         monkeypatch.delenv(k, raising=False)
     n = 2
-    env = {"NCCL_BUFFSIZE": ["262144"] * n, "NCCL_LL_BUFFSIZE": ["65536"] * n,
+    env = {"NCCL_BUFFSIZE": [buffsize] * n, "NCCL_LL_BUFFSIZE": ["65536"] * n,
            "NCCL_LL128_BUFFSIZE": ["1048576"] * n, "NCCL_MAX_NCHANNELS": ["16"] * n}
     res = _run_ranks(nbx, n, _child_knobs, env)
     for r in range(n):
         assert res[r]["init"] == 0
         ll, l128, slice_, slots, grid, llcap, l128cap, batch = res[r]["settings"][:8]
-        assert (ll, l128, slice_, slots, grid) == (32768, 786432, 131072, 2, 16), res[r]["settings"]
+        assert (ll, l128, slice_, slots, grid) == (32768, 786432, slice_want, 2, 16), res[r]["settings"]
         assert llcap <= 16 and l128cap <= 16 and batch == 1
         assert res[r]["settings"][9] == 0   # plan checks off by default
         assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
@@ -1284,7 +1385,7 @@ def test_multiprocess_nbx_override_wins(nbx, monkeypatch):
         assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
 
 
-@pytest.mark.parametrize("name,vals", [("NCCL_BUFFSIZE", ["262144", "131072"]), ("NBX_GROUP_BATCH", ["1", "0"]),
+@pytest.mark.parametrize("name,vals", [("NCCL_BUFFSIZE", ["65536", "32768"]), ("NBX_GROUP_BATCH", ["1", "0"]),
                                        ("NCCL_LL_BUFFSIZE", ["65536", "32768"]), ("NBX_CHECK_PLANS", ["1", "0"])])
 def test_multiprocess_settings_must_agree(nbx, monkeypatch, name, vals):
     """Settings that decide a call's protocol, grid, staging layout or launch

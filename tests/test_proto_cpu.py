@@ -60,3 +60,34 @@ def test_protocol_choice(lib, mask, ar, nbytes, n, want):
 
 def test_ll128_disabled_by_zero_max(lib):
     assert lib.nbxDebugChooseProto(ALL, 1, 256 * K, 64 * K, 4, 64 * K, 0, 256 * K) == P_SIMPLE
+
+
+# LL128 across GPUs (tuning.cc:250-297: LL128 is "default"
+# (2) unless NCCL_PROTO lists it, and default LL128 is enabled only on
+# validated fabrics): ranks on distinct GPUs start without LL128 unless
+# NCCL_PROTO names it (not in a "^list") or NBX_LL128_ACROSS_GPUS=1; ranks
+# sharing a GPU keep it (stress-tested there).
+@pytest.mark.parametrize("s,multi,mask", [
+    (None, 0, ALL), (None, 1, LL | SIMPLE), ("", 1, LL | SIMPLE),
+    ("LL128", 1, LL128), ("LL,LL128", 1, LL | LL128), ("^Simple", 1, LL), ("^LL", 1, SIMPLE),
+    ("^Simple", 0, LL | LL128), ("Simple", 1, SIMPLE),
+])
+def test_ll128_gated_across_gpus(lib, monkeypatch, s, multi, mask):
+    monkeypatch.delenv("NBX_LL128_ACROSS_GPUS", raising=False)
+    monkeypatch.delenv("NBX_DEBUG_ASSUME_MULTI_GPU", raising=False)
+    lib.nbxDebugGatedProtoMask.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.nbxDebugGatedProtoMask.restype = ctypes.c_int
+    assert lib.nbxDebugGatedProtoMask(None if s is None else s.encode(), multi) == mask
+
+
+def test_ll128_across_gpus_overrides(lib, monkeypatch):
+    lib.nbxDebugGatedProtoMask.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.nbxDebugGatedProtoMask.restype = ctypes.c_int
+    monkeypatch.delenv("NBX_DEBUG_ASSUME_MULTI_GPU", raising=False)
+    monkeypatch.setenv("NBX_LL128_ACROSS_GPUS", "1")
+    assert lib.nbxDebugGatedProtoMask(None, 1) == ALL
+    monkeypatch.setenv("NBX_LL128_ACROSS_GPUS", "0")
+    assert lib.nbxDebugGatedProtoMask(None, 1) == LL | SIMPLE
+    # the test hook: ranks that share a GPU are gated as if they did not
+    monkeypatch.setenv("NBX_DEBUG_ASSUME_MULTI_GPU", "1")
+    assert lib.nbxDebugGatedProtoMask(None, 0) == LL | SIMPLE

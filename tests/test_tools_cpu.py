@@ -58,3 +58,70 @@ def test_config_c_summarize_rejects_case_count_mismatch(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "config_c_profile.py"), "--summarize",
                         str(tmp_path / "cases.jsonl"), str(tmp_path / "trace.csv")], capture_output=True, text=True)
     assert r.returncode == 1 and "1 trace segments for 2 cases" in r.stdout
+
+
+# ---------------------------------------------------------------------------
+# scripts/set_thresholds.py: protocol thresholds from a bench line's sweep
+
+
+def _thr():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("set_thresholds", os.path.join(ROOT, "scripts", "set_thresholds.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_set_thresholds_on_the_r4_rehearsal():
+    """The committed 2-rank shared-GPU line (r4aj): LL wins every swept size,
+    so LL carries up to 1 MiB and LL128 nothing; the ring's 1 GiB beats the
+    direct schedule by > 5 %; a shared-GPU run never enables LL128 across GPUs."""
+    st = _thr()
+    b = st.last_collective_line(os.path.join(ROOT, "profiles", "r4", "bench_n2_shared_r4aj.json"))
+    b["shared_gpu"] = True
+    r = st.thresholds(b)
+    assert [row["chosen"] for row in r["rows"]] == ["LL"] * 4
+    env = r["env"]
+    assert env["NBX_LL_MAX_BYTES"] == 1 << 20 and env["NBX_LL128_MAX_BYTES"] == 0
+    assert env["NCCL_ALGO"] == "Ring"              # 1.7984 ms direct vs 1.7064 ms ring
+    assert env["NBX_CLIQUE_SIMPLE_MAX_BYTES"] == 32 << 20   # in-kernel 0.710 vs fold 0.733: inside the margin
+    assert env["NBX_LL128_ACROSS_GPUS"] == ""
+    assert "NBX_LL128_ONESHOT_MAX" not in env      # n = 2: no two-shot
+
+
+def test_set_thresholds_synthetic_8_ranks_with_hysteresis():
+    """A synthetic 8-GPU sweep: LL -> LL128 (one-shot, then two-shot) ->
+    Simple; a 3 % win does not switch (hysteresis), a 20 % win does; a clean
+    forced-LL128 stress on distinct GPUs enables LL128 across GPUs."""
+    st = _thr()
+    sizes = [4 << 10, 32 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]
+    sweep = {"bytes": sizes,
+             "LL":            [9.0, 10.0, 30.0, 90.0, 300.0, 1200.0],
+             "LL128":         [12.0, 9.8, 20.0, 28.0, 80.0, 300.0],    # 32 KiB: 2 % faster than LL -> stay
+             "LL128_oneshot": [12.0, 9.8, 20.0, 40.0, 150.0, 600.0],   # one-shot up to 256 KiB
+             "Simple":        [40.0, 42.0, 45.0, 50.0, 60.0, 90.0]}
+    b = {"n_gpus": 8, "collective": {"n_ranks": 8, "protocol_sweep": sweep,
+                                     "allreduce_direct": {"ms": 10.0}, "allreduce_ring": {"ms": 10.2},
+                                     "clique": {"allreduce_ms": 8.0, "fold_allreduce_ms": 12.0},
+                                     "ll128_forced": {"checked_calls": 16000, "mismatched_calls": 0}}}
+    r = st.thresholds(b)
+    assert [row["chosen"] for row in r["rows"]] == ["LL", "LL", "LL128", "LL128", "Simple", "Simple"]
+    env = r["env"]
+    assert env["NBX_LL_MAX_BYTES"] == 32 << 10
+    assert env["NBX_LL128_MAX_BYTES"] == 1 << 20
+    assert env["NBX_LL128_ONESHOT_MAX"] == 256 << 10
+    assert env["NCCL_ALGO"] == ""                       # ring 2 % slower: direct stays
+    assert env["NBX_CLIQUE_SIMPLE_MAX_BYTES"] == 1 << 40
+    assert env["NBX_LL128_ACROSS_GPUS"] == "1"
+    b["collective"]["ll128_forced"]["mismatched_calls"] = 1   # one torn line anywhere: keep it off
+    assert st.thresholds(b)["env"]["NBX_LL128_ACROSS_GPUS"] == ""
+
+
+def test_set_thresholds_cli(tmp_path):
+    import subprocess
+    import sys
+    p = tmp_path / "b.json"
+    p.write_text("not json\n" + open(os.path.join(ROOT, "profiles", "r4", "bench_n2_shared_r4aj.json")).read())
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "set_thresholds.py"), str(p), "--shared-gpu"],
+                         capture_output=True, text=True, check=True).stdout
+    assert "export NBX_LL_MAX_BYTES=1048576" in out and "unset NBX_LL128_ACROSS_GPUS" in out
