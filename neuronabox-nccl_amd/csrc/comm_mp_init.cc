@@ -1,0 +1,912 @@
+// comm_mp_init.cc — the multi-process communicator's creation.
+// Multi-process communicator (ncclCommInitRank with nranks > 1, one process
+// per rank on one node). Replaces NCCL's bootstrap + P2P transport setup
+// (bootstrap.cc, transport/p2p.cc:190-381) with a TCP bootstrap for the
+// init-time allgathers and connection buffers that the library allocates and
+// every peer IPC-maps ONCE, at init (p2pMap / p2pSendConnect / p2pRecvConnect,
+// p2p.cc:290-330,450-520):
+//   * LL / LL128 line buffers (nbx_ll.h) for small and medium messages;
+//   * the Simple protocol's staging and flag words (nbx_simple.h) for the rest,
+//     direct or ring schedule (NCCL_ALGO=Ring).
+// Peers never touch the caller's buffers and no call exchanges anything on
+// the host: a collective is one kernel on the caller's stream whose flow
+// control (the reference's waitPeer / postPeer, prims_simple.h:129-185)
+// runs inside it. All sequencing state is device-resident, so graph capture
+// and replay need nothing special.
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <string>
+#include <array>
+#include <exception>
+#include <random>
+#include <strings.h>
+#include <unistd.h>
+#include "nbx_comm.h"
+
+namespace nbxcomm {
+
+namespace {
+// Exchanged before anything is allocated: where every rank runs.
+struct MpPreInfo {
+  uint64_t pciKey;   // (domain, bus, device) of this rank's GPU: identifies it across processes
+  int32_t device;
+  int32_t cus;
+};
+
+struct MpInitInfo {
+  int32_t pid;
+  int32_t device;
+  hipIpcMemHandle_t llHandle;
+  hipIpcMemHandle_t l128Handle;
+  hipIpcMemHandle_t stageHandle;
+  hipIpcMemHandle_t sflagsHandle;
+  uint64_t nonce;          // this communicator's mapping self-check pattern (mpConnect)
+  // settings every rank must share: every rank must pick the same protocol,
+  // grid and staging layout for the same call
+  uint64_t llMaxBytes;
+  uint64_t l128MaxBytes;
+  uint64_t l128OneShotMax;
+  uint64_t sliceBytes;
+  int32_t protoMask;
+  int32_t ring;            // NCCL_ALGO=Ring
+  int32_t slots;
+  int32_t simpleGrid;
+  int32_t groupBatch;      // NBX_GROUP_BATCH: one launch per run of grouped calls, or one per call
+  int32_t checkPlans;      // NBX_CHECK_PLANS: every launch stamps / checks its plan (or none does)
+};
+
+}  // namespace
+
+// NCCL_PROTO (tuning.cc:254-259, parseList): a comma-separated list of the
+// enabled protocols among LL, LL128, Simple, or "^list" for all but those.
+// Per message (per-rank block for ReduceScatter) the first enabled protocol
+// whose buffer holds it is used: LL up to NBX_LL_MAX_BYTES (64 KiB), LL128 up
+// to NBX_LL128_MAX_BYTES (1 MiB; n <= 8 ranks), else Simple (also the
+// fallback when Simple is disabled and nothing else fits).
+// Read when the communicator is created (as NCCL reads its tuning env at init).
+int protoFromString(const char* v) {
+  if (v == nullptr || *v == 0) return kProtoAll;
+  bool exclude = v[0] == '^';
+  std::string list(exclude ? v + 1 : v);
+  int mask = 0;
+  size_t pos = 0;
+  while (pos <= list.size()) {
+    size_t e = list.find(',', pos);
+    if (e == std::string::npos) e = list.size();
+    std::string tok = list.substr(pos, e - pos);
+    if (strcasecmp(tok.c_str(), "ll") == 0) mask |= kProtoLL;
+    else if (strcasecmp(tok.c_str(), "ll128") == 0) mask |= kProtoLL128;
+    else if (strcasecmp(tok.c_str(), "simple") == 0) mask |= kProtoSimple;
+    else if (!tok.empty()) warn("NCCL_PROTO: unknown protocol '%s' ignored", tok.c_str());
+    pos = e + 1;
+  }
+  return exclude ? (kProtoAll & ~mask) : mask;
+}
+int protoFromEnv() { return protoFromString(std::getenv("NCCL_PROTO")); }
+
+// LL128 across GPUs is enabled by default only where it was validated — the
+// reference's rule (tuning.cc:250-297: protoEnable[LL128] = 2 "default", and
+// parseList turns it into 1 only when NCCL_PROTO lists LL128; a "^list"
+// leaves it at 2). LL128 trusts a 64-byte line written by one store to arrive
+// whole; within one GPU that was stress-tested, over xGMI it has
+// not been, so ranks on different GPUs drop LL128 from the default set until a
+// node run validates it (DESIGN §6 states the flip rule). It stays on when
+// NCCL_PROTO names it explicitly, or with NBX_LL128_ACROSS_GPUS=1.
+// NBX_DEBUG_ASSUME_MULTI_GPU=1 (test hook) applies this gate to ranks that
+// share a GPU, and nothing else of the multi-GPU settings.
+bool protoLL128Explicit(const char* v) {
+  if (v == nullptr || *v == 0 || v[0] == '^') return false;
+  return (protoFromString(v) & kProtoLL128) != 0;
+}
+int protoGateAcrossGpus(int mask, bool multiGpu, const char* ncclProto) {
+  const bool assume = envLong("NBX_DEBUG_ASSUME_MULTI_GPU", 0) != 0;
+  if (!(multiGpu || assume) || protoLL128Explicit(ncclProto)) return mask;
+  if (envLong("NBX_LL128_ACROSS_GPUS", 0) != 0) return mask;
+  return mask & ~kProtoLL128;
+}
+
+// Per message: LL up to the LL max; LL128 up to the LL128 max: one-shot (every
+// rank pushes the whole message to every target), for AllReduce / Reduce with
+// more than 2 ranks only up to the one-shot max and the two-shot AllReduce /
+// Reduce (reduce-scatter + gather hops, a rank's block in half an LL128 slot)
+// above it; else Simple. ReduceScatter is one hop by nature: one-shot up to
+// the LL128 max.
+// Lines per (parity, source) slot: holds maxBytes one-shot, and each half (a
+// two-shot sub-slot) holds maxBytes / 2.
+uint64_t l128SlotLinesFor(uint64_t maxBytes) {
+  const uint64_t half = (maxBytes + 1) / 2;
+  return 2 * ((half + nbx::kL128DataBytesHost - 1) / nbx::kL128DataBytesHost);
+}
+MpProto chooseProtoFor(int mask, bool twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int n, uint64_t llMax,
+                       uint64_t l128Max, uint64_t oneShotMax) {
+  if (slotBytes == 0 || n > 64) return kMpSimple;
+  if ((mask & kProtoLL) && slotBytes <= llMax) return kMpLL;
+  if ((mask & kProtoLL128) && l128Max != 0 && n <= nbx::kL128MaxRanksHost) {
+    if (!twoShotKind || n <= 2 || slotBytes <= oneShotMax) {
+      if (slotBytes <= l128Max) return kMpLL128;
+    } else if (slotBytes <= l128Max && blockBytes <= (l128SlotLinesFor(l128Max) / 2) * nbx::kL128DataBytesHost) {
+      return kMpLL128x2;
+    }
+  }
+  return kMpSimple;
+}
+
+// NCCL_ALGO (tuning.cc:254-259): "Ring" selects the ring schedule for the
+// Simple protocol; anything else (default) the direct schedule.
+// Read when the communicator is created.
+bool algoRingFromEnv() {
+  const char* v = std::getenv("NCCL_ALGO");
+  return v && strcasecmp(v, "ring") == 0;
+}
+
+long envLong(const char* name, long dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atol(v) : dflt;
+}
+
+// The reference's own tuning knobs on this path, read at communicator
+// creation like NCCL reads them (init.cc:523-541 computeBuffSizes,
+// connect.cc:314-315, tuning.cc:12), each mapped onto the setting that plays
+// its role here; the NBX_* variable of that setting, when set, wins:
+//   NCCL_BUFFSIZE       Simple connection buffer per (peer, channel): the
+//                       Simple staging per (peer, workgroup, region) is
+//                       slots x slice, so slice = NCCL_BUFFSIZE / slots
+//                       (NBX_SIMPLE_SLICE_BYTES) — only below the 64 KiB
+//                       default (mpTransportSettings);
+//   NCCL_LL_BUFFSIZE    LL buffer: half of every 8-byte line is flag, so LL
+//                       carries messages up to NCCL_LL_BUFFSIZE / 2 (NBX_LL_MAX_BYTES);
+//   NCCL_LL128_BUFFSIZE LL128 buffer: 48 payload bytes per 64-byte line, so
+//                       LL128 carries up to 3/4 of it (NBX_LL128_MAX_BYTES);
+//   NCCL_MAX_NCHANNELS / NCCL_MIN_NCHANNELS  a channel is a workgroup here:
+//                       the Simple grid (NBX_SIMPLE_MAX_GRID) and the LL /
+//                       LL128 grids are capped at the max, and the Simple grid
+//                       raised to the min (both within the co-residency cap).
+// Unset, the measured defaults stay (64 KiB slices, 64 KiB LL, 4 MiB LL128,
+// 128 Simple workgroups). NCCL_NTHREADS has no counterpart: every
+// kernel is compiled for 256-thread workgroups (a warning says it is ignored).
+long ncclEnvMapped(const char* nbxName, const char* ncclName, long dflt, long num, long den) {
+  const char* v = std::getenv(nbxName);
+  if (v && *v) return std::atol(v);
+  const char* w = std::getenv(ncclName);
+  if (w && *w && std::atol(w) > 0) return std::atol(w) / den * num;
+  return dflt;
+}
+
+// Memory that other GPUs write and this GPU reads (LL lines, Simple staging
+// and flag words). Uncached (MTYPE UC) by default: a peer's stores over xGMI
+// land in HBM and no XCD L2 can hold a stale copy, which is what RCCL uses
+// for its connection buffers too. NBX_SYNC_MEM=coarse selects plain hipMalloc
+// (A/B measurement only).
+// A connection buffer every peer maps: uncached device memory, its size
+// rounded up to whole 2 MiB pages so the buffer is an allocation of its own,
+// and its IPC handle taken at once.
+// The runtime rule behind the retry (scripts/probe_ipc_export.py: N processes
+// replaying communicator creation / destruction with the library's buffer
+// sizes, raw HIP, no libnbxccl; profiles/r4/probe_ipc_export_r4*.jsonl):
+// once exported allocations are freed, hipIpcGetMemHandle now and then refuses
+// ('invalid argument') a new allocation — 25 of 62,400 exports, 20 of them at
+// an address whose earlier allocation had been exported and freed; the same
+// pointer was refused again on an immediate retry 23 times of 25, and a fresh
+// allocation (the refused one still held, so at another address) was
+// accepted 23 times of 23. With exported buffers never freed: 0 of 19,200. So
+// a refused allocation is held aside while the next one is made (at most 4
+// tries), then freed. The same runtime condition also makes a successful
+// export name the wrong memory now and then (mpConnect, which verifies every
+// mapping and re-exports what is wrong).
+hipError_t allocSyncMem(void** p, size_t bytes, hipIpcMemHandle_t* handle /* nullptr: in-process only */) {
+  static const bool coarse = [] {
+    const char* v = std::getenv("NBX_SYNC_MEM");
+    return v && strcasecmp(v, "coarse") == 0;
+  }();
+  const size_t page = (size_t)2 << 20;
+  bytes = (bytes + page - 1) / page * page;
+  std::vector<void*> refused;
+  hipError_t e = hipSuccess;
+  for (int attempt = 0; attempt < 4; attempt++) {
+    *p = nullptr;
+    e = coarse ? hipMalloc(p, bytes) : hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess || handle == nullptr) break;
+    e = hipIpcGetMemHandle(handle, *p);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    info("hipIpcGetMemHandle refused a %zu-byte connection buffer at %p (%s): a reused exported address; "
+         "allocating another", bytes, *p, hipGetErrorString(e));
+    refused.push_back(*p);
+    *p = nullptr;
+  }
+  for (void* q : refused) (void)hipFree(q);
+  return e;
+}
+
+// A device spin gave up (host error word set): name the wait, the peer, the
+// value it waited for and the last one it saw (nbx_diag.h), once per record.
+void mpReportDeviceError(ncclComm* c) {
+  MpState* mp = mpOf(c);
+  if (!mp || !mp->hostWords || mp->hostWords[1] == 0) return;
+  const volatile uint64_t* d = (const volatile uint64_t*)((const volatile char*)mp->hostWords + nbx::kDiagByteOffset);
+  static thread_local uint64_t lastReported[nbx::kDiagWords] = {};
+  uint64_t rec[nbx::kDiagWords];
+  for (int i = 0; i < nbx::kDiagWords; i++) rec[i] = d[i];
+  if (std::memcmp(rec, lastReported, sizeof(rec)) == 0) return;
+  std::memcpy(lastReported, rec, sizeof(rec));
+  if (mp->hostWords[1] == 2) {
+    warn("comm %p rank %d: a device wait was aborted (ncclCommAbort)", (void*)c, c->rank);
+    return;
+  }
+  if (nbx::diagIsPlanCheck(rec[0])) {
+    warn("comm %p rank %d: device check failed after %.3f s: %s: peer %lld, our plan %llx, its plan %llx "
+         "(workgroup %llu)", (void*)c, c->rank, (double)rec[5] * 1e-8, nbx::diagSiteName(rec[0]),
+         (long long)(int64_t)rec[1], (unsigned long long)rec[2], (unsigned long long)rec[3],
+         (unsigned long long)rec[4]);
+    return;
+  }
+  warn("comm %p rank %d: device wait timed out after %.3f s: %s of peer %lld, waited for %llu, last saw %llu "
+       "(workgroup %llu)", (void*)c, c->rank, (double)rec[5] * 1e-8, nbx::diagSiteName(rec[0]),
+       (long long)(int64_t)rec[1], (unsigned long long)rec[2], (unsigned long long)rec[3],
+       (unsigned long long)rec[4]);
+}
+
+ncclResult_t mpOpenPeer(MpState* mp, const hipIpcMemHandle_t& h, void** p) {
+  HIPCHECK(hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess));
+  mp->peerMaps.push_back(*p);
+  return ncclSuccess;
+}
+
+// The 16-byte mapping self-check word rank `from` leaves at slot `at`.
+void checkWord(uint64_t nonce, int from, int at, uint64_t out[2]) {
+  out[0] = nonce ^ (0x9e3779b97f4a7c15ull * (uint64_t)(from + 1));
+  out[1] = ~nonce ^ (0xc2b2ae3d27d4eb4full * (uint64_t)(at + 1));
+}
+
+// Every connection buffer carries a check region after its used bytes:
+// 16 bytes per writer rank plus the owner's own word (mpConnect).
+uint64_t connCheckOff(uint64_t used) { return (used + 15) & ~(uint64_t)15; }
+uint64_t connAllocBytes(uint64_t used, int n) { return connCheckOff(used) + 16ull * (uint64_t)(n + 1); }
+
+// The connection buffers a multi-process rank exports (LL lines, LL128 lines,
+// Simple staging, Simple flag words).
+enum { kConnLL, kConnL128, kConnStage, kConnFlags, kNumConn };
+
+// One rank's LL-family state on the current device: completion word,
+// sequencing state, host abort / error words, and the LL and LL128 connection
+// buffers (IPC handles taken when `ipc`; a clique's buffers stay in-process).
+ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
+  const char* t = std::getenv("NBX_TIMEOUT_SEC");
+  if (t && std::atof(t) > 0) mp->timeoutSec = std::atof(t);
+  mp->protoMask = protoFromEnv();
+  mp->streamOrder = envLong("NBX_MP_STREAM_ORDER", 1) != 0;
+  mp->groupBatch = envLong("NBX_GROUP_BATCH", 1) != 0;
+  // Plan checks (nbx_ll.h plan words, nbx_simple.h slice headers): a launch
+  // fails, naming the peer, when ranks issue mismatched calls or cut a group
+  // differently — instead of a timeout or folded misplaced data. Off unless
+  // asked for (NBX_CHECK_PLANS=1, or the reference's own argument-checking
+  // knob NCCL_CHECK_POINTERS=1): they cost 0.7-1.9 us per small call on the
+  // shared-GPU rig, and the reference does not check this either.
+  mp->checkPlans = envLong("NBX_CHECK_PLANS", comm->checkPointers ? 1 : 0) != 0;
+  HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
+  HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
+  HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
+  HIPCHECK(hipMemset(mp->llState, 0, sizeof(nbx::LLState)));
+  if (comm->hostWords == nullptr) return ncclInternalError;
+  mp->hostWords = comm->hostWords;
+  mp->hostWordsDev = comm->hostWordsDev;
+  // LL buffer: 2 parities x n sources x 2 lines per 8-byte pack
+  {
+    uint64_t mx = (uint64_t)ncclEnvMapped("NBX_LL_MAX_BYTES", "NCCL_LL_BUFFSIZE", 64 << 10, 1, 2);
+    mx = (mx + 15) & ~(uint64_t)15;
+    if (mx < 1024) mx = 1024;
+    mp->llMaxBytes = mx;
+    mp->llSlotLines = 2 * (mx / 8);
+    mp->llDoneOff = 2 * (uint64_t)n * mp->llSlotLines;
+    mp->llPlanOff = mp->llDoneOff + (uint64_t)n + 1;
+    mp->llBytes = (mp->llPlanOff + 2 * (uint64_t)n) * sizeof(uint64_t);
+    const uint64_t llAlloc = connAllocBytes(mp->llBytes, n);
+    HIPCHECK(allocSyncMem((void**)&mp->ll, llAlloc, ipc ? &mp->llHandle : nullptr));
+    HIPCHECK(hipMemset(mp->ll, 0, llAlloc));
+  }
+  // LL128 buffer: 2 parities x n sources x 64-byte lines of 48 payload bytes (n <= 8)
+  if (n <= nbx::kL128MaxRanksHost) {
+    // 1 MiB: where Simple overtakes LL128 (48 payload bytes per 64-byte line) on
+    // the shared-GPU rig — 2 ranks: 1 MiB 15.4 vs 15.6 us, 2 MiB 25.8 vs 16.4,
+    // 4 MiB 43.8 vs 18.7; 4 ranks: 2 MiB 34.5 vs 25.4 (profiles/r4/proto_sweep_r4z)
+    uint64_t mx = (uint64_t)ncclEnvMapped("NBX_LL128_MAX_BYTES", "NCCL_LL128_BUFFSIZE", 1 << 20, 3, 4);
+    mp->l128OneShotMax = (uint64_t)envLong("NBX_LL128_ONESHOT_MAX", 256 << 10);
+    if (mx > (64u << 20)) mx = 64u << 20;   // keeps the buffer under the 4 GiB descriptor range
+    if (mx != 0) {
+      mx = (mx + 15) & ~(uint64_t)15;
+      mp->l128MaxBytes = mx;
+      mp->l128SlotLines = l128SlotLinesFor(mx);
+      mp->l128Bytes = 2 * (uint64_t)n * mp->l128SlotLines * nbx::kL128LineBytesHost;
+      const uint64_t l128Alloc = connAllocBytes(mp->l128Bytes, n);
+      HIPCHECK(allocSyncMem((void**)&mp->l128, l128Alloc, ipc ? &mp->l128Handle : nullptr));
+      HIPCHECK(hipMemset(mp->l128, 0, l128Alloc));
+    }
+  }
+  return ncclSuccess;
+}
+
+// Grid caps and Simple settings of one rank's transport. Simple grid: one
+// workgroup per CU, all co-resident (workgroup g of a rank waits on workgroup
+// g of its peers); ranks sharing a GPU split its CUs, and so do the LL
+// family's spinning grids (the env caps still apply on top).
+void mpTransportSettings(MpState* mp, int minCus, int maxShare) {
+  const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0), minCh = envLong("NCCL_MIN_NCHANNELS", 0);
+  long g = envLong("NBX_SIMPLE_MAX_GRID", 0);
+  if (g <= 0) {
+    g = 128;
+    if (maxCh > 0) g = std::min(g, maxCh);
+    if (minCh > 0) g = std::max(g, minCh);
+  }
+  g = std::min<long>(g, std::max(1, minCus / maxShare));
+  mp->llGridCap = (uint32_t)std::max(1, 4 * minCus / maxShare);
+  mp->l128GridCap = (uint32_t)std::max(1, minCus / maxShare);
+  if (maxCh > 0) {   // a channel is a workgroup here
+    mp->llGridCap = std::min<uint32_t>(mp->llGridCap, (uint32_t)maxCh);
+    mp->l128GridCap = std::min<uint32_t>(mp->l128GridCap, (uint32_t)maxCh);
+  }
+  mp->simpleGrid = (int)std::max<long>(1, std::min<long>(g, nbx::kSimpleMaxGrid));
+  mp->slots = (int)std::max<long>(2, std::min<long>(envLong("NBX_SIMPLE_SLOTS", 2), 8));
+  // NCCL_BUFFSIZE is the reference's buffer per (peer, channel) and its own
+  // default is 4 MiB, which job scripts often set explicitly; here it would
+  // become a 1 MiB slice per (peer, workgroup, region, slot) — 4 GiB of staging
+  // at 8 ranks. So it is honoured only where it LOWERS the slice
+  // below the 64 KiB default (a memory cap, its use in the reference); an
+  // explicit NBX_SIMPLE_SLICE_BYTES sets the slice (16 B .. 1 MiB) as asked.
+  long sl = envLong("NBX_SIMPLE_SLICE_BYTES", 0);
+  if (sl <= 0) {
+    sl = 64 << 10;
+    const long bs = envLong("NCCL_BUFFSIZE", 0);
+    if (bs > 0 && bs / mp->slots < sl) sl = bs / mp->slots;
+    else if (bs > 0)
+      info("NCCL_BUFFSIZE=%ld ignored: the Simple slice stays %ld bytes (only smaller buffers are honoured)", bs, sl);
+  }
+  sl = std::max<long>(nbx::kSimpleMinSliceBytes, std::min<long>(sl, 1 << 20));
+  mp->sliceBytes = (uint64_t)(sl + 15) & ~(uint64_t)15;
+  if (const char* nt = std::getenv("NCCL_NTHREADS"); nt && *nt && std::atol(nt) != 256)
+    info("NCCL_NTHREADS=%s ignored: every kernel of this library runs 256-thread workgroups", nt);
+  mp->simplePrefetch = envLong("NBX_SIMPLE_PREFETCH", 1) != 0;
+}
+
+// The Simple protocol's staging and flag words (uncached, exported when
+// `ipc`, with the check region mpConnect uses) and its counters.
+ncclResult_t mpAllocSimple(MpState* mp, int n, bool ipc) {
+  const uint64_t cells = (uint64_t)n * (uint64_t)mp->simpleGrid;
+  // slices, then one 16-byte plan header per slice cell (nbx_simple.h simpleHdr)
+  mp->stageHdrOff = 2ull * (uint64_t)mp->slots * cells * mp->sliceBytes;
+  mp->stageBytes = mp->stageHdrOff + 2ull * (uint64_t)mp->slots * cells * 16u;
+  HIPCHECK(allocSyncMem((void**)&mp->stage, connAllocBytes(mp->stageBytes, n), ipc ? &mp->stageHandle : nullptr));
+  HIPCHECK(hipMemset(mp->stage, 0, connAllocBytes(mp->stageBytes, n)));
+  mp->sflagsBytes = 4 * cells * sizeof(uint64_t);
+  HIPCHECK(allocSyncMem((void**)&mp->sflags, connAllocBytes(mp->sflagsBytes, n), ipc ? &mp->sflagsHandle : nullptr));
+  HIPCHECK(hipMemset(mp->sflags, 0, connAllocBytes(mp->sflagsBytes, n)));
+  HIPCHECK(hipMalloc((void**)&mp->scounters, 4 * cells * sizeof(uint64_t)));
+  HIPCHECK(hipMemset(mp->scounters, 0, 4 * cells * sizeof(uint64_t)));
+  return ncclSuccess;
+}
+
+// Opens every peer's connection buffers and checks every mapping before first
+// use, re-exporting any buffer whose mapping is wrong (the reference maps its
+// peers' buffers once at connection time, transport/p2p.cc:290-330 p2pMap).
+// Why the check is needed: scripts/probe_ipc_export.py (raw HIP, N processes
+// on one GPU replaying communicator creation / destruction with this
+// library's buffer sizes and memory kinds) found IPC mappings that do not
+// show the exported allocation — an importer reads zeros or ANOTHER rank's
+// buffer through it (89 canary reads), and its stores never reach the owner
+// (164), out of 62,400 imports, in the library's own memory kind as in plain
+// hipMalloc memory; the same wrong bytes are seen by every importer of that
+// handle (so it is the export, not one importer's mapping, that is wrong),
+// mostly at owner addresses that an earlier, freed allocation of the owner
+// had been exported from; with exported buffers never freed, none. Round 2's
+// wrong results (peers reading stale bytes through a mapping of a freshly
+// allocated buffer, their stores lost) are the same failure.
+// Check, per buffer and round (each with a fresh per-communicator nonce):
+// every rank stores a 16-byte word through its mapping of every peer's buffer
+// (slot = its rank) and its own word into its own buffer (slot n), all in the
+// check region after the used bytes; after a bootstrap barrier every rank
+// checks the words its peers stored into its buffers and reads every peer's
+// own word through its mappings. A wrong (owner, buffer) seen by anyone —
+// agreed by an allgather — is re-exported: its owner allocates a new buffer
+// (the old one held until the end, so the new one lands elsewhere), every
+// peer closes the wrong mapping and opens the new handle, and the round
+// repeats (at most 4). Only then does ncclCommInitRank fail (ncclSystemError).
+// NBX_IPC_VERIFY_FAIL=<rank>:<buffer> (test hook) makes round 0 report that
+// rank's buffer (0 LL, 1 LL128, 2 staging, 3 flags) wrong.
+ncclResult_t mpConnect(ncclComm* c, const std::vector<MpInitInfo>& all) {
+  MpState* mp = c->mp;
+  const int n = c->nRanks, me = c->rank;
+  void** own[kNumConn] = {(void**)&mp->ll, (void**)&mp->l128, (void**)&mp->stage, (void**)&mp->sflags};
+  hipIpcMemHandle_t* ownHandle[kNumConn] = {&mp->llHandle, &mp->l128Handle, &mp->stageHandle, &mp->sflagsHandle};
+  const uint64_t used[kNumConn] = {mp->llBytes, mp->l128Bytes, mp->stageBytes, mp->sflagsBytes};
+  const bool present[kNumConn] = {true, mp->l128 != nullptr, true, true};   // the same on every rank (n <= 8)
+  auto handleOf = [](const MpInitInfo& i, int t) -> const hipIpcMemHandle_t& {
+    return t == kConnLL ? i.llHandle : t == kConnL128 ? i.l128Handle : t == kConnStage ? i.stageHandle : i.sflagsHandle;
+  };
+  std::vector<std::array<char*, kNumConn>> peer(n);
+  std::vector<hipIpcMemHandle_t> cur((size_t)n * kNumConn);   // the handle each mapping was opened from
+  for (int j = 0; j < n; j++)
+    for (int t = 0; t < kNumConn; t++) {
+      peer[j][t] = nullptr;
+      cur[(size_t)j * kNumConn + t] = handleOf(all[j], t);
+    }
+  auto open = [&](int j, int t) -> ncclResult_t {
+    void* p = nullptr;
+    NCCLCHECK(mpOpenPeer(mp, cur[(size_t)j * kNumConn + t], &p));
+    peer[j][t] = (char*)p;
+    return ncclSuccess;
+  };
+  for (int j = 0; j < n; j++)
+    for (int t = 0; t < kNumConn; t++)
+      if (j != me && present[t]) NCCLCHECK(open(j, t));
+  int failRank = -1, failBuf = -1;
+  if (const char* v = std::getenv("NBX_IPC_VERIFY_FAIL"); v && *v) std::sscanf(v, "%d:%d", &failRank, &failBuf);
+  std::vector<void*> retired;
+  ncclResult_t res = ncclSuccess;
+  constexpr int kRounds = 4;
+  for (int round = 0;; round++) {
+    const uint64_t salt = 0x632be59bd9b4e019ull * (uint64_t)(round + 1);
+    auto nonceOf = [&](int j, int t) { return all[j].nonce ^ salt ^ (0xd6e8feb86659fd93ull * (uint64_t)(t + 1)); };
+    uint64_t w[2];
+    for (int t = 0; t < kNumConn; t++) {
+      if (!present[t]) continue;
+      const uint64_t off = connCheckOff(used[t]);
+      for (int j = 0; j < n; j++) {
+        if (j == me) continue;
+        checkWord(nonceOf(me, t), me, j, w);
+        HIPCHECK(hipMemcpy(peer[j][t] + off + 16ull * (uint64_t)me, w, 16, hipMemcpyHostToDevice));
+      }
+      checkWord(nonceOf(me, t), me, n, w);
+      HIPCHECK(hipMemcpy((char*)*own[t] + off + 16ull * (uint64_t)n, w, 16, hipMemcpyHostToDevice));
+    }
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<uint8_t> bad((size_t)n * kNumConn, 0), allBad((size_t)n * n * kNumConn);
+    int32_t dummy = 0;
+    std::vector<int32_t> gathered(n);
+    NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &dummy, sizeof(dummy), gathered.data()));   // every word stored
+    std::vector<uint64_t> mine(2 * (size_t)(n + 1));
+    for (int t = 0; t < kNumConn; t++) {
+      if (!present[t]) continue;
+      const uint64_t off = connCheckOff(used[t]);
+      HIPCHECK(hipMemcpy(mine.data(), (char*)*own[t] + off, 16ull * (uint64_t)(n + 1), hipMemcpyDeviceToHost));
+      for (int j = 0; j < n; j++) {
+        if (j == me) continue;
+        checkWord(nonceOf(j, t), j, me, w);
+        if (mine[2 * j] != w[0] || mine[2 * j + 1] != w[1]) {
+          info("comm %p rank %d: rank %d's store through its mapping of my buffer %d did not land (round %d)",
+               (void*)c, me, j, t, round);
+          bad[(size_t)me * kNumConn + t] = 1;
+        }
+        uint64_t got[2];
+        HIPCHECK(hipMemcpy(got, peer[j][t] + off + 16ull * (uint64_t)n, 16, hipMemcpyDeviceToHost));
+        checkWord(nonceOf(j, t), j, n, w);
+        if (got[0] != w[0] || got[1] != w[1]) {
+          info("comm %p rank %d: my mapping of rank %d's buffer %d shows other bytes (round %d)", (void*)c, me, j, t,
+               round);
+          bad[(size_t)j * kNumConn + t] = 1;
+        }
+      }
+    }
+    if (round == 0 && failRank == me && failBuf >= 0 && failBuf < kNumConn && present[failBuf])
+      bad[(size_t)me * kNumConn + failBuf] = 1;
+    NCCLCHECK(nbx::bootstrapAllGather(mp->bs, bad.data(), bad.size(), allBad.data()));
+    for (int q = 0; q < n; q++)
+      for (size_t i = 0; i < bad.size(); i++) bad[i] |= allBad[(size_t)q * bad.size() + i];
+    int nBad = 0;
+    for (uint8_t b : bad) nBad += b;
+    if (nBad == 0) break;
+    if (round + 1 == kRounds) {
+      warn("ncclCommInitRank : %d peer mapping(s) still wrong after %d re-exports; giving up", nBad, kRounds - 1);
+      res = ncclSystemError;
+      break;
+    }
+    mp->ipcRepairs += nBad;
+    // re-export: the owner of a wrong buffer allocates another (the old one held)
+    struct Fresh {
+      hipIpcMemHandle_t h[kNumConn];
+    } fresh{};
+    for (int t = 0; t < kNumConn; t++) {
+      if (!bad[(size_t)me * kNumConn + t]) continue;
+      retired.push_back(*own[t]);
+      *own[t] = nullptr;
+      const uint64_t bytes = connAllocBytes(used[t], n);
+      HIPCHECK(allocSyncMem(own[t], bytes, ownHandle[t]));
+      HIPCHECK(hipMemset(*own[t], 0, bytes));
+      fresh.h[t] = *ownHandle[t];
+      info("comm %p rank %d: buffer %d re-exported at %p (round %d)", (void*)c, me, t, *own[t], round);
+    }
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<Fresh> allFresh(n);
+    NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &fresh, sizeof(fresh), allFresh.data()));
+    for (int j = 0; j < n; j++) {
+      if (j == me) continue;
+      for (int t = 0; t < kNumConn; t++) {
+        if (!bad[(size_t)j * kNumConn + t]) continue;
+        auto it = std::find(mp->peerMaps.begin(), mp->peerMaps.end(), (void*)peer[j][t]);
+        if (it != mp->peerMaps.end()) mp->peerMaps.erase(it);
+        HIPCHECK(hipIpcCloseMemHandle(peer[j][t]));
+        cur[(size_t)j * kNumConn + t] = allFresh[j].h[t];
+        NCCLCHECK(open(j, t));
+      }
+    }
+  }
+  for (void* q : retired) (void)hipFree(q);
+  NCCLCHECK(res);
+  // the device tables of peer buffers (own entry: own buffer)
+  std::vector<uint64_t*> llTable(n), l128Table(n, nullptr), flagTable(n);
+  std::vector<char*> stageTable(n);
+  for (int j = 0; j < n; j++) {
+    llTable[j] = j == me ? mp->ll : (uint64_t*)peer[j][kConnLL];
+    l128Table[j] = j == me ? mp->l128 : (uint64_t*)peer[j][kConnL128];
+    stageTable[j] = j == me ? mp->stage : peer[j][kConnStage];
+    flagTable[j] = j == me ? mp->sflags : (uint64_t*)peer[j][kConnFlags];
+  }
+  auto upload = [](void** dev, const void* host, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(dev, bytes);
+    return e != hipSuccess ? e : hipMemcpy(*dev, host, bytes, hipMemcpyHostToDevice);
+  };
+  HIPCHECK(upload((void**)&mp->peerLLDev, llTable.data(), n * sizeof(uint64_t*)));
+  if (mp->l128) HIPCHECK(upload((void**)&mp->peerL128Dev, l128Table.data(), n * sizeof(uint64_t*)));
+  HIPCHECK(upload((void**)&mp->peerStageDev, stageTable.data(), n * sizeof(char*)));
+  HIPCHECK(upload((void**)&mp->peerSFlagsDev, flagTable.data(), n * sizeof(uint64_t*)));
+  return ncclSuccess;
+}
+
+ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
+  MpState* mp = new MpState();
+  c->mp = mp;
+  const int n = c->nRanks, me = c->rank;
+  mp->ring = algoRingFromEnv();
+  NCCLCHECK(nbx::bootstrapConnect(id, me, n, &mp->bs));
+  // where every rank runs: decides LL128's self-test and the Simple grid
+  MpPreInfo pre{};
+  {
+    int dom = 0, bus = 0, dv = 0, cus = 0;
+    (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device);
+    (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device);
+    (void)hipDeviceGetAttribute(&dv, hipDeviceAttributePciDeviceId, c->device);
+    HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+    pre.pciKey = ((uint64_t)(uint32_t)dom << 32) | ((uint64_t)(uint32_t)bus << 8) | (uint64_t)(uint32_t)dv;
+    pre.device = c->device;
+    pre.cus = cus;
+  }
+  std::vector<MpPreInfo> pres(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &pre, sizeof(pre), pres.data()));
+  int minCus = pre.cus, maxShare = 1;
+  for (int j = 0; j < n; j++) {
+    mp->multiGpu |= pres[j].pciKey != pre.pciKey;
+    minCus = std::min(minCus, (int)pres[j].cus);
+    int share = 0;
+    for (int q = 0; q < n; q++) share += pres[q].pciKey == pres[j].pciKey;
+    maxShare = std::max(maxShare, share);
+  }
+  mpTransportSettings(mp, minCus, maxShare);
+  NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true, c));
+  mp->protoMask = protoGateAcrossGpus(mp->protoMask, mp->multiGpu, std::getenv("NCCL_PROTO"));   // before the settings are compared
+  NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/true));
+  HIPCHECK(hipDeviceSynchronize());   // zeroed before any peer can map and write them
+
+  MpInitInfo mine{};
+  mine.pid = (int32_t)getpid();
+  mine.device = c->device;
+  mine.llMaxBytes = mp->llMaxBytes;
+  mine.l128MaxBytes = mp->l128MaxBytes;
+  mine.l128OneShotMax = mp->l128OneShotMax;
+  mine.sliceBytes = mp->sliceBytes;
+  mine.protoMask = mp->protoMask;
+  mine.ring = mp->ring;
+  mine.slots = mp->slots;
+  mine.simpleGrid = mp->simpleGrid;
+  mine.groupBatch = mp->groupBatch;
+  mine.checkPlans = mp->checkPlans;
+  mine.nonce = std::random_device{}() * 0x100000001ull ^ (uint64_t)std::random_device{}() ^
+               ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)mp;
+  mine.llHandle = mp->llHandle;
+  if (mp->l128) mine.l128Handle = mp->l128Handle;
+  mine.stageHandle = mp->stageHandle;
+  mine.sflagsHandle = mp->sflagsHandle;
+  std::vector<MpInitInfo> all(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &mine, sizeof(mine), all.data()));
+  for (int j = 0; j < n; j++) {
+    // every rank must pick the same protocol, grid and layout for the same call
+    if (all[j].llMaxBytes != mp->llMaxBytes || all[j].l128MaxBytes != mp->l128MaxBytes ||
+        all[j].l128OneShotMax != mp->l128OneShotMax || all[j].protoMask != mp->protoMask) {
+      warn("ncclCommInitRank : NCCL_PROTO / NBX_LL_MAX_BYTES / NBX_LL128_MAX_BYTES / NBX_LL128_ONESHOT_MAX differ "
+           "across ranks");
+      return ncclInvalidUsage;
+    }
+    if (all[j].ring != mine.ring || all[j].sliceBytes != mine.sliceBytes || all[j].slots != mine.slots ||
+        all[j].simpleGrid != mine.simpleGrid) {
+      warn("ncclCommInitRank : NCCL_ALGO / NBX_SIMPLE_MAX_GRID / NBX_SIMPLE_SLICE_BYTES / NBX_SIMPLE_SLOTS differ "
+           "across ranks");
+      return ncclInvalidUsage;
+    }
+    // a group's calls become one launch or one per call, and every launch
+    // advances the device-resident sequence by one: ranks must cut alike
+    if (all[j].groupBatch != mine.groupBatch) {
+      warn("ncclCommInitRank : NBX_GROUP_BATCH differs across ranks");
+      return ncclInvalidUsage;
+    }
+    // a checking rank would wait for plan words a non-checking peer never stamps
+    if (all[j].checkPlans != mine.checkPlans) {
+      warn("ncclCommInitRank : NBX_CHECK_PLANS / NCCL_CHECK_POINTERS differ across ranks");
+      return ncclInvalidUsage;
+    }
+    if (j == me || all[j].device == c->device) continue;
+    int can = 0;
+    HIPCHECK(hipDeviceCanAccessPeer(&can, c->device, all[j].device));
+    if (!can) {
+      // every data path here is a kernel store to peer memory; there is no
+      // host-staged transport, so fail cleanly instead of faulting later
+      warn("ncclCommInitRank : device %d cannot access peer device %d (no P2P)", c->device, all[j].device);
+      return ncclSystemError;
+    }
+    hipError_t e = hipDeviceEnablePeerAccess(all[j].device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHECK(e);
+    (void)hipGetLastError();
+  }
+  // every peer buffer mapped and checked before the first collective
+  NCCLCHECK(mpConnect(c, all));
+  NCCLCHECK(mpLL128SelfTest(c));
+  info("comm %p rank %d nranks %d device %d: multi-process communicator ready (Simple grid %d, slice %llu B, "
+       "staging %llu MiB)", (void*)c, me, n, c->device, mp->simpleGrid, (unsigned long long)mp->sliceBytes,
+       (unsigned long long)(mp->stageBytes >> 20));
+  return ncclSuccess;
+}
+
+void mpFreeState(MpState* mp, int device) {
+  DevGuard g(device);
+  (void)hipDeviceSynchronize();
+  for (void* p : mp->peerMaps) (void)hipIpcCloseMemHandle(p);
+  for (void* p : {(void*)mp->peerStageDev, (void*)mp->peerSFlagsDev, (void*)mp->scounters, (void*)mp->sflags,
+                  (void*)mp->stage, (void*)mp->peerL128Dev, (void*)mp->l128, (void*)mp->peerLLDev, (void*)mp->ll,
+                  (void*)mp->llState, (void*)mp->orderMem})
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : mp->groupEvents) (void)hipEventDestroy(e);
+  nbx::bootstrapClose(mp->bs);
+  delete mp;
+}
+
+void mpFree(ncclComm* c) {
+  if (c->mp) mpFreeState(c->mp, c->device);
+  if (c->lt) mpFreeState(c->lt, c->device);
+  c->mp = nullptr;
+  c->lt = nullptr;
+}
+
+// LL128 correctness probe at communicator creation. LL128 relies on a 64-byte
+// line written by one store instruction arriving whole (the flag in its last
+// 8 bytes vouches for the 56 payload bytes, nbx_ll.h). That holds for every
+// configuration measured here, but it is a property of the fabric between the
+// GPUs of this communicator, so each communicator checks it before use:
+// NBX_LL128_SELFTEST_ITERS (default 24; 0 = skip) AllReduces of integer data
+// that changes every call, at one-shot and at two-shot sizes, each result
+// compared exactly on the host. If any rank sees any wrong element, every rank
+// drops LL128 from its protocol set (decided from an allgather, so the choice
+// stays identical everywhere) and LL / Simple carry those sizes.
+ncclResult_t mpLL128SelfTest(ncclComm* c) {
+  MpState* mp = c->mp;
+  if (!(mp->protoMask & kProtoLL128) || mp->l128MaxBytes == 0) return ncclSuccess;
+  // only across GPUs (within one GPU the 64-byte line was stress-tested, DESIGN
+  // §6), unless NBX_LL128_SELFTEST_ITERS asks for it explicitly; multiGpu is
+  // the same on every rank (derived from every rank's PCI key)
+  const char* v = std::getenv("NBX_LL128_SELFTEST_ITERS");
+  const long iters = (v && *v) ? std::atol(v) : (mp->multiGpu ? 24 : 0);
+  if (iters <= 0) return ncclSuccess;
+  const int n = c->nRanks, me = c->rank;
+  // one-shot (just above the LL limit) and two-shot (n > 2, above the one-shot limit) sizes
+  std::vector<size_t> counts = {(size_t)(mp->llMaxBytes / 4 + 1024)};
+  const uint64_t twoShot = std::min<uint64_t>(mp->l128OneShotMax * 2, mp->l128MaxBytes);
+  if (n > 2 && twoShot > mp->l128OneShotMax) counts.push_back((size_t)(twoShot / 4 - 13));
+  size_t maxCount = 0;
+  for (size_t k : counts) maxCount = std::max(maxCount, k);
+  DevGuard g(c->device);
+  hipStream_t st = nullptr;
+  int32_t* dSend = nullptr;
+  int32_t* dRecv = nullptr;
+  HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIPCHECK(hipMalloc((void**)&dSend, maxCount * sizeof(int32_t)));
+  HIPCHECK(hipMalloc((void**)&dRecv, maxCount * sizeof(int32_t)));
+  std::vector<int32_t> hIn(maxCount), hOut(maxCount);
+  nbxDevRedOpFull sum{nbxDevSum, 0, 0};
+  int32_t bad = 0;
+  ncclResult_t r = ncclSuccess;
+  for (size_t count : counts) {
+    for (long it = 0; it < iters && r == ncclSuccess; it++) {
+      for (size_t i = 0; i < count; i++) hIn[i] = (int32_t)((i * 7 + (size_t)me * 13 + (size_t)it * 101) % 1000);
+      if (hipMemcpyAsync(dSend, hIn.data(), count * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+        r = ncclUnhandledCudaError;
+        break;
+      }
+      const MpCall call{kAllReduce, dSend, dRecv, count, ncclInt32, sum, 0, st};
+      r = runMpColl(c, call);
+      if (r != ncclSuccess) break;
+      if (hipMemcpyAsync(hOut.data(), dRecv, count * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess) {
+        r = ncclUnhandledCudaError;
+        break;
+      }
+      if (mp->hostWords[1] != 0) {   // a device wait gave up: an error, not a torn line
+        mpReportDeviceError(c);
+        warn("comm %p rank %d: LL128 self-test call %ld (%zu elements) did not complete", (void*)c, me, it, count);
+        r = ncclRemoteError;
+        break;
+      }
+      for (size_t i = 0; i < count && !bad; i++) {
+        int64_t want = 0;
+        for (int q = 0; q < n; q++) want += (int64_t)((i * 7 + (size_t)q * 13 + (size_t)it * 101) % 1000);
+        if (hOut[i] != (int32_t)want) bad = 1;
+      }
+    }
+  }
+  const char* fail = std::getenv("NBX_LL128_SELFTEST_FAIL");   // test hook: simulate a torn line
+  if (fail && std::strcmp(fail, "1") == 0) bad = 1;
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(dSend);
+  (void)hipFree(dRecv);
+  (void)hipStreamDestroy(st);
+  mp->lastSeq = 0;   // the probe's work is complete; its stream is gone
+  if (r != ncclSuccess) return r;
+  std::vector<int32_t> all(n);
+  NCCLCHECK(nbx::bootstrapAllGather(mp->bs, &bad, sizeof(bad), all.data()));
+  bool anyBad = false;
+  for (int32_t b : all) anyBad |= b != 0;
+  if (anyBad) {
+    warn("comm %p rank %d: LL128 self-test found torn lines on this fabric; LL128 disabled for this communicator",
+         (void*)c, me);
+    mp->protoMask &= ~kProtoLL128;
+  }
+  return ncclSuccess;
+}
+
+}  // namespace nbxcomm
+
+using namespace nbxcomm;
+
+NBX_API(ncclResult_t, ncclGetUniqueId, ncclUniqueId* out) {
+  if (out == nullptr) return ncclInvalidArgument;
+  return nbx::bootstrapCreateRoot(out);   // bootstrap.cc: the root listens for the ranks
+}
+
+NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank,
+        ncclConfig_t* config) {
+  if (newcomm == nullptr) return ncclInvalidArgument;
+  if (nranks < 1 || myrank < 0 || myrank >= nranks) {
+    warn("Invalid rank requested : %d/%d", myrank, nranks);
+    return ncclInvalidArgument;
+  }
+  if (config && (config->magic != 0xcafebeef || config->size != sizeof(ncclConfig_t))) {
+    warn("ncclCommInitRankConfig : config is not initialized with NCCL_CONFIG_INITIALIZER");
+    return ncclInvalidArgument;
+  }
+  if (std::memcmp(commId.internal, kIdMagic, sizeof(kIdMagic)) != 0) {
+    warn("ncclCommInitRank : unique id was not produced by ncclGetUniqueId");
+    return ncclInvalidArgument;
+  }
+  if (nranks > kMaxMpRanks) {   // one staging source region and one counter set per rank (kSimpleMaxRanks)
+    warn("ncclCommInitRank : %d ranks requested, this build supports up to %d per communicator", nranks,
+         kMaxMpRanks);
+    return ncclInvalidArgument;
+  }
+  if (config && config->blocking != NCCL_CONFIG_UNDEF_INT && config->blocking != 0 && config->blocking != 1) {
+    warn("Invalid config blocking attribute value %d", config->blocking);   // init.cc:1544-1547
+    return ncclInvalidArgument;
+  }
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  if (nranks == 1) {
+    NCCLCHECK(newComm(newcomm, 1, 0, dev, config));
+    return (*newcomm)->blocking ? ncclSuccess : ncclInProgress;   // nothing to wait for: already ready
+  }
+  if (!nbx::bootstrapIdHasRoot(commId)) {
+    warn("ncclCommInitRank : unique id carries no bootstrap root");
+    return ncclInvalidArgument;
+  }
+  ncclComm* c = nullptr;
+  NCCLCHECK(newComm(&c, nranks, myrank, dev, config));
+  auto init = [](ncclComm* cm, ncclUniqueId id) -> ncclResult_t {
+    ncclResult_t r;
+    try {
+      r = mpInit(cm, id);
+    } catch (const std::exception& e) {
+      warn("internal exception: %s", e.what());
+      r = ncclInternalError;
+    }
+    if (r != ncclSuccess) mpFree(cm);
+    return r;
+  };
+  if (!c->blocking) {
+    // non-blocking (init.cc:1757-1771, group.cc:390-415): the communicator is
+    // handed out at once and initialised by a background thread;
+    // ncclCommGetAsyncError reports ncclInProgress until it is done
+    c->asyncError.store(ncclInProgress);
+    *newcomm = c;
+    try {
+      c->initThread = std::thread([c, commId, dev, init] {
+        (void)hipSetDevice(dev);
+        nbx::bootstrapSetAbortFlag(&c->initAbort);
+        c->asyncError.store(init(c, commId));
+        nbx::bootstrapSetAbortFlag(nullptr);
+      });
+    } catch (const std::exception& e) {
+      warn("ncclCommInitRankConfig : cannot start the initialisation thread: %s", e.what());
+      c->asyncError.store(ncclSystemError);
+      return ncclSystemError;
+    }
+    return ncclInProgress;
+  }
+  const ncclResult_t r = init(c, commId);
+  if (r != ncclSuccess) {
+    delete c;
+    return r;
+  }
+  *newcomm = c;
+  return ncclSuccess;
+}
+
+NBX_API(ncclResult_t, ncclCommInitRank, ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
+  return ncclCommInitRankConfig(newcomm, nranks, commId, myrank, nullptr);
+}
+
+NBX_EXPORT int nbxDebugProtoMask(const char* ncclProto) { return protoFromString(ncclProto); }
+
+// The protocol set a communicator starts from (before its LL128 self-test):
+// NCCL_PROTO = ncclProto, its ranks on more than one GPU or not (the LL128
+// gate above; NBX_LL128_ACROSS_GPUS and NBX_DEBUG_ASSUME_MULTI_GPU apply).
+NBX_EXPORT int nbxDebugGatedProtoMask(const char* ncclProto, int multiGpu) {
+  return protoGateAcrossGpus(protoFromString(ncclProto), multiGpu != 0, ncclProto);
+}
+
+NBX_EXPORT int nbxDebugCommProtoMask(ncclComm_t comm) {
+  if (comm == nullptr || comm->magic != kCommMagic || mpOf(comm) == nullptr) return -1;
+  return mpOf(comm)->protoMask;   // a clique rank: its in-process transport's
+}
+
+// The transport settings a communicator runs with (its own, or a clique
+// rank's in-process transport's): out[0] LL max bytes, [1] LL128 max bytes,
+// [2] Simple slice bytes, [3] Simple slots, [4] Simple grid, [5] LL grid cap,
+// [6] LL128 grid cap, [7] group batching, [8] connection buffers re-exported
+// at creation because a peer's mapping of them was wrong (mpConnect), [9] plan
+// checks on (NBX_CHECK_PLANS / NCCL_CHECK_POINTERS). Returns
+// how many were written, -1
+// for a bad handle or a communicator without that transport.
+NBX_EXPORT int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut) {
+  if (comm == nullptr || comm->magic != kCommMagic || out == nullptr) return -1;
+  if (comm->asyncError.load() != ncclSuccess) return -1;
+  const MpState* mp = mpOf(comm);
+  if (mp == nullptr) return -1;
+  const int64_t v[10] = {(int64_t)mp->llMaxBytes, (int64_t)mp->l128MaxBytes, (int64_t)mp->sliceBytes, mp->slots,
+                         mp->simpleGrid,          (int64_t)mp->llGridCap,    (int64_t)mp->l128GridCap, mp->groupBatch,
+                         mp->ipcRepairs,          mp->checkPlans};
+  int k = 0;
+  for (; k < nOut && k < 10; k++) out[k] = v[k];
+  return k;
+}
+
+NBX_EXPORT int nbxDebugChooseProto(int protoMask, int twoShotKind, uint64_t slotBytes, uint64_t blockBytes, int nRanks,
+                                   uint64_t llMaxBytes, uint64_t ll128MaxBytes, uint64_t ll128OneShotMax) {
+  return (int)chooseProtoFor(protoMask, twoShotKind != 0, slotBytes, blockBytes, nRanks, llMaxBytes, ll128MaxBytes,
+                             ll128OneShotMax);
+}
+
+NBX_EXPORT ncclResult_t nbxBootstrapSelfTest(const ncclUniqueId* id, int rank, int nranks, int rounds) {
+  if (id == nullptr || nranks < 1 || rank < 0 || rank >= nranks || rounds < 0) return ncclInvalidArgument;
+  nbx::Bootstrap* b = nullptr;
+  NCCLCHECK(nbx::bootstrapConnect(*id, rank, nranks, &b));
+  ncclResult_t res = ncclSuccess;
+  for (int r = 0; r < rounds && res == ncclSuccess; r++) {
+    const size_t len = 8 + (size_t)(r * 37) % 4096;
+    std::vector<unsigned char> mine(len), all(len * (size_t)nranks);
+    for (size_t i = 0; i < len; i++) mine[i] = (unsigned char)(rank * 31 + r * 7 + i);
+    res = nbx::bootstrapAllGather(b, mine.data(), len, all.data());
+    for (int j = 0; j < nranks && res == ncclSuccess; j++)
+      for (size_t i = 0; i < len; i++)
+        if (all[(size_t)j * len + i] != (unsigned char)(j * 31 + r * 7 + i)) {
+          res = ncclInternalError;
+          break;
+        }
+  }
+  nbx::bootstrapClose(b);
+  return res;
+}
