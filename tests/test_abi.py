@@ -159,3 +159,23 @@ def test_p_aliases_are_the_same_functions(nbx):
         a = ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
         b = ctypes.cast(getattr(lib, "p" + name), ctypes.c_void_p).value
         assert a == b, name
+
+
+def test_reference_symbols_left_out(nbx):
+    """of nccl.h.in's entry points, exactly the non-reducing
+    collectives and point-to-point calls are not exported (a binary that
+    references them does not resolve against this library)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", nbx.library_path()], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines()}
+    left_out = {"ncclBcast", "ncclBroadcast", "ncclAllGather", "ncclSend", "ncclRecv"}
+    assert not (left_out & exported)
+    assert not ({"p" + s for s in left_out} & exported)
+    reference_api = {"ncclMemAlloc", "ncclMemFree", "ncclGetVersion", "ncclGetUniqueId", "ncclCommInitRankConfig",
+                     "ncclCommInitRank", "ncclCommInitAll", "ncclCommFinalize", "ncclCommDestroy", "ncclCommAbort",
+                     "ncclCommSplit", "ncclGetErrorString", "ncclGetLastError", "ncclCommGetAsyncError",
+                     "ncclCommCount", "ncclCommCuDevice", "ncclCommUserRank", "ncclRedOpCreatePreMulSum",
+                     "ncclRedOpDestroy", "ncclReduce", "ncclAllReduce", "ncclReduceScatter", "ncclGroupStart",
+                     "ncclGroupEnd", "ncclCommRegister", "ncclCommDeregister"}   # nccl.h.in:84-434, 31 minus 5
+    assert len(reference_api) + len(left_out) == 31
+    assert reference_api <= exported and {"p" + s for s in reference_api} <= exported
