@@ -511,8 +511,11 @@ def clique_leg(child, world: int, rank: int, dev: int, result_timeout: float = 4
     # model of the multi-process kernels (same kernels); the direct fold reads
     # every rank's block in place (M) and writes its block into every output
     # (M) / its own output (M / n) — model bytes, no PMC ratio measured
-    for name, model in (("allreduce", 2 * (M + 2 * (n - 1) * M // n)),
-                        ("reduce_scatter", 2 * (n - 1) * M // n + M + M // n),
+    # (without the in-kernel transport — ranks sharing a GPU — `allreduce` /
+    # `reduce_scatter` ran on the fold too: `simple_in_kernel` false)
+    ik = res.get("simple_in_kernel", True) is not False
+    for name, model in (("allreduce", 2 * (M + 2 * (n - 1) * M // n) if ik else 2 * M),
+                        ("reduce_scatter", 2 * (n - 1) * M // n + M + M // n if ik else M + M // n),
                         ("fold_allreduce", 2 * M), ("fold_reduce_scatter", M + M // n)):
         e = res.get(name)
         if isinstance(e, dict) and e.get("ms"):
