@@ -23,7 +23,7 @@ struct LLState {
   uint64_t recvAllSeq;  // last call in which this rank took lines from every peer
 };
 
-// Cross-stream order of one communicator's calls (nccl_api.cc runMpColl):
+// Cross-stream order of one communicator's calls (comm_mp_launch.cc runMpColl):
 // every eager call carries its sequence number; the launch's last block, once
 // every block's memory operations have completed, publishes it in `done`
 // (device memory). A call on another stream than the previous one is preceded
@@ -39,7 +39,7 @@ struct MpDone {
   uint64_t seq;
 };
 
-// A group of small collectives as ONE LL launch (nccl_api.cc runMpGroup; NCCL
+// A group of small collectives as ONE LL launch (comm_mp_launch.cc runMpGroup; NCCL
 // packs a group's collectives into one kernel's work, enqueue.cc:67-91): the
 // messages' slots are concatenated, 8-byte packs [packOff, packOff + packs of
 // this message) of the launch belong to segment s. Every segment has the
@@ -156,7 +156,7 @@ constexpr int kSimpleMaxGrid = 256;
 constexpr int kSimpleMaxRanks = 64;
 constexpr int kSimpleMinSliceBytes = 4096;   // a call uses at most ceil(block / 4 KiB) workgroups
 
-// A group of Simple-sized collectives as ONE launch (nccl_api.cc runMpGroup;
+// A group of Simple-sized collectives as ONE launch (comm_mp_launch.cc runMpGroup;
 // NCCL packs a group's collectives into one kernel's work, enqueue.cc:67-91):
 // every block b of the launch is the concatenation of block b of each
 // message, cut into the launch's slices; segment s owns the virtual slices

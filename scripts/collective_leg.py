@@ -223,7 +223,7 @@ def run(ids, rank, world, dev):
             res["errors"].append(f"{name}: {bad} elements differ")
 
     # LL128 in the default protocol set (bit 1): off by default across GPUs
-    # (nccl_api.cc protoGateAcrossGpus), and dropped by the creation-time probe
+    # (comm_mp_init.cc protoGateAcrossGpus), and dropped by the creation-time probe
     # if it saw a torn line
     import ctypes
     lib = nbx.load_library()

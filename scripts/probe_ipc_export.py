@@ -5,7 +5,7 @@ ncclCommSplit child of a 4-rank test, rank 2, 'invalid argument' on the LL
 buffer of a 3-rank communicator)?
 
 Raw HIP through ctypes, no libnbxccl. N processes on GPU 0 replay the
-library's communicator lifecycle (nccl_api.cc mpInit / mpFreeState) cycle
+library's communicator lifecycle (comm_mp_init.cc mpInit / mpFreeState) cycle
 after cycle: each rank allocates the four connection buffers a communicator
 of n ranks allocates (LL lines, LL128 lines, Simple staging, Simple flag
 words — the library's own sizes for that n and grid), takes an IPC handle of
@@ -73,7 +73,7 @@ def _ck(rc, what):
 
 
 def conn_sizes(n, grid):
-    """The four connection buffers of an n-rank communicator (nccl_api.cc mpAllocLL / mpInit defaults)."""
+    """The four connection buffers of an n-rank communicator (comm_mp_init.cc mpAllocLL / mpInit defaults)."""
     ll_slot = 2 * ((64 << 10) // 8)
     ll = (2 * n * ll_slot + n + 1) * 8
     half = (4 << 20) // 2

@@ -16,7 +16,7 @@ the current one (fewer switches, no flapping on noise). The ladder is
 LL -> LL128 -> Simple (a protocol once left is not re-entered: buffer limits
 are upper bounds), and a threshold is the largest swept size its protocol
 still carries. Emitted (as NBX_* environment settings, read at communicator
-creation, nccl_api.cc):
+creation, comm_mp_init.cc):
   NBX_LL_MAX_BYTES         largest size carried by LL (0 sizes: 1 KiB minimum)
   NBX_LL128_MAX_BYTES      largest size carried by LL128 (0 = LL128 never wins)
   NBX_LL128_ONESHOT_MAX    (n > 2) largest LL128 size at which one-shot is not

@@ -1,5 +1,5 @@
 """The in-process clique's in-kernel LL / LL128 transport (cliqueInitTransport,
-nccl_api.cc) as a GPU test: scripts/clique_stress.py forces it on for ranks
+comm_clique.cc) as a GPU test: scripts/clique_stress.py forces it on for ranks
 sharing the one GPU of the test box (NBX_CLIQUE_LL=1, each rank on its own
 streams and hardware queues, both set in that fresh process before HIP loads),
 runs random plans of AllReduce / ReduceScatter / Reduce across LL, LL128 one-

@@ -1030,7 +1030,7 @@ def test_multiprocess_nonblocking_init(nbx, n, monkeypatch):
 
 
 # Groups of LL-sized (and LL128 one-shot sized) calls run as ONE launch per run
-# of compatible calls (nccl_api.cc runMpGroup / runMpLLGroup): (kind, dtype,
+# of compatible calls (comm_mp_launch.cc runMpGroup / runMpLLGroup): (kind, dtype,
 # op, count, stream).
 # Runs are cut by kind / type / op / root changes, by the LL slot capacity
 # (64 KiB: the 16 x 4096-float AllReduces need four launches) and by the

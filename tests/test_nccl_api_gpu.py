@@ -1,4 +1,4 @@
-"""GPU tests of the NCCL API layer (nccl_api.cc) over the reduction core.
+"""GPU tests of the NCCL API layer (nccl_api.cc and the comm_*.cc units) over the reduction core.
 
 World size 1 follows taskAppend -> ncclLaunchOneRank (enqueue.cc:1564-1566,
 onerank.cu:48-79): PreMulSum runs the kernel, every other op is a copy.
