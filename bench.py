@@ -957,6 +957,14 @@ def headline(args, world: int, rank: int, local: int) -> dict:
         rf["frac_of_read_ceiling"] = round(achieved / max(ceil["read_GBs"], ceil["copy_GBs"]), 4)
         rf["ceiling_what"] = (ceil["what"] + "; frac_of_ceiling = achieved / mixed (the stream the fold faces), "
                               "frac_of_read_ceiling = achieved / max(read, copy)")
+    if world > 1:
+        # every GPU's own kernel rate (the weak-scaling value hides a straggler)
+        import torch.distributed as dist
+        mine = {"rank": rank, "device": local, "kernel_avg_ms": round(kern_avg_ms, 5),
+                "kernel_GBs": round(achieved, 1)}
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        result["per_rank"] = every
     if world == 1 and os.environ.get("NBX_BENCH_E2E", "1") != "0" and not args.no_cpu_baseline:
         result["host_e2e"] = host_e2e_leg(torch, nbx, srcs, out, stream, op)
     del srcs, out
