@@ -14,6 +14,9 @@
 // spin) so that EVERY CU is in its read phase, then every CU in its write
 // phase — long read-only and write-only runs of the whole chip.
 //
+// Then (clock phases, kclock) the same without any barrier: periods of the
+// shared wall clock. Results: profiles/r5/sweep_fold_phase_r5a.txt and
+// sweep_fold_phase_clock_r5e.txt — every shape loses to production.
 // Every variant's output is compared bit-exact with the static production
 // shape; times are medians of interleaved rounds in one process, same buffers.
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off scripts/sweep_fold_phase.hip -o scripts/sweep_fold_phase
@@ -151,6 +154,80 @@ __global__ __launch_bounds__(T) void kphase(Args a, unsigned* bar, unsigned* err
   }
 }
 
+// Clock phases (round 5, second try): no barrier at all — every CU reads the
+// same 100 MHz wall clock, and time itself is cut into periods of R ticks of
+// reading then W ticks of writing. In a read window a workgroup takes tiles
+// from one dynamic counter (thread 0, broadcast through LDS) and folds them
+// into LDS, until its K slots are full or the window closes; then it waits for
+// the write window and stores what it folded. Stragglers take fewer tiles
+// instead of holding everyone at a barrier. A tile is fetched only while at
+// least `margin` ticks of the read window remain (its loads must land before
+// the writes start).
+template <int K, int R, int W>
+__global__ __launch_bounds__(T) void kclock(Args a, unsigned* ctr, unsigned* err) {
+  constexpr int U = 4;
+  constexpr uint64_t kTile = (uint64_t)U * T;
+  constexpr uint64_t P = (uint64_t)R + W, margin = 150;   // 1.5 us: a tile's loads land
+  extern __shared__ f32x4 lds[];   // [K][U][T]
+  __shared__ unsigned tiles[K];
+  __shared__ unsigned bcast;
+  const uint64_t nTiles = a.nPacks / kTile;
+  bool done = false;
+  while (!done) {
+    // wait for a read window with room for at least one tile
+    if (threadIdx.x == 0) {
+      for (;;) {
+        const uint64_t ph = wall_clock64() % P;
+        if (ph + margin < (uint64_t)R) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    int k = 0;
+    for (; k < K; k++) {
+      if (threadIdx.x == 0) {
+        const uint64_t ph = wall_clock64() % P;
+        bcast = ph + margin < (uint64_t)R ? atomicAdd(ctr, 1u) : 0xfffffffeu;   // ~0u - 1: window closed
+      }
+      __syncthreads();
+      const unsigned t = bcast;
+      __syncthreads();
+      if (t == 0xfffffffeu) break;
+      if ((uint64_t)t >= nTiles) {
+        done = true;
+        break;
+      }
+      if (threadIdx.x == 0) tiles[k] = t;
+      const uint64_t p = (uint64_t)t * kTile + threadIdx.x;
+      f32x4 v[NSRC][U];
+      loadTile<U>(a, p, v);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[U];
+      fold<U>(v, acc);
+#pragma unroll
+      for (int u = 0; u < U; u++) lds[((size_t)k * U + u) * T + threadIdx.x] = acc[u];
+    }
+    __syncthreads();
+    if (k == 0) continue;
+    // the write window of this period (or of the next, if it has passed)
+    if (threadIdx.x == 0) {
+      for (;;) {
+        const uint64_t ph = wall_clock64() % P;
+        if (ph >= (uint64_t)R) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    for (int j = 0; j < k; j++) {
+      const uint64_t p = (uint64_t)tiles[j] * kTile + threadIdx.x;
+#pragma unroll
+      for (int u = 0; u < U; u++) a.dst[p + u * T] = lds[((size_t)j * U + u) * T + threadIdx.x];
+    }
+    __syncthreads();
+  }
+  (void)err;
+}
+
 struct V {
   std::string name;
   const void* fn;
@@ -160,6 +237,11 @@ struct V {
 template <int U, int K, int MODE>
 V phase(const char* name) {
   return V{name, (const void*)&kphase<U, K, MODE>, (size_t)K * U * T * 16};
+}
+
+template <int K, int R, int W>
+V clockv(const char* name) {
+  return V{name, (const void*)&kclock<K, R, W>, (size_t)K * 4 * T * 16};
 }
 
 int main(int argc, char** argv) {
@@ -189,6 +271,11 @@ int main(int argc, char** argv) {
                        phase<4, 8, 1>("chip K8 (128K)"),
                        phase<2, 16, 1>("chip U2 K16"),
                        phase<4, 8, 2>("chip2 K8"),
+                       clockv<8, 3600, 600>("clock K8 36/6"),
+                       clockv<8, 3300, 700>("clock K8 33/7"),
+                       clockv<8, 4000, 600>("clock K8 40/6"),
+                       clockv<4, 1800, 300>("clock K4 18/3"),
+                       clockv<4, 1600, 400>("clock K4 16/4"),
                        {"static (again)", (const void*)&kprod<false>, 0},
                        {"dyn1 (again)", (const void*)&kprod<true>, 0}};
   for (auto& v : vs)

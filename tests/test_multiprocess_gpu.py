@@ -1223,6 +1223,62 @@ def test_multiprocess_grouped_reduce_chain_root_and_nonroot(nbx, n, null_recv, m
             assert (zr == -1).all()
 
 
+def _child_transport(uid_bytes, rank, n, q, count):
+    """nbxDebugTransportAllReduce (config D's transport alone): the direct
+    schedule's pushes and gather with the fold reduced to a copy of the own
+    input, so block j of every rank's output is block j of rank j's input;
+    interleaved with real AllReduces on the same communicator (shared
+    sequencing and staging), which stay exact."""
+    try:
+        import ctypes
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        lib.nbxDebugTransportAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                                   ctypes.c_void_p, ctypes.c_void_p]
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        idx = torch.arange(count, dtype=torch.int32, device="cuda")
+        out = {"xport": [], "ar": []}
+        for it in range(3):
+            x = ((idx * 7 + rank * 131 + it) % 1000).to(torch.float32)
+            y = torch.full_like(x, -1.0)
+            rc = lib.nbxDebugTransportAllReduce(x.data_ptr(), y.data_ptr(), count, 7, comm.handle, st)
+            z = torch.full_like(x, -1.0)
+            comm.all_reduce(x.data_ptr(), z.data_ptr(), count, 7, 0, st)
+            torch.cuda.synchronize()
+            out["xport"].append((rc, y.cpu().numpy().copy()))
+            out["ar"].append(z.cpu().numpy().copy())
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n,count", [(2, 1 << 20), (3, 300001)])
+def test_multiprocess_transport_only_call(nbx, monkeypatch, n, count):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "30")
+    res = _run_ranks(nbx, n, _child_transport, count)
+    blocks = _blocks(count, 4, n)
+    i = np.arange(count, dtype=np.int64)
+    for it in range(3):
+        xs = [((i * 7 + r * 131 + it) % 1000).astype(np.float32) for r in range(n)]
+        want_x = np.empty(count, np.float32)
+        for j, (lo, hi) in enumerate(blocks):
+            want_x[lo:hi] = xs[j][lo:hi]
+        for r in range(n):
+            rc, y = res[r]["xport"][it]
+            assert rc == 0
+            assert np.array_equal(y, want_x), (r, it)
+            assert np.array_equal(res[r]["ar"][it], sum(xs)), (r, it)
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;
