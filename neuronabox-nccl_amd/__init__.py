@@ -321,11 +321,15 @@ class ncclConfig(ctypes.Structure):
     UNDEF_INT = -(2 ** 31)
 
     @classmethod
-    def initializer(cls, blocking: int | None = None) -> "ncclConfig":
+    def initializer(cls, blocking: int | None = None, **fields) -> "ncclConfig":
+        """NCCL_CONFIG_INITIALIZER, then `blocking` and any other field by name
+        (minCTAs, maxCTAs, cgaClusterSize, splitShare, ...)."""
         c = cls(ctypes.sizeof(cls), 0xcafebeef, 21904, cls.UNDEF_INT, cls.UNDEF_INT, cls.UNDEF_INT, cls.UNDEF_INT,
                 None, cls.UNDEF_INT)
         if blocking is not None:
             c.blocking = int(blocking)
+        for k, v in fields.items():
+            setattr(c, k, v)
         return c
 
 
@@ -342,12 +346,13 @@ class Communicator:
         return cls(h.value)
 
     @classmethod
-    def init_rank_config(cls, nranks: int, uid: ncclUniqueId, rank: int, blocking: int | None = None):
+    def init_rank_config(cls, nranks: int, uid: ncclUniqueId, rank: int, blocking: int | None = None, **fields):
         """ncclCommInitRankConfig; returns (communicator, result code). A
         non-blocking communicator (blocking=0) comes back at once with
-        ncclInProgress; poll async_error() until it is no longer ncclInProgress."""
+        ncclInProgress; poll async_error() until it is no longer ncclInProgress.
+        Other ncclConfig_t fields by name (minCTAs=..., maxCTAs=...)."""
         h = ctypes.c_void_p()
-        cfg = ncclConfig.initializer(blocking)
+        cfg = ncclConfig.initializer(blocking, **fields)
         rc = load_library().ncclCommInitRankConfig(ctypes.byref(h), int(nranks), uid, int(rank), ctypes.byref(cfg))
         if rc not in (ncclResult.ncclSuccess, ncclResult.ncclInProgress):
             _check(rc, "ncclCommInitRankConfig")

@@ -374,7 +374,7 @@ ncclResult_t cliqueInitTransport(Clique* cl) {
     mp->multiGpu = distinct;
     mp->protoMask = protoGateAcrossGpus(mp->protoMask, mp->multiGpu, std::getenv("NCCL_PROTO"));
     mp->ring = algoRingFromEnv();
-    mpTransportSettings(mp, minCus, maxShare);   // co-resident grids, as mpInit
+    mpTransportSettings(mp, minCus, maxShare, cl->comms[r]);   // co-resident grids, as mpInit
     if (simple) NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/false));
     mp->extDone = cl->evDone;
   }

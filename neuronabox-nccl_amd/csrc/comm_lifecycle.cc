@@ -35,8 +35,16 @@ NBX_API(ncclResult_t, ncclCommSplit, ncclComm_t comm, int color, int key, ncclCo
     return ncclInvalidArgument;
   }
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  if (config == nullptr) {
+  if (config == nullptr) {   // the parent's config (copyCommConfig, init.cc:1506-1510)
     cfg.blocking = comm->blocking;
+    cfg.cgaClusterSize = comm->cgaClusterSize;
+    cfg.splitShare = comm->splitShare;
+    // min / max CTAs as a pair (a lone minCTAs would fail the reference's
+    // config check in the child; an env-set one is read again there anyway)
+    if (comm->maxCTAs != NCCL_CONFIG_UNDEF_INT) {
+      cfg.maxCTAs = comm->maxCTAs;
+      if (comm->minCTAs != NCCL_CONFIG_UNDEF_INT) cfg.minCTAs = comm->minCTAs;
+    }
     config = &cfg;
   }
   DevGuard g(comm->device);

@@ -332,8 +332,13 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
 // workgroup per CU, all co-resident (workgroup g of a rank waits on workgroup
 // g of its peers); ranks sharing a GPU split its CUs, and so do the LL
 // family's spinning grids (the env caps still apply on top).
-void mpTransportSettings(MpState* mp, int minCus, int maxShare) {
-  const long maxCh = envLong("NCCL_MAX_NCHANNELS", 0), minCh = envLong("NCCL_MIN_NCHANNELS", 0);
+void mpTransportSettings(MpState* mp, int minCus, int maxShare, const ncclComm* comm) {
+  // connect.cc:418-422: channels = min(NCCL_MAX_NCHANNELS, config maxCTAs) and
+  // at least max(NCCL_MIN_NCHANNELS, config minCTAs); a channel is a workgroup here
+  long maxCh = envLong("NCCL_MAX_NCHANNELS", 0), minCh = envLong("NCCL_MIN_NCHANNELS", 0);
+  if (comm->maxCTAs != NCCL_CONFIG_UNDEF_INT && comm->maxCTAs > 0)
+    maxCh = maxCh > 0 ? std::min<long>(maxCh, comm->maxCTAs) : comm->maxCTAs;
+  if (comm->minCTAs != NCCL_CONFIG_UNDEF_INT && comm->minCTAs > 0) minCh = std::max<long>(minCh, comm->minCTAs);
   long g = envLong("NBX_SIMPLE_MAX_GRID", 0);
   if (g <= 0) {
     g = 128;
@@ -581,7 +586,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     for (int q = 0; q < n; q++) share += pres[q].pciKey == pres[j].pciKey;
     maxShare = std::max(maxShare, share);
   }
-  mpTransportSettings(mp, minCus, maxShare);
+  mpTransportSettings(mp, minCus, maxShare, c);
   NCCLCHECK(mpAllocLL(mp, n, /*ipc=*/true, c));
   mp->protoMask = protoGateAcrossGpus(mp->protoMask, mp->multiGpu, std::getenv("NCCL_PROTO"));   // before the settings are compared
   NCCLCHECK(mpAllocSimple(mp, n, /*ipc=*/true));
@@ -776,10 +781,8 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
     warn("Invalid rank requested : %d/%d", myrank, nranks);
     return ncclInvalidArgument;
   }
-  if (config && (config->magic != 0xcafebeef || config->size != sizeof(ncclConfig_t))) {
-    warn("ncclCommInitRankConfig : config is not initialized with NCCL_CONFIG_INITIALIZER");
-    return ncclInvalidArgument;
-  }
+  ncclConfig_t cfg;
+  NCCLCHECK(parseConfig(config, &cfg));   // parseCommConfig (init.cc:1526-1594)
   if (std::memcmp(commId.internal, kIdMagic, sizeof(kIdMagic)) != 0) {
     warn("ncclCommInitRank : unique id was not produced by ncclGetUniqueId");
     return ncclInvalidArgument;
@@ -789,14 +792,10 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
          kMaxMpRanks);
     return ncclInvalidArgument;
   }
-  if (config && config->blocking != NCCL_CONFIG_UNDEF_INT && config->blocking != 0 && config->blocking != 1) {
-    warn("Invalid config blocking attribute value %d", config->blocking);   // init.cc:1544-1547
-    return ncclInvalidArgument;
-  }
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
   if (nranks == 1) {
-    NCCLCHECK(newComm(newcomm, 1, 0, dev, config));
+    NCCLCHECK(newComm(newcomm, 1, 0, dev, &cfg));
     return (*newcomm)->blocking ? ncclSuccess : ncclInProgress;   // nothing to wait for: already ready
   }
   if (!nbx::bootstrapIdHasRoot(commId)) {
@@ -804,7 +803,7 @@ NBX_API(ncclResult_t, ncclCommInitRankConfig, ncclComm_t* newcomm, int nranks, n
     return ncclInvalidArgument;
   }
   ncclComm* c = nullptr;
-  NCCLCHECK(newComm(&c, nranks, myrank, dev, config));
+  NCCLCHECK(newComm(&c, nranks, myrank, dev, &cfg));
   auto init = [](ncclComm* cm, ncclUniqueId id) -> ncclResult_t {
     ncclResult_t r;
     try {

@@ -91,6 +91,13 @@ struct ncclComm {
   int rank = 0;
   int device = 0;
   int blocking = 1;
+  // ncclConfig_t minCTAs / maxCTAs after NCCL_MIN_CTAS / NCCL_MAX_CTAS
+  // (init.cc:1455-1494); NCCL_CONFIG_UNDEF_INT: not set. A CTA (channel) is a
+  // workgroup here: they bound the transports' grids (mpTransportSettings).
+  int minCTAs = NCCL_CONFIG_UNDEF_INT;
+  int maxCTAs = NCCL_CONFIG_UNDEF_INT;
+  int cgaClusterSize = NCCL_CONFIG_UNDEF_INT;   // accepted and kept (no clusters on CDNA)
+  int splitShare = NCCL_CONFIG_UNDEF_INT;       // accepted and kept (children share nothing here)
   bool checkPointers = false;
   std::atomic<int> asyncError{ncclSuccess};
   std::mutex opsMu;
@@ -186,6 +193,10 @@ ncclResult_t hostToDevRedOp(nbxDevRedOpFull* opFull, ncclRedOp_t op, ncclDataTyp
 // every block starts on a 16-byte boundary relative to the buffer.
 void blockRange(size_t count, int eb, int n, int b, size_t* off, size_t* len);
 ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclConfig_t* config);
+// parseCommConfig (init.cc:1526-1594): the caller's config copied up to its
+// own size (older versions get the defaults of the fields they predate), then
+// checked; ncclInvalidArgument, with the reference's WARN, for a bad one.
+ncclResult_t parseConfig(const ncclConfig_t* config, ncclConfig_t* out);
 
 // ---- comm_clique.cc
 ncclResult_t flushPending();   // launch every complete collective queued for every clique
@@ -272,7 +283,7 @@ MpProto chooseProtoFor(int mask, bool twoShotKind, uint64_t slotBytes, uint64_t 
 bool algoRingFromEnv();
 long envLong(const char* name, long dflt);
 ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm);
-void mpTransportSettings(MpState* mp, int minCus, int maxShare);
+void mpTransportSettings(MpState* mp, int minCus, int maxShare, const ncclComm* comm);
 ncclResult_t mpAllocSimple(MpState* mp, int n, bool ipc);
 ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id);
 ncclResult_t mpLL128SelfTest(ncclComm* c);

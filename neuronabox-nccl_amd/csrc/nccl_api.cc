@@ -272,6 +272,47 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
   return ncclSuccess;
 }
 
+ncclResult_t parseConfig(const ncclConfig_t* config, ncclConfig_t* out) {
+  const ncclConfig_t dflt = NCCL_CONFIG_INITIALIZER;
+  *out = dflt;
+  if (config == nullptr) return ncclSuccess;
+  size_t realSize = 0;
+  std::memcpy(&realSize, config, sizeof(size_t));
+  if (realSize > sizeof(ncclConfig_t)) realSize = sizeof(ncclConfig_t);
+  std::memcpy((void*)out, config, realSize);
+  if (out->magic != 0xcafebeef) {
+    warn("ncclConfig_t argument not initialized via NCCL_CONFIG_INITIALIZER");
+    return ncclInvalidArgument;
+  }
+  if (out->version < NCCL_VERSION(2, 14, 0)) out->blocking = dflt.blocking;
+  if (out->version < NCCL_VERSION(2, 17, 0)) {
+    out->cgaClusterSize = dflt.cgaClusterSize;
+    out->minCTAs = dflt.minCTAs;
+    out->maxCTAs = dflt.maxCTAs;
+    out->netName = dflt.netName;
+  }
+  if (out->blocking != NCCL_CONFIG_UNDEF_INT && out->blocking != 0 && out->blocking != 1) {
+    warn("Invalid config blocking attribute value %d", out->blocking);
+    return ncclInvalidArgument;
+  }
+  if (out->cgaClusterSize != NCCL_CONFIG_UNDEF_INT && out->cgaClusterSize < 0) {
+    warn("Invalid config cgaClusterSize attribute value %d", out->cgaClusterSize);
+    return ncclInvalidArgument;
+  }
+  // as the reference: an unset maxCTAs is INT_MIN here, so minCTAs alone fails
+  // this check too (init.cc:1555-1563)
+  if ((out->minCTAs != NCCL_CONFIG_UNDEF_INT && out->minCTAs <= 0) ||
+      (out->maxCTAs != NCCL_CONFIG_UNDEF_INT && out->maxCTAs <= 0) || out->minCTAs > out->maxCTAs) {
+    warn("Invalid config min/max channels attribute value %d/%d", out->minCTAs, out->maxCTAs);
+    return ncclInvalidArgument;
+  }
+  if (out->splitShare != NCCL_CONFIG_UNDEF_INT && out->splitShare != 0 && out->splitShare != 1) {
+    warn("Invalid config splitShare attribute value %d", out->splitShare);
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
 ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclConfig_t* config) {
   ncclComm* c = new (std::nothrow) ncclComm();
   if (c == nullptr) return ncclSystemError;
@@ -290,11 +331,31 @@ ncclResult_t newComm(ncclComm** out, int nRanks, int rank, int dev, const ncclCo
     }
     std::memset(c->hostWords, 0, 64);
   }
-  if (config && config->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = config->blocking;
-  if (const char* be = std::getenv("NCCL_COMM_BLOCKING")) {   // init.cc:1444-1446: the env overrides the config
+  if (config) {   // checked by parseConfig already
+    if (config->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = config->blocking;
+    c->minCTAs = config->minCTAs;
+    c->maxCTAs = config->maxCTAs;
+    c->cgaClusterSize = config->cgaClusterSize;
+    c->splitShare = config->splitShare;
+  }
+  // envConfigOverride (init.cc:1437-1494): the environment overrides the config
+  if (const char* be = std::getenv("NCCL_COMM_BLOCKING")) {   // init.cc:1444-1446
     char* end = nullptr;
     const long v = std::strtol(be, &end, 10);
     if (end != be && *end == '\0' && (v == 0 || v == 1)) c->blocking = (int)v;
+  }
+  auto envInt = [](const char* name, int* field) {
+    const char* v = std::getenv(name);
+    if (v == nullptr || *v == 0) return;
+    char* end = nullptr;
+    const long x = std::strtol(v, &end, 10);
+    if (end != v && *end == '\0') *field = (int)x;
+  };
+  envInt("NCCL_MIN_CTAS", &c->minCTAs);
+  envInt("NCCL_MAX_CTAS", &c->maxCTAs);
+  if (c->minCTAs != NCCL_CONFIG_UNDEF_INT && c->maxCTAs != NCCL_CONFIG_UNDEF_INT && c->minCTAs > c->maxCTAs) {
+    warn("minCTAs %d is larger than maxCTAs %d, set both to %d", c->minCTAs, c->maxCTAs, c->maxCTAs);
+    c->minCTAs = c->maxCTAs;
   }
   *out = c;
   return ncclSuccess;

@@ -179,3 +179,37 @@ def test_reference_symbols_left_out(nbx):
                      "ncclGroupEnd", "ncclCommRegister", "ncclCommDeregister"}   # nccl.h.in:84-434, 31 minus 5
     assert len(reference_api) + len(left_out) == 31
     assert reference_api <= exported and {"p" + s for s in reference_api} <= exported
+
+
+_UID = []
+
+
+def _one_rank_uid(nbx):
+    """One unique id for every case (a one-rank communicator never connects to its root)."""
+    if not _UID:
+        _UID.append(nbx.get_unique_id())
+    return _UID[0]
+
+
+@pytest.mark.parametrize("fields,ok", [
+    ({"minCTAs": 4}, False),                     # the reference's check: an unset maxCTAs is INT_MIN
+    ({"minCTAs": 0, "maxCTAs": 8}, False), ({"maxCTAs": -2}, False), ({"minCTAs": 8, "maxCTAs": 4}, False),
+    ({"splitShare": 2}, False), ({"cgaClusterSize": -1}, False), ({"blocking": 3}, False),
+    ({"magic": 0x1234}, False),
+    ({"maxCTAs": 8}, True), ({"minCTAs": 2, "maxCTAs": 8}, True), ({"splitShare": 1, "cgaClusterSize": 0}, True),
+    ({"version": 21600, "minCTAs": 0}, True),    # < 2.17: the CTA fields predate the caller and take defaults
+])
+def test_config_checks_as_parse_comm_config(nbx, fields, ok):
+    """ncclCommInitRankConfig checks the config as parseCommConfig does
+    (init.cc:1526-1594) before any device call: bad values are
+    ncclInvalidArgument; good ones get past the check (here, with no GPU, the
+    call fails later and differently, or succeeds on a GPU box)."""
+    lib = nbx.load_library()
+    cfg = nbx.ncclConfig.initializer(**fields)
+    h = ctypes.c_void_p()
+    uid = _one_rank_uid(nbx)
+    rc = lib.ncclCommInitRankConfig(ctypes.byref(h), 1, uid, 0, ctypes.byref(cfg))
+    inval = int(nbx.ncclResult.ncclInvalidArgument)
+    assert (rc != inval) if ok else (rc == inval), rc
+    if rc in (0, 7) and h.value:
+        lib.ncclCommDestroy(h)

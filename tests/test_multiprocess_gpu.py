@@ -1347,7 +1347,7 @@ def test_multiprocess_comm_split(nbx, monkeypatch):
             assert res[r]["sum2"] == float(sum(p + 1 for p in members)), (r, res[r])
 
 
-def _child_knobs(uid_bytes, rank, n, q, env):
+def _child_knobs(uid_bytes, rank, n, q, env, cfg=None):
     """The reference's own knobs (NCCL_BUFFSIZE, NCCL_LL_BUFFSIZE,
     NCCL_LL128_BUFFSIZE, NCCL_MAX/MIN_NCHANNELS) as the communicator applies
     them, then exact AllReduces at an LL, an LL128 and a Simple size. `env`:
@@ -1366,7 +1366,10 @@ def _child_knobs(uid_bytes, rank, n, q, env):
         torch.cuda.set_device(0)
         uid = nbx.ncclUniqueId.from_buffer_copy(uid_bytes)
         try:
-            comm = nbx.Communicator.init_rank(n, uid, rank)
+            if cfg is None:
+                comm = nbx.Communicator.init_rank(n, uid, rank)
+            else:   # ncclConfig_t fields (minCTAs / maxCTAs ...)
+                comm, rc = nbx.Communicator.init_rank_config(n, uid, rank, **cfg)
         except nbx.NcclError as e:
             q.put((rank, "ok", {"init": int(e.code)}))
             return
@@ -1412,6 +1415,27 @@ def test_multiprocess_reference_knobs(nbx, monkeypatch, buffsize, slice_want):
         assert (ll, l128, slice_, slots, grid) == (32768, 786432, slice_want, 2, 16), res[r]["settings"]
         assert llcap <= 16 and l128cap <= 16 and batch == 1
         assert res[r]["settings"][9] == 0   # plan checks off by default
+        assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
+
+
+@pytest.mark.parametrize("cfg,env,grid", [({"maxCTAs": 8}, {}, 8), ({"minCTAs": 16, "maxCTAs": 64}, {}, 64),
+                                          ({"maxCTAs": 64}, {"NCCL_MAX_CTAS": ["4", "4"]}, 4),
+                                          ({"maxCTAs": 100}, {"NCCL_MAX_NCHANNELS": ["12", "12"]}, 12)])
+def test_multiprocess_config_ctas(nbx, monkeypatch, cfg, env, grid):
+    """ncclConfig_t minCTAs / maxCTAs (a CTA / channel is a workgroup here,
+    connect.cc:418-422: min(NCCL_MAX_NCHANNELS, maxCTAs) and at least
+    max(NCCL_MIN_NCHANNELS, minCTAs)), NCCL_MAX_CTAS overriding the config
+    (envConfigOverride, init.cc:1460-1463): the Simple grid and the LL / LL128
+    caps follow; results exact."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    for k in ("NBX_SIMPLE_MAX_GRID", "NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_MIN_CTAS", "NCCL_MAX_CTAS"):
+        monkeypatch.delenv(k, raising=False)
+    res = _run_ranks(nbx, 2, _child_knobs, env, cfg)
+    for r in range(2):
+        assert res[r]["init"] == 0, res[r]
+        ll, l128, slice_, slots, g, llcap, l128cap = res[r]["settings"][:7]
+        assert g == grid and llcap <= grid and l128cap <= grid, res[r]["settings"]
         assert all(res[r][c] for c in (2048, 131072, 1 << 20)), res[r]
 
 
