@@ -22,6 +22,13 @@ class DevRedOpFull(ctypes.Structure):
 CASES = {   # name: (ncclDataType_t, ncclRedOp_t, element size, MiB per input)
     "f32": (7, 0, 4, 256), "f16": (6, 0, 2, 256), "bf16": (9, 0, 2, 256), "i64max": (4, 2, 8, 128),
     "fp8e4m3": (10, 0, 1, 128), "fp8e5m2": (11, 0, 1, 128), "f32max": (7, 2, 4, 256),
+    "i32max": (2, 2, 4, 256), "u32min": (3, 3, 4, 256), "i8max": (0, 2, 1, 256), "u64min": (5, 3, 8, 128),
+    "u8min": (1, 3, 1, 256), "u8sum": (1, 0, 1, 256), "i8prod": (0, 1, 1, 256), "i32prod": (2, 1, 4, 256),
+    "i64prod": (4, 1, 8, 128), "i64sum": (4, 0, 8, 128), "i32sum": (2, 0, 4, 256),
+    "i8avg": (0, 4, 1, 256), "u32avg": (3, 4, 4, 256), "i64avg": (4, 4, 8, 128),
+    "f16max": (6, 2, 2, 256), "bf16max": (9, 2, 2, 256), "f64sum": (8, 0, 8, 256), "f64max": (8, 2, 8, 256),
+    "f16prod": (6, 1, 2, 256), "f32prod": (7, 1, 4, 256), "bf16avg": (9, 4, 2, 256), "f32avg": (7, 4, 4, 256),
+    "fp8max": (10, 2, 1, 128),
 }
 
 
@@ -57,9 +64,9 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(5)
         srcs = []
         for _ in range(8):
-            if dt in (6, 9, 7):
+            if dt in (6, 9, 7, 8):
                 b = torch.rand(n, device="cuda", generator=g).to({6: torch.float16, 9: torch.bfloat16,
-                                                                    7: torch.float32}[dt]).view(torch.uint8)
+                                                                    7: torch.float32, 8: torch.float64}[dt]).view(torch.uint8)
             else:
                 b = torch.randint(0, 256, (mib << 20,), dtype=torch.uint8, device="cuda", generator=g)
                 if dt in (10, 11):
