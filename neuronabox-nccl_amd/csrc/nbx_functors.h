@@ -217,6 +217,9 @@ struct FnProdInt : FnBase<FnProdInt<E>, E> {
 template <class E>
 struct FnMinMaxInt : FnBase<FnMinMaxInt<E>, E> {
   static constexpr int kUnrollCap = sizeof(E) == 1 ? 4 : 16;
+  // bytes: a second workgroup per CU hides the SWAR fold (u8 min 5.61 -> 5.92
+  // TB/s, profiles/r5/ab_swar8_shared_out_r5k.jsonl)
+  static constexpr int kBigBlocksPerCU = sizeof(E) == 1 ? 2 : 1;
   E xormask;  // reduce_kernel.h:43-46
   __device__ explicit FnMinMaxInt(uint64_t arg) : xormask((E)arg) {}
   __device__ E red(E a, E b) const { return ((E)(a ^ xormask) < (E)(b ^ xormask)) ? a : b; }
@@ -226,7 +229,7 @@ struct FnMinMaxInt : FnBase<FnMinMaxInt<E>, E> {
   // and its bit 7 says x & 0x7f >= y & 0x7f; with the high bits that gives
   // x >= y unsigned; a byte mask of x < y selects a, else b (a tie -> b).
   // Per-byte extract / compare / select / repack cost ~5 VALU per element
-  // (4.2 TB/s at 8 x 256 MiB, profiles/r5/dtype_survey_bpc_r5h.jsonl).
+  // (4.20 TB/s at 8 x 256 MiB; this form 5.61, profiles/r5/ab_swar8_shared_out_r5k.jsonl).
   __device__ static uint32_t swarPick(uint32_t a, uint32_t b, uint32_t m) {
     const uint32_t H = 0x80808080u;
     const uint32_t x = a ^ m, y = b ^ m;
