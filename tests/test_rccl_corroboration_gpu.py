@@ -1,0 +1,83 @@
+"""Corroboration against RCCL (ROCm's NCCL-derived library, torch.distributed
+backend "nccl"), on the GPU: the only arithmetic a one-rank NCCL call performs
+is the PreMulSum pre-op (onerank.cu:14-45: y = x * scalar in the element type,
+ncclRedOpCreatePreMulSum's scalar, enqueue.cc:1648-1685) — the functor whose
+per-type rounding (f16 / bf16 through a float round trip with RNE back,
+reduce_kernel.h:424-484) the oracle restates. One rank is all a one-GPU box can
+run RCCL at (it refuses two ranks on one GPU). RCCL is not the reference
+(NCCL 2.19.4 inside NeuronaBox-NCCL) — it is a separate port of the same
+functors, so agreement here corroborates the restatement rather than pins it
+(DESIGN §3). Compared bit for bit, NaN payloads aside (NaN-ness compared)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+import torch.distributed as dist
+import bench
+bench.init_process_group("nccl", 0, 1, 0)   # before any other GPU call of this process
+torch.cuda.set_device(0)
+from tests.conftest import load_package
+nbx = load_package()
+nbx.load_library()
+comm = nbx.Communicator.init_all([0])[0]    # a one-rank communicator of libnbxccl
+st = torch.cuda.current_stream().cuda_stream
+out = []
+for dt, code in ((torch.float16, 6), (torch.bfloat16, 9), (torch.float32, 7), (torch.float64, 8)):
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = (torch.randn(1 << 16, generator=g, device="cuda", dtype=torch.float64) * 3).to(dt)
+    fi = torch.finfo(dt)
+    sp = torch.tensor([float("inf"), -float("inf"), float("nan"), 0.0, -0.0, fi.tiny, -fi.tiny, fi.tiny / 4,
+                       fi.max, -fi.max, fi.eps, 1.0, -1.0, 2.0 ** -20], dtype=torch.float64, device="cuda").to(dt)
+    x = torch.cat([x, sp])
+    n = x.numel()
+    for f in (0.1, 1.0 / 3.0, -2.5, 1e-3, 3.0, 0.125, 1.0 / 7.0, 1e-6):
+        ft = torch.tensor([f], dtype=dt, device="cuda")
+        y = x.clone()
+        dist.all_reduce(y, op=dist._make_nccl_premul_sum(ft))
+        sc = ft.cpu()                              # the same scalar bits, host-immediate for libnbxccl
+        op = comm.redop_create_premulsum(sc.data_ptr(), code)
+        z = torch.full_like(x, 7.0)
+        comm.all_reduce(x.data_ptr(), z.data_ptr(), n, code, op, st)
+        torch.cuda.synchronize()
+        comm.redop_destroy(op)
+        iy = y.view({2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()])
+        iz = z.view(iy.dtype)
+        both_nan = torch.isnan(y) & torch.isnan(z)
+        diff = ((iy != iz) & ~both_nan).nonzero().flatten()
+        out.append({"dtype": str(dt), "factor": f, "n": n, "mismatches": int(diff.numel()),
+                    "first": [[float(x[i]), float(y[i]), float(z[i])] for i in diff[:3].tolist()]})
+comm.destroy()
+dist.destroy_process_group()
+print("RESULT " + json.dumps(out), flush=True)
+"""
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_premulsum_one_rank_matches_rccl():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=env, capture_output=True, text=True, timeout=280,
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert line, p.stdout[-2000:] + p.stderr[-2000:]
+    res = json.loads(line[-1][len("RESULT "):])
+    assert len(res) == 4 * 8
+    bad = [r for r in res if r["mismatches"]]
+    assert not bad, bad[:4]
