@@ -315,10 +315,34 @@ struct FnMinMaxF : FnBase<FnMinMaxF<Ty>, typename Ty::Elt> {
     return pickA ? a : b;   // narrowing a widened value is exact: keep the bits
   }
   __device__ E red(E a, E b) const { return isMin ? pick<true>(a, b) : pick<false>(a, b); }
+  // fp8: a dword's four codes widened by two v_cvt_pk_f32_* per operand, the
+  // four picks gathered into a byte mask, one select — instead of one convert
+  // per code and operand and a byte insert per result (3.57 TB/s at 8 x 128
+  // MiB, profiles/r5/dtype_survey_bpc_r5h.jsonl)
+  template <bool MIN>
+  __device__ static uint32_t pickDword8(uint32_t a, uint32_t b) {
+    float fa[4], fb[4];
+    Ty::wide4(a, fa);
+    Ty::wide4(b, fb);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const bool p = (MIN ? (fa[i] < fb[i]) : (fa[i] > fb[i])) | isNan(fb[i]);
+      m |= p ? (0xffu << (8 * i)) : 0u;
+    }
+    return (a & m) | (b & ~m);
+  }
   // the min/max choice is uniform: decided once per pack, never per element
   // (written per element it compiled into divergent branches: 5.0 vs 6.3 TB/s
   // at config B, profiles/r2/probe_dtypes_r3d.jsonl)
   __device__ u32x4 redPack(u32x4 a, u32x4 b) const {
+    if constexpr (sizeof(E) == 1) {
+      if (isMin)
+        return u32x4{pickDword8<true>(a[0], b[0]), pickDword8<true>(a[1], b[1]), pickDword8<true>(a[2], b[2]),
+                     pickDword8<true>(a[3], b[3])};
+      return u32x4{pickDword8<false>(a[0], b[0]), pickDword8<false>(a[1], b[1]), pickDword8<false>(a[2], b[2]),
+                   pickDword8<false>(a[3], b[3])};
+    }
     PackU<E> x, y;
     x.v = a;
     y.v = b;

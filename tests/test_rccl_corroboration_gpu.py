@@ -1,6 +1,7 @@
 """Corroboration against RCCL (ROCm's NCCL-derived library, torch.distributed
 backend "nccl"), on the GPU: the only arithmetic a one-rank NCCL call performs
 is the PreMulSum pre-op (onerank.cu:14-45: y = x * scalar in the element type,
+fp16 / fp32 / fp64 here — torch passes no bf16 scalar —
 ncclRedOpCreatePreMulSum's scalar, enqueue.cc:1648-1685) — the functor whose
 per-type rounding (f16 / bf16 through a float round trip with RNE back,
 reduce_kernel.h:424-484) the oracle restates. One rank is all a one-GPU box can
@@ -32,30 +33,36 @@ nbx.load_library()
 comm = nbx.Communicator.init_all([0])[0]    # a one-rank communicator of libnbxccl
 st = torch.cuda.current_stream().cuda_stream
 out = []
-for dt, code in ((torch.float16, 6), (torch.bfloat16, 9), (torch.float32, 7), (torch.float64, 8)):
-    g = torch.Generator(device="cuda").manual_seed(11)
-    x = (torch.randn(1 << 16, generator=g, device="cuda", dtype=torch.float64) * 3).to(dt)
+# (torch dispatches its NCCL pre-multiply scalar over float / half / double
+# only: "expected scalar type Float but found BFloat16" for bf16)
+for dt, code in ((torch.float16, 6), (torch.float32, 7), (torch.float64, 8)):
     fi = torch.finfo(dt)
     sp = torch.tensor([float("inf"), -float("inf"), float("nan"), 0.0, -0.0, fi.tiny, -fi.tiny, fi.tiny / 4,
                        fi.max, -fi.max, fi.eps, 1.0, -1.0, 2.0 ** -20], dtype=torch.float64, device="cuda").to(dt)
-    x = torch.cat([x, sp])
-    n = x.numel()
-    for f in (0.1, 1.0 / 3.0, -2.5, 1e-3, 3.0, 0.125, 1.0 / 7.0, 1e-6):
-        ft = torch.tensor([f], dtype=dt, device="cuda")
-        y = x.clone()
-        dist.all_reduce(y, op=dist._make_nccl_premul_sum(ft))
-        sc = ft.cpu()                              # the same scalar bits, host-immediate for libnbxccl
-        op = comm.redop_create_premulsum(sc.data_ptr(), code)
-        z = torch.full_like(x, 7.0)
-        comm.all_reduce(x.data_ptr(), z.data_ptr(), n, code, op, st)
-        torch.cuda.synchronize()
-        comm.redop_destroy(op)
-        iy = y.view({2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()])
-        iz = z.view(iy.dtype)
-        both_nan = torch.isnan(y) & torch.isnan(z)
-        diff = ((iy != iz) & ~both_nan).nonzero().flatten()
-        out.append({"dtype": str(dt), "factor": f, "n": n, "mismatches": int(diff.numel()),
-                    "first": [[float(x[i]), float(y[i]), float(z[i])] for i in diff[:3].tolist()]})
+    for n in (1 << 16, (1 << 16) + 14):           # specials first; an aligned and a ragged count
+        g = torch.Generator(device="cuda").manual_seed(11)
+        x = torch.cat([sp, (torch.randn(n - sp.numel(), generator=g, device="cuda", dtype=torch.float64) * 3).to(dt)])
+        for f in (0.1, 1.0 / 3.0, -2.5, 1e-3, 3.0, 0.125, 1.0 / 7.0, 1e-6):
+            ft = torch.tensor([f], dtype=dt, device="cuda")
+            y = x.clone()
+            dist.all_reduce(y, op=dist._make_nccl_premul_sum(ft))
+            sc = ft.cpu()                              # the same scalar bits, host-immediate for libnbxccl
+            op = comm.redop_create_premulsum(sc.data_ptr(), code)
+            z = torch.full_like(x, 7.0)
+            comm.all_reduce(x.data_ptr(), z.data_ptr(), n, code, op, st)
+            torch.cuda.synchronize()
+            comm.redop_destroy(op)
+            iy = y.view({2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()])
+            iz = z.view(iy.dtype)
+            ix = x.view(iy.dtype)
+            both_nan = torch.isnan(y) & torch.isnan(z)
+            diff = ((iy != iz) & ~both_nan).nonzero().flatten()
+            # elements RCCL handed back unscaled though the product differs
+            untouched = ((iy == ix) & (iz != ix) & ~both_nan).nonzero().flatten()
+            out.append({"dtype": str(dt), "factor": f, "n": n, "mismatches": int(diff.numel()),
+                        "mismatch_lo": int(diff.min()) if diff.numel() else None,
+                        "untouched_by_rccl": int(untouched.numel()),
+                        "first": [[float(x[i]), float(y[i]), float(z[i])] for i in diff[:3].tolist()]})
 comm.destroy()
 dist.destroy_process_group()
 print("RESULT " + json.dumps(out), flush=True)
@@ -78,6 +85,17 @@ def test_premulsum_one_rank_matches_rccl():
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]
     assert line, p.stdout[-2000:] + p.stderr[-2000:]
     res = json.loads(line[-1][len("RESULT "):])
-    assert len(res) == 4 * 8
-    bad = [r for r in res if r["mismatches"]]
+    assert len(res) == 3 * 2 * 8
+    bad = [r for r in res if r["mismatches"] and not _rccl_f64_tail(r)]
     assert not bad, bad[:4]
+
+
+def _rccl_f64_tail(r):
+    """RCCL 2.26.6 (torch 2.10's librccl) returns the last elements of a ragged
+    fp64 one-rank PreMulSum unscaled — a copy of the input, not x * scalar (r5n:
+    every mismatch at n = 65550 was an element past 65536 left equal to its
+    input, f16 / f32 scale the same tail). That is RCCL's tail handling, not the
+    functor's arithmetic; the aligned count pins fp64 and only those tail
+    elements are excused here."""
+    return (r["dtype"] == "torch.float64" and r["n"] % 64 and r["mismatch_lo"] is not None
+            and r["mismatch_lo"] >= r["n"] - r["n"] % 64 and r["untouched_by_rccl"] == r["mismatches"])
