@@ -672,6 +672,7 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0, 
     out["hbm_model"] = simple_hbm_model(world, S)
     out["transport_allreduce"] = agg("transport_allreduce_ms", 2 * (world - 1) / world, S)
     add_hbm_rates(out, world, S)
+    add_fabric_rates(out, allres, world, S)
     # LL128 forced across the fabric (NCCL_PROTO=LL128): every call checked
     fc = [r.get("ll128_forced_checked_calls") for r in allres]
     fm = [r.get("ll128_forced_mismatched_calls") for r in allres]
@@ -714,6 +715,76 @@ def add_hbm_rates(out: dict, world: int, msg_bytes: int) -> None:
         e["hbm_GBs_per_rank"] = round(model * (r if r else 1.0) / (e["ms"] * 1e-3) / 1e9, 1)
     out["hbm_rate_what"] = ("hbm_GBs_per_rank = staging-model HBM bytes per rank x measured HBM/model ratio "
                             "(profiles/r4/simple_traffic_pmc_r4j.json; 1.0 where unmeasured) / call time")
+
+
+# bytes over an entry's busiest link, one direction (M = message, n ranks) and
+# the probe (push / pull) that prices it: the direct schedules push one block
+# to every peer per phase; the ring sends 2 (n-1) blocks to its right
+# neighbour over one link; the clique's direct fold pulls block r from every
+# peer and pushes the finished block back (both directions at once)
+FABRIC_LINK_MODELS = {
+    "allreduce_direct": (("push",), lambda n, M: 2 * M // n),
+    "transport_allreduce": (("push",), lambda n, M: 2 * M // n),
+    "reduce_scatter": (("push",), lambda n, M: M // n),
+    "allreduce_ring": (("push",), lambda n, M: 2 * (n - 1) * M // n),
+}
+FABRIC_CLIQUE_MODELS = {
+    "allreduce": (("push",), lambda n, M: 2 * M // n),
+    "reduce_scatter": (("push",), lambda n, M: M // n),
+    "fold_allreduce": (("pull", "push"), lambda n, M: M // n),
+    "fold_reduce_scatter": (("pull",), lambda n, M: M // n),
+}
+
+
+def _fabric_floor(e: dict, kinds, link_bytes: int, rates: dict) -> None:
+    if not isinstance(e, dict) or not e.get("ms") or any(k not in rates for k in kinds):
+        return
+    floor_ms = max(link_bytes / (rates[k] * 1e9) * 1e3 for k in kinds)
+    e["fabric_link_bytes"] = link_bytes
+    e["fabric_floor_ms"] = round(floor_ms, 4)
+    e["fabric_frac"] = round(floor_ms / e["ms"], 3)
+
+
+def add_fabric_rates(out: dict, allres: list, world: int, msg_bytes: int) -> None:
+    """config D against the fabric. Every rank's
+    nbxDebugLinkProbe moves the same bytes to (push: the transport's stores)
+    or from (pull: its loads) every peer at once; the per-link rate is those
+    bytes / the max-over-ranks time. An entry's floor is what its schedule
+    moves over its busiest link in one direction / that rate
+    (FABRIC_LINK_MODELS), and fabric_frac = floor / the entry's time."""
+    n = world
+    moved = [r.get("link_bytes_per_peer") for r in allres]
+    rates = {}
+    for kind in ("push", "pull"):
+        ms = [r.get(f"link_{kind}_ms") for r in allres]
+        if any(v is None for v in ms + moved) or max(ms) <= 0:
+            continue
+        rates[kind] = moved[0] / (max(ms) * 1e-3) / 1e9
+    if not rates:
+        return
+    out["fabric"] = {"bytes_per_peer": moved[0],
+                     "push_GBs_per_link": round(rates["push"], 2) if "push" in rates else None,
+                     "pull_GBs_per_link": round(rates["pull"], 2) if "pull" in rates else None,
+                     "push_GBs_per_gpu": round(rates["push"] * (n - 1), 2) if "push" in rates else None,
+                     "what": "nbxDebugLinkProbe: every rank moves bytes_per_peer to (push, system-scope stores) or "
+                             "from (pull, system-scope loads) every peer's staging at once; per link = bytes / "
+                             "max-over-ranks time; entries carry fabric_floor_ms = busiest-link bytes / that rate "
+                             "and fabric_frac = floor / time" + (" (ranks share one GPU: the 'links' are its HBM)"
+                                                                  if out.get("shared_gpu") else "")}
+    out["fabric_rates"] = rates
+    for key, (kinds, f) in FABRIC_LINK_MODELS.items():
+        _fabric_floor(out.get(key), kinds, f(n, msg_bytes), rates)
+
+
+def add_clique_fabric(coll: dict, world: int, msg_bytes: int) -> None:
+    """The clique's config-D entries against the same per-link rates (the
+    clique reaches its peers by direct pointers over the same fabric)."""
+    rates = coll.get("fabric_rates")
+    cl = coll.get("clique")
+    if not rates or not isinstance(cl, dict):
+        return
+    for key, (kinds, f) in FABRIC_CLIQUE_MODELS.items():
+        _fabric_floor(cl.get(key), kinds, f(world, msg_bytes), rates)
 
 
 def simple_hbm_model(world: int, msg_bytes: int):
@@ -985,6 +1056,7 @@ def run_legs(result: dict, world: int, rank: int, local: int, child, clique_chil
         cl = clique_leg(clique_child, world, rank, local, budget=budget)
         if coll is not None:
             coll["clique"] = cl
+            add_clique_fabric(coll, world, COUNT_D * 4)
     if os.environ.get("NBX_BENCH_RCCL", "1") != "0":
         emitter.leg = "the RCCL leg"
         left = budget.agreed_left(world)
@@ -995,6 +1067,7 @@ def run_legs(result: dict, world: int, rank: int, local: int, child, clique_chil
     emitter.leg = None
     if coll is not None:
         coll["leg_budget"] = {"budget_s": budget.total, "used_s": round(budget.total - budget.left(), 1)}
+        coll.pop("fabric_rates", None)
     return coll
 
 

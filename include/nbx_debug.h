@@ -79,6 +79,19 @@ int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut);
 ncclResult_t nbxDebugTransportAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
                                         ncclComm_t comm, ncclStream_t stream);
 
+/* Per-link fabric rate of a multi-process communicator (the roofline config
+ * D is priced against): each rank pushes (pull = 0, the Simple transport's
+ * system-scope stores) or pulls (pull = 1, its system-scope loads)
+ * bytesPerPeer to / from every peer's staging at once, in its own part of
+ * each peer's slice area, on workgroupsPerPeer workgroups per peer (0: 32).
+ * One kernel on `stream`; *bytesMovedPerPeer = the bytes one launch moves per
+ * peer (bytesPerPeer rounded up to whole passes). Not ordered against
+ * collectives and it overwrites the peers' staging: the caller keeps every
+ * rank's communicator quiet around it. ncclInvalidArgument without a
+ * multi-process transport. Measurement only. */
+ncclResult_t nbxDebugLinkProbe(ncclComm_t comm, size_t bytesPerPeer, int pull, int workgroupsPerPeer,
+                               ncclStream_t stream, size_t* bytesMovedPerPeer);
+
 /* Stream ceilings in the caller's process (SURVEY §8(d) "a measured stream
  * ceiling"): kind 0 reads nSrcs == 8 buffers of `bytes` each with the hot
  * kernel's loads and tile (16-B nontemporal, 8 x 4 packs per lane, one

@@ -666,7 +666,7 @@ void mpFreeState(MpState* mp, int device) {
   for (void* p : mp->peerMaps) (void)hipIpcCloseMemHandle(p);
   for (void* p : {(void*)mp->peerStageDev, (void*)mp->peerSFlagsDev, (void*)mp->scounters, (void*)mp->sflags,
                   (void*)mp->stage, (void*)mp->peerL128Dev, (void*)mp->l128, (void*)mp->peerLLDev, (void*)mp->ll,
-                  (void*)mp->llState, (void*)mp->orderMem})
+                  (void*)mp->llState, (void*)mp->orderMem, (void*)mp->probeSink})
     if (p) (void)hipFree(p);
   for (hipEvent_t e : mp->groupEvents) (void)hipEventDestroy(e);
   nbx::bootstrapClose(mp->bs);

@@ -350,3 +350,36 @@ NBX_EXPORT ncclResult_t nbxDebugTransportAllReduce(const void* sendbuff, void* r
     return ncclInternalError;
   }
 }
+
+// Per-link fabric rate (the roofline config D's entries are priced against):
+// every rank moves `bytesPerPeer` to (pull = 0: the transport's system-scope
+// stores) or from (pull = 1: its system-scope loads) each peer's Simple
+// staging at once, in its own part of the peer's data area (the slices, never
+// the flag words or plan headers), with workgroupsPerPeer workgroups per peer
+// (0: 32). One kernel on `stream`; *bytesMovedPerPeer receives what one launch
+// moves per peer (bytesPerPeer rounded to whole passes over the part). NOT
+// ordered against collectives: the caller keeps every rank's communicator
+// quiet around it (no Simple call in flight on any rank) — it overwrites the
+// peers' staging slices. Measurement only.
+NBX_EXPORT ncclResult_t nbxDebugLinkProbe(ncclComm_t comm, size_t bytesPerPeer, int pull, int workgroupsPerPeer,
+                                         ncclStream_t stream, size_t* bytesMovedPerPeer) {
+  NCCLCHECK(commCheck(comm, "LinkProbe"));
+  NCCLCHECK(commEnsureReady(comm));
+  MpState* mp = comm->mp;
+  const int n = comm->nRanks;
+  if (mp == nullptr || n < 2 || bytesPerPeer == 0 || bytesMovedPerPeer == nullptr || workgroupsPerPeer < 0)
+    return ncclInvalidArgument;
+  const int wg = workgroupsPerPeer > 0 ? workgroupsPerPeer : 32;
+  // this rank's part of a peer's slices: 16-B packs, whole per workgroup, < 2 GiB
+  const uint64_t part = std::min<uint64_t>(mp->stageHdrOff / (uint64_t)n, 1ull << 30) & ~(uint64_t)(16 * wg - 1);
+  if (part == 0) return ncclInvalidArgument;
+  const uint64_t chunkPacks = part / 16 / (uint64_t)wg;
+  const uint64_t perPass = chunkPacks * 16 * (uint64_t)wg;
+  const uint64_t passes = std::max<uint64_t>(1, (bytesPerPeer + perPass - 1) / perPass);
+  if (passes > (1u << 20)) return ncclInvalidArgument;
+  DevGuard g(comm->device);
+  if (mp->probeSink == nullptr) HIPCHECK(hipMalloc((void**)&mp->probeSink, nbx::kLinkProbeSinkWords * sizeof(uint32_t)));
+  *bytesMovedPerPeer = (size_t)(passes * perPass);
+  return nbx::launchLinkProbe(mp->peerStageDev, comm->rank, n, part, chunkPacks, wg, (int)passes, pull != 0,
+                              mp->probeSink, (hipStream_t)stream);
+}

@@ -240,6 +240,7 @@ struct MpState {
   uint64_t* scounters = nullptr;
   char** peerStageDev = nullptr;
   uint64_t** peerSFlagsDev = nullptr;
+  uint32_t* probeSink = nullptr;    // nbxDebugLinkProbe's never-written pull sink (allocated on first use)
   uint64_t sliceBytes = 0;          // NBX_SIMPLE_SLICE_BYTES: staging bytes per (slot, source, workgroup)
   int slots = 2;                    // NBX_SIMPLE_SLOTS
   int simpleGrid = 0;               // workgroups of a full-size Simple call (NBX_SIMPLE_MAX_GRID, CU-capped)

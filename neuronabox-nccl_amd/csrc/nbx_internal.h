@@ -54,6 +54,12 @@ ncclResult_t launchMpWaitDone(const uint64_t* done, uint64_t target, const volat
 // measurement only, nbx_simple_bench.cc): n x grid workgroups, argsDev[n].
 ncclResult_t launchSimpleFusedF32Sum(const SimpleArgs* argsDev, int n, unsigned grid, bool ring, hipStream_t stream);
 int simpleFusedMaxResident(bool ring);   // workgroups of kSimpleFused resident at once (-1: HIP error)
+// nbxDebugLinkProbe's kernel (nbx_ll_debug.hip): (n - 1) x wgPerPeer workgroups,
+// each moving chunkPacks 16-B packs of this rank's part of one peer's staging,
+// `passes` times; sink[kLinkProbeSinkWords] is written only by a pull, and only in theory.
+constexpr int kLinkProbeSinkWords = 256;   // = kBlock (nbx_kargs.h)
+ncclResult_t launchLinkProbe(char* const* peerStageDev, int me, int n, uint64_t part, uint64_t chunkPacks,
+                             int wgPerPeer, int passes, bool pull, uint32_t* sink, hipStream_t stream);
 // LL128 two-shot AllReduce (args.nLines = sub-slot lines; blockLines sizes the grid).
 ncclResult_t launchLL128AllReduce2(ncclDataType_t dt, const nbxDevRedOpFull& op, LLArgs& args, uint64_t blockLines,
                                    hipStream_t stream);

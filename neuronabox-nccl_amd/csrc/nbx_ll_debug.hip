@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "../../include/nbx_debug.h"
+#include "nbx_internal.h"
 #include "nbx_kernels.h"
 
 namespace nbx {
@@ -49,7 +50,58 @@ __global__ __launch_bounds__(64) void kL128TearReader(LLArgs a, uint32_t flag, u
   l128FoldLine(fn, a, v, 0, t, 1, a.blockElts, [&](int, uint64_t off, uint64_t w) { llStoreBytes(out, off, kL128DataBytes, w); });
 }
 
+// Link probe (nbxDebugLinkProbe): workgroup w serves peer q = the w / wgPerPeer-th
+// other rank, moving chunk j = w % wgPerPeer of this rank's part of q's Simple
+// data area — pushed with the transport's system-scope stores, or pulled with
+// its system-scope loads — `passes` times over. Four packs in flight per lane
+// per step; a pull's loads stay live through an XOR that is stored only if it
+// equals a value no real data produces.
+template <bool PULL>
+__global__ __launch_bounds__(kBlock) void kLinkProbe(char* const* peerStage, int me, uint64_t part,
+                                                     uint64_t chunkPacks, int wgPerPeer, int passes, uint32_t* sink) {
+  const int w = (int)blockIdx.x;
+  int q = w / wgPerPeer;
+  q += q >= me ? 1 : 0;
+  const uint64_t j = (uint64_t)(w % wgPerPeer);
+  const __amdgpu_buffer_rsrc_t rs = sysRsrc(peerStage[q] + (uint64_t)me * part, part);
+  const uint64_t base = j * chunkPacks;
+  const uint64_t step = 4ull * blockDim.x;
+  u32x4 acc = {(uint32_t)me, (uint32_t)j, 0u, 0u};
+  for (int pass = 0; pass < passes; pass++) {
+    for (uint64_t i = threadIdx.x; i < chunkPacks; i += step) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint64_t k = i + (uint64_t)u * blockDim.x;
+        if (k < chunkPacks) {
+          if constexpr (PULL) v[u] = ldSys(rs, base + k);
+          else stSys(rs, base + k, acc + (u32x4){(uint32_t)k, (uint32_t)pass, 0u, 0u});
+        }
+      }
+      if constexpr (PULL) {
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (i + (uint64_t)u * blockDim.x < chunkPacks) acc ^= v[u];
+      }
+    }
+  }
+  if (PULL && acc[0] == 0x9e3779b9u && acc[1] == 0x7f4a7c15u && acc[2] == 0xf39cc060u) sink[threadIdx.x] = acc[3];
+}
+
 }  // namespace
+
+ncclResult_t launchLinkProbe(char* const* peerStageDev, int me, int n, uint64_t part, uint64_t chunkPacks,
+                             int wgPerPeer, int passes, bool pull, uint32_t* sink, hipStream_t stream) {
+  static_assert(kLinkProbeSinkWords == kBlock, "one sink word per lane");
+  const dim3 grid((unsigned)((n - 1) * wgPerPeer));
+  if (pull)
+    hipLaunchKernelGGL(kLinkProbe<true>, grid, dim3(kBlock), 0, stream, peerStageDev, me, part, chunkPacks, wgPerPeer,
+                       passes, sink);
+  else
+    hipLaunchKernelGGL(kLinkProbe<false>, grid, dim3(kBlock), 0, stream, peerStageDev, me, part, chunkPacks,
+                       wgPerPeer, passes, sink);
+  return hipGetLastError() == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+}
 
 // The Simple rig's call as ONE dispatch (kSimpleFused, fp32 sum only): every
 // rank's workgroups in one grid, so rocprofv3's PMC passes can count the

@@ -192,6 +192,40 @@ def ll128_stress(c, rank, world, st, res):
     res["ll128_forced_mismatched_calls"] = bad
 
 
+LINK_PROBE_BYTES = 256 << 20   # per peer per launch
+
+
+def link_probe(lib, comm, st, res):
+    """The fabric's per-link rate (what config D is priced against, bench.py
+    add_fabric_rates): every rank pushes to, then pulls from, every peer's
+    staging at once (nbxDebugLinkProbe). The probe overwrites the peers'
+    staging slices, so the communicator is kept quiet around it: a small
+    AllReduce (LL, not the staging) after each rank's stream drained, before
+    the first probe and after the last — no peer is still in a Simple call
+    when the probes start, or still probing when the next one starts."""
+    import ctypes
+    import torch
+    lib.nbxDebugLinkProbe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                      ctypes.POINTER(ctypes.c_size_t)]
+    moved = ctypes.c_size_t(0)
+
+    def quiet():
+        torch.cuda.synchronize()
+        for f in _ALIGN:
+            f()
+        torch.cuda.synchronize()
+
+    for pull, name in ((0, "push"), (1, "pull")):
+        def probe():
+            rc_ = lib.nbxDebugLinkProbe(comm.handle, LINK_PROBE_BYTES, pull, 0, st, ctypes.byref(moved))
+            if rc_ != 0:
+                raise RuntimeError(f"nbxDebugLinkProbe: {rc_}")
+        quiet()
+        res[f"link_{name}_ms"] = _time_calls(probe, ITERS)
+    quiet()
+    res["link_bytes_per_peer"] = int(moved.value)
+
+
 def run(ids, rank, world, dev):
     import torch
     nbx = _pkg()
@@ -264,6 +298,7 @@ def run(ids, rank, world, dev):
     xport()
     torch.cuda.synchronize()
     res["transport_allreduce_ms"] = _time_calls(xport, ITERS)
+    link_probe(lib, comm, st, res)
     _progress("config D timed", res)
 
     # Simple path with inputs that change every call (direct and ring schedules,

@@ -34,6 +34,7 @@ for line in sys.stdin:
             time.sleep(600)
         print("RESULT " + json.dumps({"rank": rank, "ok": True, "errors": [], "allreduce_direct_ms": 10.0 + rank,
                                       "transport_allreduce_ms": 6.0, "reduce_scatter_ms": 5.0,
+                                      "link_push_ms": 4.0 + rank, "link_pull_ms": 2.0, "link_bytes_per_peer": 1 << 28,
                                       "ipc_repairs": {"direct": rank, "ring": 0},
                                       "ll128_forced_checked_calls": 2000, "ll128_forced_mismatched_calls": 0}),
               flush=True)
@@ -173,3 +174,15 @@ def test_legs_finish_normally_inside_the_budget(tmp_path):
     r = ard["hbm_over_model_applied"]
     assert abs(ard["hbm_GBs_per_rank"] - round(ard["hbm_model_bytes_per_rank"] * r / 11e-3 / 1e9, 1)) < 1e-9
     assert coll["leg_budget"]["budget_s"] == 60.0
+    # the fabric: per-link rates from the slowest rank's probe, floors per entry
+    fab = coll["fabric"]
+    push, pull = (1 << 28) / 5e-3 / 1e9, (1 << 28) / 2e-3 / 1e9
+    assert abs(fab["push_GBs_per_link"] - round(push, 2)) < 1e-9 and abs(fab["pull_GBs_per_link"] - round(pull, 2)) < 1e-9
+    assert "fabric_rates" not in coll
+    floor = 2 * M // n / (push * 1e9) * 1e3
+    assert ard["fabric_link_bytes"] == 2 * M // n and abs(ard["fabric_floor_ms"] - round(floor, 4)) < 1e-9
+    assert abs(ard["fabric_frac"] - round(floor / 11.0, 3)) < 1e-9
+    rs = coll["reduce_scatter"]
+    assert rs["fabric_link_bytes"] == M // n
+    fa = coll["clique"]["fold_allreduce"]
+    assert abs(fa["fabric_floor_ms"] - round(max(M // n / (pull * 1e9), M // n / (push * 1e9)) * 1e3, 4)) < 1e-9

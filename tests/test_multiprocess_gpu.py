@@ -1279,6 +1279,72 @@ def test_multiprocess_transport_only_call(nbx, monkeypatch, n, count):
             assert np.array_equal(res[r]["ar"][it], sum(xs)), (r, it)
 
 
+def _child_link_probe(uid_bytes, rank, n, q):
+    """nbxDebugLinkProbe (the fabric rate config D is priced against): push
+    and pull launches succeed and report whole passes of at least the asked
+    bytes; bad arguments are refused; a Simple-sized AllReduce after it (the
+    communicator kept quiet around the probe, as collective_leg.py does) is
+    exact although the probe overwrote the staging slices."""
+    try:
+        import ctypes
+
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        lib.nbxDebugLinkProbe.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        a = torch.ones(16, device="cuda")
+        b = torch.empty_like(a)
+
+        def quiet():
+            torch.cuda.synchronize()
+            comm.all_reduce(a.data_ptr(), b.data_ptr(), 16, 7, 0, st)
+            torch.cuda.synchronize()
+
+        moved = ctypes.c_size_t(0)
+        out = {"rc": [], "moved": []}
+        quiet()
+        for pull, nbytes, wg in ((0, 64 << 20, 0), (1, 64 << 20, 0), (0, 3 << 20, 8), (1, 1, 5)):
+            out["rc"].append(lib.nbxDebugLinkProbe(comm.handle, nbytes, pull, wg, st, ctypes.byref(moved)))
+            out["moved"].append((nbytes, wg, int(moved.value)))
+        quiet()
+        out["bad"] = [lib.nbxDebugLinkProbe(comm.handle, 0, 0, 0, st, ctypes.byref(moved)),
+                      lib.nbxDebugLinkProbe(comm.handle, 1 << 20, 0, -1, st, ctypes.byref(moved)),
+                      lib.nbxDebugLinkProbe(comm.handle, 1 << 20, 0, 0, st, None)]
+        count = 8 << 20   # 32 MiB fp32: the Simple protocol, through the staging the probe overwrote
+        idx = torch.arange(count, dtype=torch.int32, device="cuda")
+        x = ((idx * 7 + rank * 131) % 1000).to(torch.float32)
+        y = torch.full_like(x, -1.0)
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 7, 0, st)
+        torch.cuda.synchronize()
+        want = sum(((idx * 7 + r * 131) % 1000).to(torch.float32) for r in range(n))
+        out["exact"] = bool(torch.equal(y, want))
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multiprocess_link_probe(nbx, monkeypatch, n):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "30")
+    res = _run_ranks(nbx, n, _child_link_probe)
+    for r in range(n):
+        o = res[r]
+        assert o["rc"] == [0, 0, 0, 0], o
+        for nbytes, wg, moved in o["moved"]:
+            assert moved >= nbytes and moved % (16 * (wg or 32)) == 0, (nbytes, wg, moved)
+        assert o["bad"] == [4, 4, 4], o   # ncclInvalidArgument
+        assert o["exact"], r
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;
