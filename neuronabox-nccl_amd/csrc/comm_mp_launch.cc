@@ -370,10 +370,11 @@ NBX_EXPORT ncclResult_t nbxDebugLinkProbe(ncclComm_t comm, size_t bytesPerPeer, 
   if (mp == nullptr || n < 2 || bytesPerPeer == 0 || bytesMovedPerPeer == nullptr || workgroupsPerPeer < 0)
     return ncclInvalidArgument;
   const int wg = workgroupsPerPeer > 0 ? workgroupsPerPeer : 32;
-  // this rank's part of a peer's slices: 16-B packs, whole per workgroup, < 2 GiB
-  const uint64_t part = std::min<uint64_t>(mp->stageHdrOff / (uint64_t)n, 1ull << 30) & ~(uint64_t)(16 * wg - 1);
-  if (part == 0) return ncclInvalidArgument;
+  // this rank's part of a peer's slices (16-B packs, < 2 GiB for the buffer
+  // resource), cut into one whole chunk per workgroup
+  const uint64_t part = std::min<uint64_t>(mp->stageHdrOff / (uint64_t)n, 1ull << 30) & ~15ull;
   const uint64_t chunkPacks = part / 16 / (uint64_t)wg;
+  if (chunkPacks == 0) return ncclInvalidArgument;
   const uint64_t perPass = chunkPacks * 16 * (uint64_t)wg;
   const uint64_t passes = std::max<uint64_t>(1, (bytesPerPeer + perPass - 1) / perPass);
   if (passes > (1u << 20)) return ncclInvalidArgument;
