@@ -14,12 +14,18 @@
 // is innocuous and every op is correctly rounded):
 //   f16  : native v_add_f16 / v_mul_f16 (RNE), packed by the compiler.
 //   bf16 : widen (shift), fp32 op, v_cvt_pk_bf16_f32 (RNE, NaN stays NaN).
-//   fp8  : v_cvt_pk_f32_{fp8,bf8} widen, fp32 op, v_cvt_pk_{fp8,bf8}_f32 narrow
-//          (RNE; overflow -> NaN for e4m3fn, -> inf for e5m2). The hardware
-//          narrowing was checked equal to the software definition f32ToSmall
-//          on all 2^32 fp32 inputs (scripts/probe_fp8_cvt.hip,
-//          profiles/r1/probe_fp8_cvt.txt). Not in the reference: this build's
-//          definition.
+//   fp8  : v_cvt_pk_f32_{fp8,bf8} widen, fp32 op, saturate, v_cvt_pk_{fp8,bf8}_f32
+//          narrow (RNE). Saturation is HIP's __HIP_SATFINITE (amd_hip_fp8.h),
+//          what RCCL's fp8 functors narrow with: a finite result beyond the
+//          largest finite code becomes that code with its sign; inf and NaN
+//          go through (e5m2 inf; e4m3fn, which has none, NaN). The converter
+//          alone was checked equal to f32ToSmall on all 2^32 fp32 inputs
+//          (scripts/probe_fp8_cvt.hip, profiles/r1/probe_fp8_cvt.txt), the
+//          saturated form to f32ToSmallSat (scripts/probe_fp8_sat.hip,
+//          profiles/r5/probe_fp8_sat_r5t.txt), and the one-rank PreMulSum to
+//          RCCL 2.26's on every code (tests/test_rccl_corroboration_gpu.py).
+//          Not in the reference (NCCL 2.19 has no fp8): this build's
+//          definition, aligned with the NCCL lineage's AMD port.
 //   f32/f64 : native IEEE ops; denormals preserved (.amdhsa_float_denorm_mode 3);
 //          build with -ffp-contract=off so x*s + acc is never fused.
 //   min/max (floats): NaN operand yields the other operand, ties return the
@@ -67,9 +73,10 @@ struct TyBF16 {
 };
 
 // fp8 narrowing, specification form: OCP e4m3fn / e5m2, round-to-nearest-even,
-// overflow -> NaN (e4m3fn, which has no infinity) / -> +-inf (e5m2). Kernels
-// use the hardware converter, which equals this function bit for bit (up to
-// the NaN code) on every fp32 input; kept as the executable specification.
+// overflow -> NaN (e4m3fn, which has no infinity) / -> +-inf (e5m2) — the
+// hardware converter's behaviour, which equals this function bit for bit (up
+// to the NaN code) on every fp32 input. Kernels narrow with SATFINITE first
+// (f32ToSmallSat below, satE4M3 / satE5M2 above the types).
 template <int E, int M, bool FN>
 __device__ __forceinline__ uint32_t f32ToSmall(float x) {
   const uint32_t u = __float_as_uint(x);
@@ -97,13 +104,42 @@ __device__ __forceinline__ uint32_t f32ToSmall(float x) {
   enc = a >= 0x7f800000u ? (a == 0x7f800000u && !FN ? infCode : nanCode) : enc;
   return sign | enc;
 }
+// ... with SATFINITE (the kernels' narrowing): a finite x beyond the largest
+// finite value becomes the largest finite code with x's sign.
+template <int E, int M, bool FN>
+__device__ __forceinline__ uint32_t f32ToSmallSat(float x) {
+  constexpr uint32_t expAllOnes = ((1u << E) - 1u) << M;
+  constexpr uint32_t maxFinite = FN ? (expAllOnes | ((1u << M) - 2u))
+                                    : ((expAllOnes - (1u << M)) | ((1u << M) - 1u));
+  constexpr float maxf = FN ? 448.0f : 57344.0f;
+  static_assert(E + M == 7 && (FN ? E == 4 : E == 5), "OCP e4m3fn / e5m2 only");
+  const uint32_t u = __float_as_uint(x);
+  if ((u & 0x7f800000u) != 0x7f800000u && __builtin_fabsf(x) > maxf) return ((u >> 31) << 7) | maxFinite;
+  return f32ToSmall<E, M, FN>(x);
+}
+
+// SATFINITE before the converter. e4m3fn: clamp, then x * 0 + clamped puts
+// NaN back for a NaN or infinite x (inf * 0 = NaN: e4m3fn narrows inf to NaN
+// anyway) and is exact otherwise — two instructions. e5m2 keeps infinities,
+// so the clamp is selected by a finiteness test instead.
+__device__ __forceinline__ float satE4M3(float x) {
+  return __builtin_fmaf(x, 0.0f, __builtin_amdgcn_fmed3f(x, 448.0f, -448.0f));
+}
+__device__ __forceinline__ float satE5M2(float x) {
+  return __builtin_isfinite(x) ? __builtin_amdgcn_fmed3f(x, 57344.0f, -57344.0f) : x;
+}
 
 struct TyE4M3 {
   using Elt = uint8_t; using C = float;
   __device__ static C wide(Elt e) { return __builtin_amdgcn_cvt_pk_f32_fp8((int)e, false)[0]; }
-  __device__ static Elt narrow(C c) { return (Elt)(__builtin_amdgcn_cvt_pk_fp8_f32(c, c, 0, false) & 0xff); }
+  __device__ static Elt narrow(C c) {
+    const float s = satE4M3(c);
+    return (Elt)(__builtin_amdgcn_cvt_pk_fp8_f32(s, s, 0, false) & 0xff);
+  }
   // two results into bytes {0,1} (hi = false) or {2,3} (hi = true) of `old`
   __device__ static uint32_t narrow2(float x, float y, uint32_t old, bool hi) {
+    x = satE4M3(x);
+    y = satE4M3(y);
     return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x, y, (int)old, true)
               : (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x, y, (int)old, false);
   }
@@ -117,8 +153,13 @@ struct TyE4M3 {
 struct TyE5M2 {
   using Elt = uint8_t; using C = float;
   __device__ static C wide(Elt e) { return __builtin_amdgcn_cvt_pk_f32_bf8((int)e, false)[0]; }
-  __device__ static Elt narrow(C c) { return (Elt)(__builtin_amdgcn_cvt_pk_bf8_f32(c, c, 0, false) & 0xff); }
+  __device__ static Elt narrow(C c) {
+    const float s = satE5M2(c);
+    return (Elt)(__builtin_amdgcn_cvt_pk_bf8_f32(s, s, 0, false) & 0xff);
+  }
   __device__ static uint32_t narrow2(float x, float y, uint32_t old, bool hi) {
+    x = satE5M2(x);
+    y = satE5M2(y);
     return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(x, y, (int)old, true)
               : (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(x, y, (int)old, false);
   }

@@ -39,8 +39,12 @@
  *
  * fp8 (OCP e4m3fn, e5m2): NOT in the reference (NCCL 2.19 has no fp8 type) —
  * PARITY UNPINNED by the reference; this build's own definition, following the
- * half pattern: op in fp32, round-to-nearest-even to fp8; overflow -> NaN for
- * e4m3fn (no infinity), -> +-inf for e5m2.
+ * half pattern: op in fp32, round-to-nearest-even to fp8 with SATFINITE as
+ * HIP's amd_hip_fp8.h defines it (what RCCL 2.26's fp8 functors narrow with):
+ * a finite value beyond the largest finite code becomes that code with its
+ * sign; +-inf and NaN go through (e5m2 +-inf; e4m3fn, which has no infinity,
+ * NaN). Corroborated against RCCL's one-rank PreMulSum on every code
+ * (tests/test_rccl_corroboration_gpu.py).
  *
  * PIN STATUS: the reference cannot be built here (its device headers need
  * cuda_runtime.h / cuda_fp16.h / PTX; writing stand-ins is not permitted), and
@@ -136,10 +140,23 @@ uint16_t oracle_f32_to_bf16(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);                                              /* RNE */
   return (uint16_t)(u >> 16);
 }
+/* fp8 narrowing with SATFINITE (header): finite |x| above the largest finite
+ * value (448 e4m3fn, 57344 e5m2) -> the largest finite code with x's sign. */
+static uint32_t f32_to_fp8_sat(float x, int E, int M, int fn) {
+  uint32_t u = f2u(x);
+  float maxv = fn ? 448.0f : 57344.0f;
+  if ((u & 0x7f800000u) != 0x7f800000u && fabsf(x) > maxv) {
+    uint32_t expAllOnes = ((1u << E) - 1u) << M;
+    uint32_t maxFinite = fn ? (expAllOnes | ((1u << M) - 2u)) : (expAllOnes - (1u << M)) | ((1u << M) - 1u);
+    return ((u >> 31) << (E + M)) | maxFinite;
+  }
+  return f32_to_small(x, E, M, fn);
+}
+
 float oracle_e4m3_to_f32(uint8_t c) { return small_to_f32(c, 4, 3, 1); }
-uint8_t oracle_f32_to_e4m3(float f) { return (uint8_t)f32_to_small(f, 4, 3, 1); }
+uint8_t oracle_f32_to_e4m3(float f) { return (uint8_t)f32_to_fp8_sat(f, 4, 3, 1); }
 float oracle_e5m2_to_f32(uint8_t c) { return small_to_f32(c, 5, 2, 0); }
-uint8_t oracle_f32_to_e5m2(float f) { return (uint8_t)f32_to_small(f, 5, 2, 0); }
+uint8_t oracle_f32_to_e5m2(float f) { return (uint8_t)f32_to_fp8_sat(f, 5, 2, 0); }
 
 /* ------------------------------------------------------------------------ */
 /* Element functors. fminf/fmaxf restated (see header).                       */

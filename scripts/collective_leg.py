@@ -381,8 +381,8 @@ def config_e(comm, rank, world, st, res):
     finite codes), checked bit-exact against a GPU restatement on the same
     seeded inputs (every rank regenerates every rank's input): max is
     order-free; the fp8 sum folds each block c in the direct schedule's order
-    c+1, ..., c with an fp32 add and an RNE narrowing per step (NaN = any NaN
-    code, the kernel's and torch's NaN encodings may differ)."""
+    c+1, ..., c with an fp32 add and a saturating RNE narrowing per step
+    (SATFINITE: clamp to +-448, then torch's cast; NaN = any NaN code)."""
     import torch
     I64, F8, MAX, SUM = 4, 10, 2, 0
 
@@ -420,12 +420,13 @@ def config_e(comm, rank, world, st, res):
             continue
         acc = xs[(c + 1) % world][lo:hi].view(f8)
         for q in range(1, world):
-            acc = (acc.float() + xs[(c + 1 + q) % world][lo:hi].view(f8).float()).to(f8)
+            acc = (acc.float() + xs[(c + 1 + q) % world][lo:hi].view(f8).float()).clamp(-448.0, 448.0).to(f8)
         exp[lo:hi] = acc.view(torch.uint8)
     nan_e = (exp & 0x7f) == 0x7f
     nan_g = (y & 0x7f) == 0x7f
     ok_f = bool(((y == exp) | (nan_e & nan_g)).all().item())
     res["config_e_fp8_nan_fraction"] = round(float(nan_e.float().mean().item()), 4)
+    res["config_e_fp8_saturated_fraction"] = round(float(((exp & 0x7f) == 0x7e).float().mean().item()), 4)
     res["config_e_fp8_sum_ms"] = _time_calls(lambda: comm.all_reduce(xs[rank].data_ptr(), y.data_ptr(), E_F8, F8, SUM,
                                                                       st), ITERS)
     del xs, y, exp

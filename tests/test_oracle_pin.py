@@ -140,7 +140,10 @@ def test_bf16_codec_matches_torch(oracle):
 @pytest.mark.parametrize("dtype", [10, 11])
 def test_fp8_codec_matches_torch(oracle, dtype):
     """fp8 is this build's extension (parity unpinned vs the reference); the
-    codec itself is checked against torch's OCP float8 types."""
+    codec itself is checked against torch's OCP float8 types, with SATFINITE
+    (finite values beyond the largest code clamped to it before torch's cast,
+    inf and NaN passed as they are — HIP's amd_hip_fp8.h definition, which
+    RCCL's fp8 functors use)."""
     torch = pytest.importorskip("torch")
     tdt = torch.float8_e4m3fn if dtype == 10 else torch.float8_e5m2
     dec = oracle.e4m3_to_f32 if dtype == 10 else oracle.e5m2_to_f32
@@ -156,8 +159,10 @@ def test_fp8_codec_matches_torch(oracle, dtype):
     f = np.concatenate([rng.uniform(-1.2 * mx, 1.2 * mx, 20000).astype(np.float32),
                         (rng.standard_normal(20000) * 10 ** rng.uniform(-9, 0, 20000)).astype(np.float32),
                         ref[m], (ref[m][:-1] + np.diff(ref[m]) / 2).astype(np.float32)])
+    f = np.concatenate([f, np.float32([mx * 1.01, -mx * 1.5, 1e30, -3e38, np.inf, -np.inf, np.nan])])
     got = np.array([enc(float(x)) for x in f], dtype=np.uint8)
-    tref = torch.from_numpy(f).to(tdt).view(torch.uint8).numpy()
+    sat = np.where(np.isfinite(f), np.clip(f, -mx, mx), f).astype(np.float32)
+    tref = torch.from_numpy(sat).to(tdt).view(torch.uint8).numpy()
     gnan = np.isnan(np.array([dec(int(c)) for c in got]))
     rnan = np.isnan(torch.from_numpy(tref).view(tdt).to(torch.float32).numpy())
     assert np.array_equal(gnan, rnan)

@@ -99,3 +99,121 @@ def _rccl_f64_tail(r):
     elements are excused here."""
     return (r["dtype"] == "torch.float64" and r["n"] % 64 and r["mismatch_lo"] is not None
             and r["mismatch_lo"] >= r["n"] - r["n"] % 64 and r["untouched_by_rccl"] == r["mismatches"])
+
+
+CHILD_ALL = r"""
+import ctypes, json, os, sys
+sys.path.insert(0, sys.argv[1])
+import torch
+torch.cuda.set_device(0)
+rccl = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"), mode=ctypes.RTLD_LOCAL)
+rccl.ncclCommInitAll.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+rccl.ncclRedOpCreatePreMulSum.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+rccl.ncclRedOpDestroy.argtypes = [ctypes.c_int, ctypes.c_void_p]
+rccl.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_void_p]
+rccl.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+from tests.conftest import load_package
+nbx = load_package()
+nbx.load_library()
+rc_comm = ctypes.c_void_p()
+dev = (ctypes.c_int * 1)(0)
+assert rccl.ncclCommInitAll(ctypes.byref(rc_comm), 1, dev) == 0
+comm = nbx.Communicator.init_all([0])[0]
+st = torch.cuda.current_stream().cuda_stream
+N = 1 << 16
+g = torch.Generator(device="cuda").manual_seed(5)
+def bits(nbytes):
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g, device="cuda")
+out = []
+# (ncclDataType_t, torch dtype of the element, scalars)
+INTS = [(0, torch.int8, (3, -2, 127)), (1, torch.uint8, (3, 255, 16)), (2, torch.int32, (3, -7, 65537)),
+        (3, torch.uint32, (3, 4294967295, 65537)), (4, torch.int64, (3, -7, 4294967297)),
+        (5, torch.uint64, (3, 2**64 - 1, 4294967297))]
+FLOATS = [(6, torch.float16), (9, torch.bfloat16), (7, torch.float32), (8, torch.float64)]
+F8 = [(10, torch.float8_e4m3fn), (11, torch.float8_e5m2)]
+FACTORS = (0.1, -2.5, 1.0 / 3.0, 1e-3, 3.0, 0.125)
+cases = []
+for code, dt, scal in INTS:
+    es = torch.empty(0, dtype=dt).element_size()
+    x = bits(N * es).view(dt)
+    for v in scal:
+        sc = torch.tensor([v if v < 2**63 else v - 2**64], dtype=torch.int64).to(dt) if dt == torch.uint64 else \
+             torch.tensor([v], dtype=torch.int64).to(dt)
+        cases.append((code, dt, x, sc, v))
+for code, dt in FLOATS:
+    fi = torch.finfo(dt)
+    sp = torch.tensor([float("inf"), -float("inf"), float("nan"), 0.0, -0.0, fi.tiny, -fi.tiny, fi.tiny / 4,
+                       fi.max, -fi.max, fi.eps, 1.0, -1.0, 2.0 ** -20], dtype=torch.float64, device="cuda").to(dt)
+    x = torch.cat([sp, (torch.randn(N - sp.numel(), generator=g, device="cuda", dtype=torch.float64) * 3).to(dt)])
+    for f in FACTORS:
+        cases.append((code, dt, x, torch.tensor([f], dtype=torch.float64).to(dt), f))
+for code, dt in F8:
+    x = torch.cat([torch.arange(256, dtype=torch.uint8, device="cuda"), bits(N - 256)]).view(dt)
+    for f in FACTORS + (448.0, 2.0 ** -6):
+        cases.append((code, dt, x, torch.tensor([f], dtype=torch.float32).to(dt), f))
+for code, dt, x, sc, label in cases:
+    y = torch.empty_like(x)
+    z = torch.empty_like(x)
+    yv = y.view(torch.uint8); yv.fill_(0x5a)
+    zv = z.view(torch.uint8); zv.fill_(0xa5)
+    sc = sc.contiguous()
+    op = ctypes.c_int()
+    r1 = rccl.ncclRedOpCreatePreMulSum(ctypes.byref(op), ctypes.c_void_p(sc.data_ptr()), code, 1, rc_comm)
+    if r1 != 0:
+        out.append({"type": code, "scalar": label, "rccl_error": r1})
+        continue
+    r2 = rccl.ncclAllReduce(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), N, code, op.value, rc_comm,
+                            ctypes.c_void_p(st))
+    torch.cuda.synchronize()
+    rccl.ncclRedOpDestroy(op.value, rc_comm)
+    ours = comm.redop_create_premulsum(sc.data_ptr(), code)
+    comm.all_reduce(x.data_ptr(), z.data_ptr(), N, code, ours, st)
+    torch.cuda.synchronize()
+    comm.redop_destroy(ours)
+    es = x.element_size()
+    iy = y.view(torch.uint8).view(-1, es)
+    iz = z.view(torch.uint8).view(-1, es)
+    neq = (iy != iz).any(dim=1)
+    if dt.is_floating_point:
+        both_nan = torch.isnan(y.float() if es == 1 else y) & torch.isnan(z.float() if es == 1 else z)
+        neq &= ~both_nan
+    d = neq.nonzero().flatten()
+    def hx(t, i):
+        return t.view(torch.uint8).view(-1, es)[i].flip(0).cpu().numpy().tobytes().hex()
+    out.append({"type": code, "scalar": label, "rc": r2, "n": N, "mismatches": int(d.numel()),
+                "first": [[hx(x, i), hx(y, i), hx(z, i)] for i in d[:4].tolist()]})
+comm.destroy()
+rccl.ncclCommDestroy(rc_comm)
+print("RESULT " + json.dumps(out), flush=True)
+"""
+
+
+def _librccl():
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "librccl.so")
+    return p if os.path.exists(p) else None
+
+
+@pytest.mark.gpu
+def test_premulsum_every_type_matches_rccl_direct():
+    """The same one-rank PreMulSum corroboration for every type RCCL 2.26
+    takes, through librccl's own C API (ctypes; torch's dispatch stops at
+    fp16 / fp32 / fp64): integers (wrapping products, full-range random bits),
+    bf16 and fp16 / fp32 / fp64 with specials, and fp8 e4m3 / e5m2 over every
+    code — where RCCL is the only other implementation at hand (this build's
+    fp8 is "parity unpinned" against the reference, which has none). Aligned
+    count (RCCL's fp64 ragged tail is the other test's subject). Bit for bit,
+    NaN payloads aside."""
+    if _librccl() is None:
+        pytest.skip("torch ships no librccl.so")
+    p = subprocess.run([sys.executable, "-c", CHILD_ALL, ROOT], capture_output=True, text=True, timeout=280, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert line, p.stdout[-2000:] + p.stderr[-2000:]
+    res = json.loads(line[-1][len("RESULT "):])
+    print(json.dumps(res))
+    assert len(res) == 6 * 3 + 4 * 6 + 2 * 8
+    bad = [r for r in res if r.get("rccl_error") or r.get("rc") or r.get("mismatches")]
+    assert not bad, bad[:6]
