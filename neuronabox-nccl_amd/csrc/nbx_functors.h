@@ -18,7 +18,8 @@
 //          narrow (RNE). Saturation is HIP's __HIP_SATFINITE (amd_hip_fp8.h),
 //          what RCCL's fp8 functors narrow with: a finite result beyond the
 //          largest finite code becomes that code with its sign; inf and NaN
-//          go through (e5m2 inf; e4m3fn, which has none, NaN). The converter
+//          go through (e5m2 inf; e4m3fn, which has none, NaN) — two
+//          instructions per element (satFinite). The converter
 //          alone was checked equal to f32ToSmall on all 2^32 fp32 inputs
 //          (scripts/probe_fp8_cvt.hip, profiles/r1/probe_fp8_cvt.txt), the
 //          saturated form to f32ToSmallSat (scripts/probe_fp8_sat.hip,
@@ -118,16 +119,20 @@ __device__ __forceinline__ uint32_t f32ToSmallSat(float x) {
   return f32ToSmall<E, M, FN>(x);
 }
 
-// SATFINITE before the converter. e4m3fn: clamp, then x * 0 + clamped puts
-// NaN back for a NaN or infinite x (inf * 0 = NaN: e4m3fn narrows inf to NaN
-// anyway) and is exact otherwise — two instructions. e5m2 keeps infinities,
-// so the clamp is selected by a finiteness test instead.
-__device__ __forceinline__ float satE4M3(float x) {
-  return __builtin_fmaf(x, 0.0f, __builtin_amdgcn_fmed3f(x, 448.0f, -448.0f));
+// SATFINITE before the converter, two instructions for either format: an
+// fmed3 clamp to +-max, then fma(x, 2^-149, clamp). For a finite x the
+// added x * 2^-149 is below half an ulp of the clamp (|x| < 2^128), so the
+// fma returns the clamp exactly; for +-inf it returns +-inf (the clamp has
+// x's sign) and for NaN NaN — the converter then narrows those as HIP's
+// SATFINITE does (e5m2 inf, e4m3fn NaN). Needs f32 denormals kept (2^-149 is
+// one), as every kernel here is built (.amdhsa_float_denorm_mode_32 3).
+// Exhaustively equal to f32ToSmallSat (scripts/probe_fp8_sat.hip).
+template <int MAXV>
+__device__ __forceinline__ float satFinite(float x) {
+  return __builtin_fmaf(x, 0x1p-149f, __builtin_amdgcn_fmed3f(x, (float)MAXV, -(float)MAXV));
 }
-__device__ __forceinline__ float satE5M2(float x) {
-  return __builtin_isfinite(x) ? __builtin_amdgcn_fmed3f(x, 57344.0f, -57344.0f) : x;
-}
+__device__ __forceinline__ float satE4M3(float x) { return satFinite<448>(x); }
+__device__ __forceinline__ float satE5M2(float x) { return satFinite<57344>(x); }
 
 struct TyE4M3 {
   using Elt = uint8_t; using C = float;
