@@ -28,7 +28,7 @@ CASES = {   # name: (ncclDataType_t, ncclRedOp_t, element size, MiB per input)
     "i8avg": (0, 4, 1, 256), "u32avg": (3, 4, 4, 256), "i64avg": (4, 4, 8, 128),
     "f16max": (6, 2, 2, 256), "bf16max": (9, 2, 2, 256), "f64sum": (8, 0, 8, 256), "f64max": (8, 2, 8, 256),
     "f16prod": (6, 1, 2, 256), "f32prod": (7, 1, 4, 256), "bf16avg": (9, 4, 2, 256), "f32avg": (7, 4, 4, 256),
-    "fp8max": (10, 2, 1, 128), "fp8e5min": (11, 3, 1, 128),
+    "fp8max": (10, 2, 1, 128), "fp8e5min": (11, 3, 1, 128), "fp8prod": (10, 1, 1, 128), "fp8avg": (10, 4, 1, 128),
 }
 
 
