@@ -673,6 +673,11 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0, 
     out["transport_allreduce"] = agg("transport_allreduce_ms", 2 * (world - 1) / world, S)
     add_hbm_rates(out, world, S)
     add_fabric_rates(out, allres, world, S)
+    # the Simple transport's knobs on the same 1 GiB AllReduce (max over ranks)
+    kn = [r.get("simple_knobs_ms") for r in allres]
+    if all(isinstance(k, dict) for k in kn) and kn:
+        out["simple_knobs"] = {name: round(max(k.get(name, 0.0) for k in kn), 4) for name in kn[0]}
+        out["simple_knobs"]["default"] = (out.get("allreduce_direct") or {}).get("ms")
     # LL128 forced across the fabric (NCCL_PROTO=LL128): every call checked
     fc = [r.get("ll128_forced_checked_calls") for r in allres]
     fm = [r.get("ll128_forced_mismatched_calls") for r in allres]

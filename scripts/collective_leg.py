@@ -10,9 +10,10 @@ the bench's own line down. It is spawned before the parent touches the GPU and
 talks over stdin/stdout:
 
   parent -> child   "ID\\n"               (rank 0 only)
-  child  -> parent  "ID <hex> x6\\n"      ncclUniqueIds: direct, ring, and the LL / LL128 /
-                                         LL128-one-shot / Simple comms of the protocol sweep
-  parent -> child   "RUN <hex> x6\\n"     (every rank, after the parent's broadcast)
+  child  -> parent  "ID <hex> x9\\n"      ncclUniqueIds: direct, ring, the LL / LL128 /
+                                         LL128-one-shot / Simple comms of the protocol
+                                         sweep, and the three Simple-knob comms
+  parent -> child   "RUN <hex> x9\\n"     (every rank, after the parent's broadcast)
   child  -> parent  "PARTIAL <json>\\n"    (after every stage: the results so far; the
                                          parent reports the last one if the leg runs out
                                          of its time budget)
@@ -155,6 +156,46 @@ def protocol_sweep(ids, rank, world, st, shared_gpu, res):
             res["ok"] = False
             res["errors"].append(f"sweep {name}: async error")
         c.destroy()
+
+
+# the Simple transport's init-time knobs against the default (64 KiB slices,
+# 128 workgroups, 2 slots), on config D's 1 GiB direct AllReduce: what
+# scripts/set_thresholds.py reads to pick the xGMI defaults from a node run
+SIMPLE_KNOBS = (("slice256K", {"NBX_SIMPLE_SLICE_BYTES": str(256 << 10)}),
+                ("grid64", {"NBX_SIMPLE_MAX_GRID": "64"}),
+                ("slots4", {"NBX_SIMPLE_SLOTS": "4"}))
+
+
+def simple_knob_sweep(ids, rank, world, st, x, y, exp, res):
+    """1 GiB AllReduce ms per Simple knob setting (one communicator each, the
+    knob set at creation; every rank sets the same), each output checked."""
+    import torch
+    from __graft_entry__ import _load_package
+    nbx = _load_package()
+    out = {}
+    for (name, env), uid in zip(SIMPLE_KNOBS, ids):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            c = nbx.Communicator.init_rank(world, nbx.ncclUniqueId.from_buffer_copy(bytes.fromhex(uid)), rank)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        y.zero_()
+        c.all_reduce(x.data_ptr(), y.data_ptr(), COUNT, 7, 0, st)
+        torch.cuda.synchronize()
+        if not torch.equal(y, exp):
+            res["ok"] = False
+            res["errors"].append(f"simple knob {name}: {int((y != exp).sum().item())} elements differ")
+        out[name] = _time_calls(lambda: c.all_reduce(x.data_ptr(), y.data_ptr(), COUNT, 7, 0, st), ITERS)
+        if c.async_error() != 0:
+            res["ok"] = False
+            res["errors"].append(f"simple knob {name}: async error")
+        c.destroy()
+    res["simple_knobs_ms"] = out
 
 
 LL128_STRESS_CALLS = 1000   # per size: one-shot and (n > 2) two-shot -> >= 2000 calls
@@ -300,6 +341,8 @@ def run(ids, rank, world, dev):
     res["transport_allreduce_ms"] = _time_calls(xport, ITERS)
     link_probe(lib, comm, st, res)
     _progress("config D timed", res)
+    simple_knob_sweep(ids[6:6 + len(SIMPLE_KNOBS)], rank, world, st, x, y, exp, res)
+    _progress("Simple knobs timed", res)
 
     # Simple path with inputs that change every call (direct and ring schedules,
     # 32 MiB): catches any stale peer data a cache could serve across calls
@@ -437,6 +480,10 @@ def config_e(comm, rank, world, st, res):
             res["errors"].append(f"{name}: output differs from the bit-exact restatement")
 
 
+# direct, ring, the protocol sweep's four, the Simple knobs'
+N_IDS = 6 + len(SIMPLE_KNOBS)
+
+
 def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -451,10 +498,10 @@ def main():
             continue
         if parts[0] == "ID":
             nbx = _pkg()   # imports torch first (one HIP runtime); no GPU use: the root is a host thread
-            _emit("ID " + " ".join(bytes(nbx.get_unique_id()).hex() for _ in range(6)))
+            _emit("ID " + " ".join(bytes(nbx.get_unique_id()).hex() for _ in range(N_IDS)))
         elif parts[0] == "RUN":
             try:
-                res = run(parts[1:7], rank, world, dev)
+                res = run(parts[1:1 + N_IDS], rank, world, dev)
             except Exception as e:   # reported to the parent, never raised past it
                 res = {"rank": rank, "ok": False, "errors": [f"{type(e).__name__}: {e}"]}
             _emit("RESULT " + json.dumps(res))

@@ -30,13 +30,22 @@ creation, comm_mp_init.cc):
   NBX_LL128_ACROSS_GPUS    "1" only when the run spanned GPUs, its forced-LL128
                            stress checked >= 2000 calls with no mismatch, and
                            LL128 carries some size (DESIGN §6's flip rule)
+  NBX_SIMPLE_SLICE_BYTES / NBX_SIMPLE_MAX_GRID / NBX_SIMPLE_SLOTS
+                           from `collective.simple_knobs` (1 GiB AllReduce ms
+                           per Simple knob setting, collective_leg.py
+                           SIMPLE_KNOBS): the fastest setting when it beats the
+                           default by more than the margin, else unset
 Usage: python scripts/set_thresholds.py BENCH.json [--margin 0.05] [--json]
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from collective_leg import SIMPLE_KNOBS  # noqa: E402  (no GPU or torch import at module level)
 
 LADDER = ("LL", "LL128", "Simple")
 
@@ -131,6 +140,18 @@ def thresholds(bench: dict, margin: float = 0.05) -> dict:
     env["NBX_LL128_ACROSS_GPUS"] = "1" if (multi and clean and env["NBX_LL128_MAX_BYTES"] > 0) else ""
     why.append(f"LL128 across GPUs: forced stress {forced.get('checked_calls')} calls, "
                f"{forced.get('mismatched_calls')} mismatched -> {'enable' if env['NBX_LL128_ACROSS_GPUS'] else 'keep off'}")
+    kn = coll.get("simple_knobs") or {}
+    knob_env = dict(SIMPLE_KNOBS)
+    for var in sorted({v for e in knob_env.values() for v in e}):
+        env[var] = ""
+    base = kn.get("default")
+    timed = {k: v for k, v in kn.items() if k in knob_env and v}
+    if base and timed:
+        best = min(timed, key=timed.get)
+        if base > timed[best] * (1 + margin):
+            env.update(knob_env[best])
+        why.append(f"Simple knobs, 1 GiB AllReduce: default {base} ms, {timed} -> "
+                   f"{best if base > timed[best] * (1 + margin) else 'default'}")
     vr = coll.get("vs_rccl") or {}
     if vr.get("sweep_best_protocol"):
         why.append(f"best protocol / RCCL per size: {vr['sweep_best_protocol']}")

@@ -35,6 +35,7 @@ for line in sys.stdin:
         print("RESULT " + json.dumps({"rank": rank, "ok": True, "errors": [], "allreduce_direct_ms": 10.0 + rank,
                                       "transport_allreduce_ms": 6.0, "reduce_scatter_ms": 5.0,
                                       "link_push_ms": 4.0 + rank, "link_pull_ms": 2.0, "link_bytes_per_peer": 1 << 28,
+                                      "simple_knobs_ms": {"slice256K": 9.0 + rank, "grid64": 12.0, "slots4": 10.0},
                                       "ipc_repairs": {"direct": rank, "ring": 0},
                                       "ll128_forced_checked_calls": 2000, "ll128_forced_mismatched_calls": 0}),
               flush=True)
@@ -184,5 +185,6 @@ def test_legs_finish_normally_inside_the_budget(tmp_path):
     assert abs(ard["fabric_frac"] - round(floor / 11.0, 3)) < 1e-9
     rs = coll["reduce_scatter"]
     assert rs["fabric_link_bytes"] == M // n
+    assert coll["simple_knobs"] == {"slice256K": 10.0, "grid64": 12.0, "slots4": 10.0, "default": 11.0}
     fa = coll["clique"]["fold_allreduce"]
     assert abs(fa["fabric_floor_ms"] - round(max(M // n / (pull * 1e9), M // n / (push * 1e9)) * 1e3, 4)) < 1e-9

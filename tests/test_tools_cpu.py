@@ -115,6 +115,13 @@ def test_set_thresholds_synthetic_8_ranks_with_hysteresis():
     assert env["NBX_LL128_ACROSS_GPUS"] == "1"
     b["collective"]["ll128_forced"]["mismatched_calls"] = 1   # one torn line anywhere: keep it off
     assert st.thresholds(b)["env"]["NBX_LL128_ACROSS_GPUS"] == ""
+    # Simple knobs: no sweep -> every knob unset; a 3 % win keeps the default; a 20 % win sets it
+    assert env["NBX_SIMPLE_SLICE_BYTES"] == "" and env["NBX_SIMPLE_MAX_GRID"] == "" and env["NBX_SIMPLE_SLOTS"] == ""
+    b["collective"]["simple_knobs"] = {"slice256K": 9.7, "grid64": 11.0, "slots4": 10.5, "default": 10.0}
+    assert st.thresholds(b)["env"]["NBX_SIMPLE_SLICE_BYTES"] == ""
+    b["collective"]["simple_knobs"]["grid64"] = 8.0
+    e2 = st.thresholds(b)["env"]
+    assert e2["NBX_SIMPLE_MAX_GRID"] == "64" and e2["NBX_SIMPLE_SLICE_BYTES"] == "" and e2["NBX_SIMPLE_SLOTS"] == ""
 
 
 def test_set_thresholds_cli(tmp_path):
