@@ -673,6 +673,11 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0, 
     out["transport_allreduce"] = agg("transport_allreduce_ms", 2 * (world - 1) / world, S)
     add_hbm_rates(out, world, S)
     add_fabric_rates(out, allres, world, S)
+    cv = [r.get("curve_allreduce_ms") for r in allres]
+    if cv and all(isinstance(c, list) and len(c) == len(CURVE_BYTES) for c in cv):
+        out["allreduce_curve"] = {"bytes": list(CURVE_BYTES), "ms": [round(max(col), 4) for col in zip(*cv)],
+                                  "busbw_GBs": [round(b / (max(col) * 1e-3) / 1e9 * 2 * (world - 1) / world, 2)
+                                                for b, col in zip(CURVE_BYTES, zip(*cv))]}
     # the Simple transport's knobs on the same 1 GiB AllReduce (max over ranks)
     kn = [r.get("simple_knobs_ms") for r in allres]
     if all(isinstance(k, dict) for k in kn) and kn:
@@ -836,6 +841,9 @@ def vs_rccl(coll, rccl):
             j = SWEEP_BYTES.index(b) if b in SWEEP_BYTES else None
             best.append(None if not cands or j is None else round(min(cands) / rsw[j], 3))
         out["sweep_best_protocol"] = best
+    cu, rcu = coll.get("allreduce_curve") or {}, rccl.get("curve_allreduce_ms")
+    if cu.get("ms") and rcu and len(rcu) == len(cu["ms"]):
+        out["allreduce_curve"] = [ratio(a, b) for a, b in zip(cu["ms"], rcu)]
     out["what"] = "libnbxccl time / RCCL time (< 1: libnbxccl faster)"
     return out
 
@@ -884,6 +892,12 @@ def rccl_leg(world: int):
         for name, cnt in (("allreduce_1MiB_us", 256 << 10), ("allreduce_4KiB_us", 1024)):
             z = torch.ones(cnt, device="cuda")
             out[name] = round(timed(lambda: dist.all_reduce(z), 100) * 1e6, 2)
+        curve = []
+        for b in CURVE_BYTES:
+            z = x[:b // 4]
+            curve.append(round(timed(lambda: dist.all_reduce(z), 5) * 1e3, 4))
+        out["curve_bytes"] = list(CURVE_BYTES)
+        out["curve_allreduce_ms"] = curve
         sweep = []
         for b in SWEEP_BYTES:
             z = torch.ones(b // 4, device="cuda")
@@ -899,6 +913,7 @@ def rccl_leg(world: int):
 
 COUNT_D = 256 << 20   # config D: fp32 elements per rank (1 GiB)
 SWEEP_BYTES = [4 << 10, 32 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]   # = collective_leg.SWEEP_BYTES
+CURVE_BYTES = (64 << 20, 256 << 20)   # = collective_leg.CURVE_BYTES: AllReduce between the sweep and config D
 
 
 def parse_args(argv=None):

@@ -198,6 +198,8 @@ def simple_knob_sweep(ids, rank, world, st, x, y, exp, res):
     res["simple_knobs_ms"] = out
 
 
+CURVE_BYTES = (64 << 20, 256 << 20)   # = bench.CURVE_BYTES
+
 LL128_STRESS_CALLS = 1000   # per size: one-shot and (n > 2) two-shot -> >= 2000 calls
 
 
@@ -343,6 +345,18 @@ def run(ids, rank, world, dev):
     _progress("config D timed", res)
     simple_knob_sweep(ids[6:6 + len(SIMPLE_KNOBS)], rank, world, st, x, y, exp, res)
     _progress("Simple knobs timed", res)
+    # the large-message curve between the sweep (<= 16 MiB) and config D
+    # (1 GiB) on the default communicator, each size checked once
+    curve = []
+    for b in CURVE_BYTES:
+        n = b // 4
+        y.zero_()
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), n, F32, SUM, st)
+        torch.cuda.synchronize()
+        check(f"allreduce_{b >> 20}MiB", y[:n], exp[:n])
+        curve.append(_time_calls(lambda: comm.all_reduce(x.data_ptr(), y.data_ptr(), n, F32, SUM, st), ITERS))
+    res["curve_bytes"] = list(CURVE_BYTES)
+    res["curve_allreduce_ms"] = curve
 
     # Simple path with inputs that change every call (direct and ring schedules,
     # 32 MiB): catches any stale peer data a cache could serve across calls

@@ -36,6 +36,7 @@ for line in sys.stdin:
                                       "transport_allreduce_ms": 6.0, "reduce_scatter_ms": 5.0,
                                       "link_push_ms": 4.0 + rank, "link_pull_ms": 2.0, "link_bytes_per_peer": 1 << 28,
                                       "simple_knobs_ms": {"slice256K": 9.0 + rank, "grid64": 12.0, "slots4": 10.0},
+                                      "curve_allreduce_ms": [1.0 + rank, 3.0],
                                       "ipc_repairs": {"direct": rank, "ring": 0},
                                       "ll128_forced_checked_calls": 2000, "ll128_forced_mismatched_calls": 0}),
               flush=True)
@@ -186,5 +187,21 @@ def test_legs_finish_normally_inside_the_budget(tmp_path):
     rs = coll["reduce_scatter"]
     assert rs["fabric_link_bytes"] == M // n
     assert coll["simple_knobs"] == {"slice256K": 10.0, "grid64": 12.0, "slots4": 10.0, "default": 11.0}
+    cu = coll["allreduce_curve"]
+    assert cu["bytes"] == [64 << 20, 256 << 20] and cu["ms"] == [2.0, 3.0]
+    assert abs(cu["busbw_GBs"][1] - round((256 << 20) / 3e-3 / 1e9, 2)) < 1e-9   # n = 2: busbw = algbw
     fa = coll["clique"]["fold_allreduce"]
     assert abs(fa["fabric_floor_ms"] - round(max(M // n / (pull * 1e9), M // n / (push * 1e9)) * 1e3, 4)) < 1e-9
+
+
+def test_vs_rccl_ratios_include_the_curve():
+    coll = {"allreduce_direct": {"ms": 10.0}, "reduce_scatter": {"ms": 6.0}, "ll128_allreduce_1MiB_us": 20.0,
+            "ll_allreduce_4KiB_us": 8.0, "allreduce_curve": {"bytes": [64 << 20, 256 << 20], "ms": [1.0, 3.0]},
+            "protocol_sweep": {"bytes": bench.SWEEP_BYTES[:2], "LL": [5.0, 7.0], "Simple": [9.0, 6.0]}}
+    rccl = {"ok": True, "allreduce": {"ms": 8.0}, "reduce_scatter": {"ms": 6.0}, "allreduce_1MiB_us": 25.0,
+            "allreduce_4KiB_us": 10.0, "curve_allreduce_ms": [2.0, 3.0], "sweep_allreduce_us": [10.0, 6.0]}
+    v = bench.vs_rccl(coll, rccl)
+    assert v["allreduce_1GiB"] == 1.25 and v["reduce_scatter_1GiB"] == 1.0
+    assert v["allreduce_curve"] == [0.5, 1.0]
+    assert v["sweep_best_protocol"] == [0.5, 1.0]
+    assert bench.vs_rccl(coll, {"ok": False}) is None
