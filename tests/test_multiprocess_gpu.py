@@ -1345,6 +1345,59 @@ def test_multiprocess_link_probe(nbx, monkeypatch, n):
         assert o["exact"], r
 
 
+def _child_past_32_bits(uid_bytes, rank, n, q):
+    """Counts past 2^32 through the multi-process communicator (size_t counts,
+    nccl.h.in:315 / :331): a u8 sum AllReduce of 2^32 + 37 elements and a u8
+    ReduceScatter whose send buffer holds n x (2^31 + 3) elements, on the
+    Simple protocol, checked whole (uint8 adds wrap, as the reference's)."""
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+
+        def pattern(r, count):
+            base = ((torch.arange(1 << 20, dtype=torch.int32, device="cuda") * 7 + 13 * r + 1) % 251).to(torch.uint8)
+            return base.repeat(count // base.numel() + 1)[:count].contiguous()
+        out = {}
+        count = (1 << 32) + 37
+        x = pattern(rank, count)
+        y = torch.empty_like(x)
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), count, 1, 0, st)   # ncclUint8, ncclSum
+        torch.cuda.synchronize()
+        want = pattern(0, count)
+        for r in range(1, n):
+            want += pattern(r, count)
+        out["allreduce"] = bool(torch.equal(y, want))
+        del x, y, want
+        torch.cuda.empty_cache()
+        rc = (1 << 31) + 3
+        x = pattern(rank, rc * n)
+        y = torch.empty(rc, dtype=torch.uint8, device="cuda")
+        comm.reduce_scatter(x.data_ptr(), y.data_ptr(), rc, 1, 0, st)
+        torch.cuda.synchronize()
+        want = pattern(0, rc * n)[rank * rc:(rank + 1) * rc].clone()
+        for r in range(1, n):
+            want += pattern(r, rc * n)[rank * rc:(rank + 1) * rc]
+        out["reduce_scatter"] = bool(torch.equal(y, want))
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_counts_past_32_bits(nbx, monkeypatch):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    res = _run_ranks(nbx, 2, _child_past_32_bits)
+    for r in range(2):
+        assert res[r] == {"allreduce": True, "reduce_scatter": True}, (r, res[r])
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;

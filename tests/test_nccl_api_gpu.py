@@ -161,6 +161,47 @@ def test_clique_allreduce_shared_device(nbx, oracle, torch_gpu, nranks, dtype, o
             c.destroy()
 
 
+def test_clique_counts_past_32_bits(nbx, torch_gpu):
+    """Counts past 2^32 through ncclCommInitAll (2 ranks on the one GPU: the
+    event-ordered direct fold): u8 sum AllReduce of 2^32 + 37 elements and a
+    ReduceScatter of recvcount 2^31 + 3, checked whole (u8 adds wrap)."""
+    torch = torch_gpu
+    comms = nbx.Communicator.init_all([0, 0])
+
+    def pattern(r, count):
+        base = ((torch.arange(1 << 20, dtype=torch.int32, device="cuda") * 5 + 29 * r + 3) % 253).to(torch.uint8)
+        return base.repeat(count // base.numel() + 1)[:count].contiguous()
+    try:
+        count = (1 << 32) + 37
+        xs = [pattern(r, count) for r in range(2)]
+        ys = [torch.empty_like(x) for x in xs]
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        torch.cuda.synchronize()
+        nbx.group_start()
+        for r in range(2):
+            comms[r].all_reduce(xs[r].data_ptr(), ys[r].data_ptr(), count, 1, 0, streams[r].cuda_stream)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        want = xs[0] + xs[1]
+        assert torch.equal(ys[0], want) and torch.equal(ys[1], want)
+        del xs, ys, want
+        torch.cuda.empty_cache()
+        rc = (1 << 31) + 3
+        xs = [pattern(r, 2 * rc) for r in range(2)]
+        ys = [torch.empty(rc, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        torch.cuda.synchronize()
+        nbx.group_start()
+        for r in range(2):
+            comms[r].reduce_scatter(xs[r].data_ptr(), ys[r].data_ptr(), rc, 1, 0, streams[r].cuda_stream)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        for r in range(2):
+            assert torch.equal(ys[r], xs[0][r * rc:(r + 1) * rc] + xs[1][r * rc:(r + 1) * rc]), r
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_clique_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, nranks):
     torch = torch_gpu
