@@ -1398,6 +1398,70 @@ def test_multiprocess_counts_past_32_bits(nbx, monkeypatch):
         assert res[r] == {"allreduce": True, "reduce_scatter": True}, (r, res[r])
 
 
+def _child_in_place(uid_bytes, rank, n, q):
+    """In-place calls as the reference defines them (nccl.h.in:315-331):
+    AllReduce with sendbuff == recvbuff, ReduceScatter with recvbuff ==
+    sendbuff + rank * recvcount, Reduce with recvbuff == sendbuff on the root —
+    at LL, LL128 (one- and two-shot) and Simple sizes, each compared bit for
+    bit with the same call out of place (itself checked against the oracle by
+    the suites above)."""
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        g = torch.Generator(device="cuda").manual_seed(77 + rank)
+        out = []
+        for count in (1000, 100003, 2 * 1024 * 1024 + 5):   # LL, LL128 (two-shot above 256 KiB at n > 2), Simple
+            for kind in ("allreduce", "reducescatter", "reduce"):
+                total = count * n if kind == "reducescatter" else count
+                x = torch.randn(total, generator=g, device="cuda")
+                ref = torch.full((count,), -7.0, device="cuda")
+                ip = x.clone()
+                torch.cuda.synchronize()
+                root = (n - 1) if kind == "reduce" else 0
+                if kind == "allreduce":
+                    comm.all_reduce(x.data_ptr(), ref.data_ptr(), count, 7, 0, st)
+                    comm.all_reduce(ip.data_ptr(), ip.data_ptr(), count, 7, 0, st)
+                    got = ip
+                elif kind == "reducescatter":
+                    comm.reduce_scatter(x.data_ptr(), ref.data_ptr(), count, 7, 0, st)
+                    comm.reduce_scatter(ip.data_ptr(), ip[rank * count:].data_ptr(), count, 7, 0, st)
+                    got = ip[rank * count:(rank + 1) * count]
+                else:
+                    comm.reduce(x.data_ptr(), ref.data_ptr() if rank == root else 0, count, 7, 0, root, st)
+                    comm.reduce(ip.data_ptr(), ip.data_ptr() if rank == root else 0, count, 7, 0, root, st)
+                    got = ip if rank == root else None
+                torch.cuda.synchronize()
+                same = True if got is None else bool(torch.equal(got, ref))
+                untouched = True
+                if kind == "reducescatter":   # the other blocks of the send buffer stay as they were
+                    untouched = bool(torch.equal(ip[:rank * count], x[:rank * count]) and
+                                     torch.equal(ip[(rank + 1) * count:], x[(rank + 1) * count:]))
+                elif kind == "reduce" and rank != root:
+                    untouched = bool(torch.equal(ip, x))
+                out.append((count, kind, same, untouched))
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n,algo", [(2, ""), (3, ""), (3, "Ring"), (4, "")])
+def test_multiprocess_in_place(nbx, monkeypatch, n, algo):
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NCCL_ALGO", algo)
+    res = _run_ranks(nbx, n, _child_in_place)
+    for r in range(n):
+        bad = [c for c in res[r] if not (c[2] and c[3])]
+        assert not bad and len(res[r]) == 9, (r, bad)
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;
