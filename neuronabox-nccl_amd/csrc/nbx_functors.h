@@ -19,7 +19,8 @@
 //          what RCCL's fp8 functors narrow with: a finite result beyond the
 //          largest finite code becomes that code with its sign; inf and NaN
 //          go through (e5m2 inf; e4m3fn, which has none, NaN) — two
-//          instructions per element (satFinite). The converter
+//          instructions per element (satFinite), 1.5 for a converter's pair
+//          (satFinite2). The converter
 //          alone was checked equal to f32ToSmall on all 2^32 fp32 inputs
 //          (scripts/probe_fp8_cvt.hip, profiles/r1/probe_fp8_cvt.txt), the
 //          saturated form to f32ToSmallSat (scripts/probe_fp8_sat.hip,
@@ -133,6 +134,16 @@ __device__ __forceinline__ float satFinite(float x) {
 }
 __device__ __forceinline__ float satE4M3(float x) { return satFinite<448>(x); }
 __device__ __forceinline__ float satE5M2(float x) { return satFinite<57344>(x); }
+// the same for a pair about to share one converter: two clamps, one packed
+// fma (v_pk_fma_f32) — 1.5 instructions per element
+template <int MAXV>
+__device__ __forceinline__ f32x2 satFinite2(float x, float y) {
+  const f32x2 c = {__builtin_amdgcn_fmed3f(x, (float)MAXV, -(float)MAXV),
+                   __builtin_amdgcn_fmed3f(y, (float)MAXV, -(float)MAXV)};
+  const f32x2 v = {x, y};
+  const f32x2 e = {0x1p-149f, 0x1p-149f};
+  return __builtin_elementwise_fma(v, e, c);
+}
 
 struct TyE4M3 {
   using Elt = uint8_t; using C = float;
@@ -143,10 +154,9 @@ struct TyE4M3 {
   }
   // two results into bytes {0,1} (hi = false) or {2,3} (hi = true) of `old`
   __device__ static uint32_t narrow2(float x, float y, uint32_t old, bool hi) {
-    x = satE4M3(x);
-    y = satE4M3(y);
-    return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x, y, (int)old, true)
-              : (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(x, y, (int)old, false);
+    const f32x2 s = satFinite2<448>(x, y);
+    return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(s[0], s[1], (int)old, true)
+              : (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(s[0], s[1], (int)old, false);
   }
   // 4 codes in a dword <-> 4 floats
   __device__ static void wide4(uint32_t w, float (&f)[4]) {
@@ -163,8 +173,9 @@ struct TyE5M2 {
     return (Elt)(__builtin_amdgcn_cvt_pk_bf8_f32(s, s, 0, false) & 0xff);
   }
   __device__ static uint32_t narrow2(float x, float y, uint32_t old, bool hi) {
-    x = satE5M2(x);
-    y = satE5M2(y);
+    const f32x2 s = satFinite2<57344>(x, y);
+    x = s[0];
+    y = s[1];
     return hi ? (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(x, y, (int)old, true)
               : (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(x, y, (int)old, false);
   }
