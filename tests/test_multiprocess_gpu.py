@@ -1462,6 +1462,96 @@ def test_multiprocess_in_place(nbx, monkeypatch, n, algo):
         assert not bad and len(res[r]) == 9, (r, bad)
 
 
+# every type x every op through the multi-process communicator at each
+# protocol's sizes (bytes per message; LL, LL128 one-shot, LL128 two-shot at
+# n = 3, Simple), AllReduce throughout, ReduceScatter / Reduce for sum and max
+EVERY_TYPE_BYTES = (4001, 100003, 600001, (3 << 20) + 5)
+
+
+def _every_type_cases():
+    cases = []
+    for dtype in range(12):
+        for b in EVERY_TYPE_BYTES:
+            count = max(1, b // (8 if dtype in (4, 5, 8) else 4 if dtype in (2, 3, 7) else 2 if dtype in (6, 9) else 1))
+            for op in range(5):
+                cases.append(("ar", dtype, op, count))
+            if b >= 100003:
+                for op in (0, 2):
+                    cases.append(("rs", dtype, op, max(1, count // 3)))
+                    cases.append(("red", dtype, op, count))
+    return cases
+
+
+def _child_every_type(uid_bytes, rank, n, q):
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        for i, (kind, dtype, op, count) in enumerate(_every_type_cases()):
+            x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
+            tx = torch.from_numpy(x.copy()).cuda()
+            ty = torch.zeros(x.size // n if kind == "rs" else x.size, dtype=torch.uint8, device="cuda")
+            if kind == "ar":
+                comm.all_reduce(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
+            elif kind == "rs":
+                comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
+            else:
+                comm.reduce(tx.data_ptr(), ty.data_ptr(), count, dtype, op, _ll_root(i, n), st)
+            torch.cuda.synchronize()
+            out[i] = ty.cpu().numpy().copy()
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_every_type_and_op(nbx, oracle, monkeypatch):
+    """All 12 types x sum / prod / max / min / avg as AllReduce, and
+    ReduceScatter / Reduce for sum and max, through the multi-process
+    communicator at LL, LL128 one-shot, LL128 two-shot and Simple sizes
+    (3 ranks, odd byte counts), each bit-exact vs the oracle in the direct
+    schedule's fold order."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    n = 3
+    res = _run_ranks(nbx, n, _child_every_type)
+    bad = []
+    for i, (kind, dtype, op, count) in enumerate(_every_type_cases()):
+        total = count * n if kind == "rs" else count
+        xs = oracle.random_inputs(dtype, 8, total, seed=77 + dtype + count)[:n]   # = _ll_input, all ranks at once
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        st = oracle.NP_STORAGE[dtype]
+        eb = np.dtype(st).itemsize
+        kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+        exp = {}
+        if kind == "ar":
+            full = np.empty(count, dtype=st)
+            for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+                if hi > lo:
+                    order = [(c + 1 + k) % n for k in range(n)]
+                    full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg, **kw)[0]
+            exp = {r: full for r in range(n)}
+        elif kind == "rs":
+            for r in range(n):
+                order = [(r + 1 + k) % n for k in range(n)]
+                exp[r] = oracle.reduce_multi([xs[j][r * count:(r + 1) * count] for j in order], dtype, devop, arg,
+                                             **kw)[0]
+        else:
+            root = _ll_root(i, n)
+            order = [(root + 1 + k) % n for k in range(n)]
+            exp[root] = oracle.reduce_multi([xs[j] for j in order], dtype, devop, arg, **kw)[0]
+        for r, e in exp.items():
+            if not np.array_equal(res[r][i], np.ascontiguousarray(e).view(np.uint8)):
+                bad.append((kind, dtype, op, count, r))
+    assert not bad, bad[:10]
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;
