@@ -202,6 +202,59 @@ def test_clique_counts_past_32_bits(nbx, torch_gpu):
             c.destroy()
 
 
+def test_clique_every_type_and_op(nbx, oracle, torch_gpu):
+    """Every type x sum / prod / max / min / avg as a 3-rank clique AllReduce
+    (odd count, the event-ordered direct fold), and ReduceScatter / Reduce
+    for sum and max, bit-exact vs the oracle in the clique's fold orders."""
+    torch = torch_gpu
+    nranks = 3
+    comms = nbx.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    bad = []
+    try:
+        for dtype in range(12):
+            eb = np.dtype(oracle.NP_STORAGE[dtype]).itemsize
+            count = 60001 // eb + 3
+            for op in range(5):
+                kinds = ("ar", "rs", "red") if op in (0, 2) else ("ar",)
+                for kind in kinds:
+                    total = count * nranks if kind == "rs" else count
+                    xs = oracle.random_inputs(dtype, nranks, total, seed=300 + 7 * dtype + op)
+                    txs = [t_of(torch, x) for x in xs]
+                    outs = [torch.zeros(count * eb, dtype=torch.uint8, device="cuda") for _ in range(nranks)]
+                    torch.cuda.synchronize()
+                    nbx.group_start()
+                    for r in range(nranks):
+                        sp, rp, s_ = txs[r].data_ptr(), outs[r].data_ptr(), streams[r].cuda_stream
+                        if kind == "ar":
+                            comms[r].all_reduce(sp, rp, count, dtype, op, s_)
+                        elif kind == "rs":
+                            comms[r].reduce_scatter(sp, rp, count, dtype, op, s_)
+                        else:
+                            comms[r].reduce(sp, rp if r == 2 else 0, count, dtype, op, 2, s_)
+                    nbx.group_end()
+                    torch.cuda.synchronize()
+                    devop, arg = oracle.host_to_dev_redop(op, dtype, nranks)
+                    if kind == "ar":
+                        exp = _ring_order_reduce(oracle, xs, dtype, devop, arg, devop == 4, nranks,
+                                                 _blocks(count, eb, nranks))
+                        want = {r: exp for r in range(nranks)}
+                    elif kind == "rs":
+                        exp = _ring_order_reduce(oracle, xs, dtype, devop, arg, devop == 4, nranks,
+                                                 lambda b: (b * count, (b + 1) * count))
+                        want = {r: exp[r * count:(r + 1) * count] for r in range(nranks)}
+                    else:
+                        want = {2: _ring_order_reduce(oracle, xs, dtype, devop, arg, devop == 4, nranks,
+                                                      _blocks(count, eb, nranks), root=2)}
+                    for r, e in want.items():
+                        if not np.array_equal(outs[r].cpu().numpy(), np.ascontiguousarray(e).view(np.uint8)):
+                            bad.append((kind, dtype, op, r))
+    finally:
+        for c in comms:
+            c.destroy()
+    assert not bad, bad[:10]
+
+
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_clique_reduce_scatter_and_reduce(nbx, oracle, torch_gpu, nranks):
     torch = torch_gpu
