@@ -99,13 +99,14 @@ ncclResult_t cliqueOrderBefore(Clique* c, int r, hipStream_t s);
 ncclResult_t cliqueOrderAfter(Clique* c, int r, hipStream_t s);
 
 // Run one collective across every rank of an in-process clique.
-ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
+ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts0) {
   const int n = c->n;
-  const PendingColl& p0 = parts[0];
-  if (!sameCollective(parts)) {
+  if (!sameCollective(parts0)) {
     warn("collective mismatch across ranks of the clique");
     return ncclInvalidUsage;
   }
+  std::vector<PendingColl> parts = parts0;   // localPre: each rank's pre-multiplied scratch, summed
+  const PendingColl& p0 = parts[0];
   const int eb = typeSize(p0.dt);
   NBX_TRACE("clique coll kind=%d n=%d count=%zu dt=%d op=%d", (int)p0.kind, n, p0.count, (int)p0.dt, p0.op.op);
   // 1. enter: every rank's stream reaches the collective (after the previous
@@ -113,6 +114,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts) {
   for (int r = 0; r < n; r++) {
     DevGuard g(c->devs[r]);
     NCCLCHECK(cliqueOrderBefore(c, r, parts[r].stream));
+    if (parts[r].localPre) NCCLCHECK(localPreOp(c->comms[r], c->devs[r], &parts[r], n));
     HIPCHECK(hipEventRecord(c->evEnter[r], parts[r].stream));
   }
   for (int r = 0; r < n; r++) {
@@ -246,7 +248,7 @@ constexpr size_t kMaxCliqueBatch = 64;
 ncclResult_t runCliqueRounds(Clique* c, const std::vector<std::vector<PendingColl>>& rounds) {
   const int n = c->n;
   auto batchable = [&](const std::vector<PendingColl>& parts) {
-    return sameCollective(parts) && !(parts[0].kind == kAllReduce && n > NBX_MAX_DSTS);
+    return sameCollective(parts) && !(parts[0].kind == kAllReduce && n > NBX_MAX_DSTS) && !parts[0].localPre;
   };
   size_t i = 0;
   while (i < rounds.size()) {

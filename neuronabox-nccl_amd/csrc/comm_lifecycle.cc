@@ -158,6 +158,12 @@ ncclResult_t commFree(ncclComm* comm) {
   // calls still queued in this thread's open group die with the communicator
   t_groupMpComms.erase(std::remove(t_groupMpComms.begin(), t_groupMpComms.end(), comm), t_groupMpComms.end());
   mpFree(comm);
+  if (comm->preScratch || !comm->preScratchOld.empty()) {
+    DevGuard dg(comm->device);
+    (void)hipDeviceSynchronize();
+    if (comm->preScratch) (void)hipFree(comm->preScratch);
+    for (void* p : comm->preScratchOld) (void)hipFree(p);
+  }
   if (c) {
     std::lock_guard<std::mutex> gp(g_pendMu);
     std::lock_guard<std::mutex> g(c->mu);

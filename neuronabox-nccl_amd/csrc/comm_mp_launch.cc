@@ -186,9 +186,11 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc, bool tr
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring && !transport, c.stream);
 }
 
-ncclResult_t runMpColl(ncclComm* comm, const MpCall& c) {
-  if (c.count == 0) return ncclSuccess;
-  return runMpOrdered(comm, c.stream, [&]() -> ncclResult_t {
+ncclResult_t runMpColl(ncclComm* comm, const MpCall& c0) {
+  if (c0.count == 0) return ncclSuccess;
+  return runMpOrdered(comm, c0.stream, [&]() -> ncclResult_t {
+    MpCall c = c0;   // after the cross-stream wait: the pre-pass reuses scratch an earlier call read
+    if (c.localPre) NCCLCHECK(localPreOp(comm, comm->device, &c, comm->nRanks));
     const MpProto proto = mpProtoOf(comm, c);
     return proto == kMpSimple ? mpLaunchSimple(comm, &c, 1) : mpLaunchLL(comm, c, proto);
   });
@@ -249,7 +251,8 @@ thread_local std::vector<ncclComm*> t_groupMpComms;
 // non-root may even pass NULL), so a cut that looked at it would split the
 // root's run where the non-roots batch theirs — every rank runs
 // each grouped Reduce as its own launch instead, a rule every rank evaluates
-// alike. A group whose AllReduce / ReduceScatter calls alias differently on
+// alike. A user PreMulSum (localPre) runs alone too: its pre-pass fills the
+// communicator's one scratch buffer. A group whose AllReduce / ReduceScatter calls alias differently on
 // different ranks is outside what the batching supports (LL / LL128 ranks then
 // time out waiting for lines that never come; Simple ranks could fold
 // misplaced slices; NBX_CHECK_PLANS=1 makes both fail loudly, naming the peer):
@@ -285,11 +288,13 @@ ncclResult_t runMpGroup(ncclComm* comm) {
       size_t j = i + 1;
       const MpProto p = calls[i].count > 0 ? mpProtoOf(comm, calls[i]) : kMpSimple;
       const size_t maxSegs = p == kMpSimple ? (size_t)nbx::kSimpleMaxSegs : (size_t)nbx::kLLMaxSegs;
-      if (mp->groupBatch && calls[i].kind != kReduce && (p == kMpLL || p == kMpLL128 || p == kMpSimple)) {
+      if (mp->groupBatch && calls[i].kind != kReduce && !calls[i].localPre &&
+          (p == kMpLL || p == kMpLL128 || p == kMpSimple)) {
         uint64_t used = p == kMpSimple ? 0 : unitsOf(calls[i], p);
         std::vector<Span> spans, sj;
         mpCallSpans(calls[i], comm->nRanks, &spans);
-        while (j < calls.size() && j - i < maxSegs && calls[j].count > 0 && sameOp(calls[i], calls[j]) &&
+        while (j < calls.size() && j - i < maxSegs && calls[j].count > 0 && !calls[j].localPre &&
+               sameOp(calls[i], calls[j]) &&
                mpProtoOf(comm, calls[j]) == p && (p == kMpSimple || used + unitsOf(calls[j], p) <= capOf(p))) {
           sj.clear();
           mpCallSpans(calls[j], comm->nRanks, &sj);

@@ -114,6 +114,12 @@ struct ncclComm {
   // initialisation (the LL128 self-test's kernels) before it joins that thread.
   int* hostWords = nullptr;
   int* hostWordsDev = nullptr;
+  // user PreMulSum across ranks (localPreScratch): this rank's input
+  // pre-multiplied by its own scalar; superseded buffers are kept until the
+  // communicator is freed (an earlier call may still read them)
+  void* preScratch = nullptr;
+  size_t preScratchBytes = 0;
+  std::vector<void*> preScratchOld;
   ~ncclComm() {
     if (hostWords) (void)hipHostFree(hostWords);
   }
@@ -133,6 +139,12 @@ struct PendingColl {
   nbxDevRedOpFull op;
   int root;
   hipStream_t stream;
+  // a user PreMulSum (ncclRedOpCreatePreMulSum) across ranks: the scalar
+  // multiplies THIS rank's input only — the reference applies the pre-op to
+  // the local Input source alone (prims_simple.h:269-270) and exchanges the
+  // peers' own scalars for the direct paths (:617-628), so the result is
+  // sum_r s_r * x_r. Run as a pre-pass into scratch, then a Sum (localPreOp).
+  bool localPre = false;
 };
 
 // One reducing collective as enqueued on a multi-process communicator (the
@@ -298,6 +310,9 @@ ncclResult_t mpLaunchLL(ncclComm* comm, const MpCall& c, MpProto proto, const Mp
                         int nSegs = 0);
 ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc, bool transport = false);
 ncclResult_t runMpColl(ncclComm* comm, const MpCall& c);
+// localPre calls: scratch = this rank's input x its own scalar (one pre-op
+// reduce on c.stream), then *c sums the scratch (op Sum, localPre cleared)
+ncclResult_t localPreOp(ncclComm* comm, int device, PendingColl* c, int nRanks);
 ncclResult_t runMpGroup(ncclComm* comm);
 ncclResult_t flushMpGroups();
 

@@ -206,6 +206,41 @@ ncclResult_t launchOneRank(void* dst, const void* src, size_t count, const nbxDe
 }
 
 
+// localPre (PendingColl): scratch = x * s on c->stream, then the collective
+// sums the scratch. Scratch grows by doubling and is never freed while the
+// communicator lives (an earlier call, possibly on another stream, may still
+// read the old buffer); growing is refused inside a stream capture — one eager
+// call of the size first, as graph capture of NCCL calls expects anyway.
+ncclResult_t localPreOp(ncclComm* comm, int device, PendingColl* c, int nRanks) {
+  const size_t eb = (size_t)typeSize(c->dt);
+  const size_t elts = c->kind == kReduceScatter ? c->count * (size_t)nRanks : c->count;
+  const size_t bytes = elts * eb;
+  DevGuard g(device);
+  if (comm->preScratchBytes < bytes) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHECK(hipStreamIsCapturing(c->stream, &cap));
+    if (cap != hipStreamCaptureStatusNone) {
+      warn("user PreMulSum of %zu bytes inside a stream capture needs its scratch first: run one eager call of "
+           "that size on this communicator before capturing", bytes);
+      return ncclInvalidUsage;
+    }
+    size_t want = std::max<size_t>(bytes, std::max<size_t>(2 * comm->preScratchBytes, 1u << 20));
+    void* p = nullptr;
+    HIPCHECK(hipMalloc(&p, want));
+    if (comm->preScratch) comm->preScratchOld.push_back(comm->preScratch);
+    comm->preScratch = p;
+    comm->preScratchBytes = want;
+  }
+  void* dsts[1] = {comm->preScratch};
+  const void* srcs[1] = {c->send};
+  NCCLCHECK(nbxReduceMulti(dsts, 1, srcs, 1, elts, c->dt, c->op, /*nPreOpSrcs=*/1, /*postOp=*/0,
+                           (ncclStream_t)c->stream));
+  c->send = comm->preScratch;
+  c->op = nbxDevRedOpFull{nbxDevSum, 0, 0};
+  c->localPre = false;
+  return ncclSuccess;
+}
+
 // ---------------------------------------------------------------------------
 // Group semantics (group.cc:82-103 depth is thread-local). One-rank
 // collectives launch at enqueue, as in the reference (taskAppend returns after
@@ -246,8 +281,11 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
     if (r != ncclSuccess) comm->asyncError.store(r);
     return r;
   }
+  // a user PreMulSum: the scalar is this rank's alone (PendingColl::localPre)
+  const bool localPre = (int)op >= (int)ncclNumOps && opFull.op == nbxDevPreMulSum;
   if (comm->mp) {
-    const MpCall call{kind, sendbuff, recvbuff, count, dt, opFull, root, stream};
+    MpCall call{kind, sendbuff, recvbuff, count, dt, opFull, root, stream};
+    call.localPre = localPre;
     if (t_groupDepth > 0) {   // run at the outermost ncclGroupEnd
       if (comm->mp->group.empty()) t_groupMpComms.push_back(comm);
       comm->mp->group.push_back(call);
@@ -266,7 +304,9 @@ ncclResult_t enqueueColl(CollKind kind, const char* opName, const void* sendbuff
   }
   {
     std::lock_guard<std::mutex> g(g_pendMu);
-    comm->clique->pending[comm->rank].push_back(PendingColl{kind, sendbuff, recvbuff, count, dt, opFull, root, stream});
+    PendingColl pc{kind, sendbuff, recvbuff, count, dt, opFull, root, stream};
+    pc.localPre = localPre;
+    comm->clique->pending[comm->rank].push_back(pc);
   }
   if (t_groupDepth == 0) return flushPending();
   return ncclSuccess;

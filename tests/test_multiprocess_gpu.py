@@ -1552,6 +1552,138 @@ def test_multiprocess_every_type_and_op(nbx, oracle, monkeypatch):
     assert not bad, bad[:10]
 
 
+# user PreMulSum with a different scalar on every rank: the reference applies
+# each rank's scalar to its own input only (prims_simple.h:269-270, :617-628),
+# so the result is sum_r s_r * x_r. (dtype, count, kind); scalars per rank
+PREMUL_CASES = [(7, 1000, "ar"), (7, 100003, "ar"), (7, 2 * 1024 * 1024 + 5, "ar"), (7, 100003, "rs"),
+                (7, 2 * 1024 * 1024 + 5, "rs"), (7, 100003, "red"), (6, 40001, "ar"), (9, 700001, "ar"),
+                (2, 100003, "ar"), (4, 5001, "red"), (10, 300001, "ar"), (8, 50001, "rs")]
+PREMUL_FLOATS = (0.5, -1.25, 3.0, 0.75)
+PREMUL_INTS = (3, -2, 5, 7)
+
+
+def _premul_scalar(np_, dtype, r):
+    from oracle import oracle
+    st = oracle.NP_STORAGE[dtype]
+    if dtype in (0, 1, 2, 3, 4, 5):
+        return np_.array([PREMUL_INTS[r]]).astype(st)
+    f = PREMUL_FLOATS[r]
+    if dtype == 6:
+        return np_.array([oracle.f32_to_f16(f)], dtype=st)
+    if dtype == 9:
+        return np_.array([oracle.f32_to_bf16(f)], dtype=st)
+    if dtype == 10:
+        return np_.array([oracle.f32_to_e4m3(f)], dtype=st)
+    if dtype == 11:
+        return np_.array([oracle.f32_to_e5m2(f)], dtype=st)
+    return np_.array([f]).astype(st)
+
+
+def _child_premul(uid_bytes, rank, n, q, device_scalar):
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        for i, (dtype, count, kind) in enumerate(PREMUL_CASES):
+            sc = _premul_scalar(np, dtype, rank)
+            if device_scalar:
+                dsc = torch.from_numpy(sc.view(np.uint8).copy()).cuda()
+                op = comm.redop_create_premulsum(dsc.data_ptr(), dtype, nbx.ncclScalarResidence.ncclScalarDevice)
+            else:
+                op = comm.redop_create_premulsum(sc.ctypes.data, dtype)
+            x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
+            tx = torch.from_numpy(x.copy()).cuda()
+            ty = torch.zeros(x.size // n if kind == "rs" else x.size, dtype=torch.uint8, device="cuda")
+            root = 1 % n
+            if kind == "ar":
+                comm.all_reduce(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
+            elif kind == "rs":
+                comm.reduce_scatter(tx.data_ptr(), ty.data_ptr(), count, dtype, op, st)
+            else:
+                comm.reduce(tx.data_ptr(), ty.data_ptr() if rank == root else 0, count, dtype, op, root, st)
+            torch.cuda.synchronize()
+            comm.redop_destroy(op)
+            out[i] = ty.cpu().numpy().copy()
+        # the same op inside a group next to an ordinary call (never batched with it)
+        sc = _premul_scalar(np, 7, rank)
+        op = comm.redop_create_premulsum(sc.ctypes.data, 7)
+        x = _ll_input("ar", 7, 1000, n, rank)
+        tx = torch.from_numpy(x.view(np.uint8).copy()).cuda()
+        ty1 = torch.zeros(x.nbytes, dtype=torch.uint8, device="cuda")
+        ty2 = torch.zeros(x.nbytes, dtype=torch.uint8, device="cuda")
+        nbx.group_start()
+        comm.all_reduce(tx.data_ptr(), ty1.data_ptr(), 1000, 7, 0, st)
+        comm.all_reduce(tx.data_ptr(), ty2.data_ptr(), 1000, 7, op, st)
+        nbx.group_end()
+        torch.cuda.synchronize()
+        comm.redop_destroy(op)
+        out["group_sum"] = ty1.cpu().numpy().copy()
+        out["group_premul"] = ty2.cpu().numpy().copy()
+        assert comm.async_error() == 0
+        comm.destroy()
+        q.put((rank, "ok", out))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def _premul_expected(oracle, kind, dtype, count, n, xs_by_rank):
+    """sum over ranks of (x_r * s_r rounded to the type), folded in the
+    direct schedule's order; expected per rank (Reduce: the root only)."""
+    st = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st).itemsize
+    scaled = [oracle.reduce_multi([xs_by_rank[r]], dtype, 3, int(_premul_scalar(np, dtype, r).view(
+        {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[eb])[0]), n_pre_op_srcs=1)[0] for r in range(n)]
+    exp = {}
+    if kind == "ar":
+        full = np.empty(count, dtype=st)
+        for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+            if hi > lo:
+                order = [(c + 1 + k) % n for k in range(n)]
+                full[lo:hi] = oracle.reduce_multi([scaled[j][lo:hi] for j in order], dtype, 0)[0]
+        exp = {r: full for r in range(n)}
+    elif kind == "rs":
+        for r in range(n):
+            order = [(r + 1 + k) % n for k in range(n)]
+            exp[r] = oracle.reduce_multi([scaled[j][r * count:(r + 1) * count] for j in order], dtype, 0)[0]
+    else:
+        root = 1 % n
+        order = [(root + 1 + k) % n for k in range(n)]
+        exp[root] = oracle.reduce_multi([scaled[j] for j in order], dtype, 0)[0]
+    return exp
+
+
+@pytest.mark.parametrize("n,device_scalar", [(2, False), (3, False), (3, True)])
+def test_multiprocess_user_premulsum_per_rank_scalars(nbx, oracle, monkeypatch, n, device_scalar):
+    """ncclRedOpCreatePreMulSum with a different scalar on every rank (host
+    immediate or device-resident): sum_r s_r * x_r, as the reference computes
+    it, at LL, LL128 and Simple sizes for AllReduce / ReduceScatter / Reduce
+    and several types; inside a group it runs beside a plain Sum call."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    res = _run_ranks(nbx, n, _child_premul, device_scalar)
+    bad = []
+    for i, (dtype, count, kind) in enumerate(PREMUL_CASES):
+        xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
+        for r, e in _premul_expected(oracle, kind, dtype, count, n, xs).items():
+            if not np.array_equal(res[r][i], np.ascontiguousarray(e).view(np.uint8)):
+                bad.append((kind, dtype, count, r))
+    assert not bad, bad
+    xs = [_ll_input("ar", 7, 1000, n, r) for r in range(n)]
+    e = _premul_expected(oracle, "ar", 7, 1000, n, xs)[0]
+    plain = np.empty(1000, np.float32)
+    for c, (lo, hi) in enumerate(_blocks(1000, 4, n)):
+        order = [(c + 1 + k) % n for k in range(n)]
+        plain[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], 7, 0)[0]
+    for r in range(n):
+        assert np.array_equal(res[r]["group_premul"], e.view(np.uint8)), r
+        assert np.array_equal(res[r]["group_sum"], plain.view(np.uint8)), r
+
+
 def _child_split(uid_bytes, rank, n, q):
     """ncclCommSplit over a multi-process communicator: children ordered by
     key (ties by parent rank), NCCL_SPLIT_NOCOLOR gets NULL, every child works;

@@ -202,6 +202,63 @@ def test_clique_counts_past_32_bits(nbx, torch_gpu):
             c.destroy()
 
 
+def test_clique_user_premulsum_per_rank_scalars(nbx, oracle, torch_gpu):
+    """A 3-rank clique with a different PreMulSum scalar per rank: sum_r s_r x_r
+    (the reference's per-rank pre-op), AllReduce / ReduceScatter / Reduce on
+    the fold path, f32 and bf16."""
+    torch = torch_gpu
+    nranks = 3
+    scal = (0.5, -1.25, 3.0)
+    comms = nbx.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    try:
+        for dtype in (F32, BF16):
+            st_ = oracle.NP_STORAGE[dtype]
+            eb = np.dtype(st_).itemsize
+            bits = [np.array([s_], np.float32).view(np.uint32)[0] if dtype == F32 else oracle.f32_to_bf16(s_)
+                    for s_ in scal]
+            hs = [np.array([b], dtype=np.uint32 if dtype == F32 else np.uint16) for b in bits]
+            for kind in ("ar", "rs", "red"):
+                count = 50003
+                total = count * nranks if kind == "rs" else count
+                xs = oracle.random_inputs(dtype, nranks, total, seed=61 + dtype)
+                txs = [t_of(torch, x) for x in xs]
+                outs = [torch.zeros(count * eb, dtype=torch.uint8, device="cuda") for _ in range(nranks)]
+                ops = [comms[r].redop_create_premulsum(hs[r].ctypes.data, dtype) for r in range(nranks)]
+                torch.cuda.synchronize()
+                nbx.group_start()
+                for r in range(nranks):
+                    sp, rp, s_ = txs[r].data_ptr(), outs[r].data_ptr(), streams[r].cuda_stream
+                    if kind == "ar":
+                        comms[r].all_reduce(sp, rp, count, dtype, ops[r], s_)
+                    elif kind == "rs":
+                        comms[r].reduce_scatter(sp, rp, count, dtype, ops[r], s_)
+                    else:
+                        comms[r].reduce(sp, rp if r == 2 else 0, count, dtype, ops[r], 2, s_)
+                nbx.group_end()
+                torch.cuda.synchronize()
+                for r in range(nranks):
+                    comms[r].redop_destroy(ops[r])
+                scaled = [oracle.reduce_multi([xs[r]], dtype, 3, int(bits[r]), n_pre_op_srcs=1)[0]
+                          for r in range(nranks)]
+                if kind == "ar":
+                    exp = _ring_order_reduce(oracle, scaled, dtype, 0, 0, False, nranks, _blocks(count, eb, nranks))
+                    want = {r: exp for r in range(nranks)}
+                elif kind == "rs":
+                    exp = _ring_order_reduce(oracle, scaled, dtype, 0, 0, False, nranks,
+                                             lambda b: (b * count, (b + 1) * count))
+                    want = {r: exp[r * count:(r + 1) * count] for r in range(nranks)}
+                else:
+                    want = {2: _ring_order_reduce(oracle, scaled, dtype, 0, 0, False, nranks,
+                                                  _blocks(count, eb, nranks), root=2)}
+                for r, e in want.items():
+                    assert np.array_equal(outs[r].cpu().numpy(), np.ascontiguousarray(e).view(np.uint8)), \
+                        (dtype, kind, r)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_clique_every_type_and_op(nbx, oracle, torch_gpu):
     """Every type x sum / prod / max / min / avg as a 3-rank clique AllReduce
     (odd count, the event-ordered direct fold), and ReduceScatter / Reduce
