@@ -26,7 +26,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# (ncclDataType, torch dtype name); ops: 0 sum, 2 max, 3 min
+# (ncclDataType, torch dtype name); ops: 0 sum, 2 max, 3 min, PREMUL a user
+# ncclRedOpCreatePreMulSum with rank r's own scalar (r % 3) + 1 (fp32 / int32 /
+# int64 only, where every sum stays exact): expected sum_r s_r * x_r
+PREMUL = 9
 TYPES = [(7, "float32"), (2, "int32"), (4, "int64"), (6, "float16"), (9, "bfloat16")]
 SIZES = [1, 3, 100, 1000, 4099, 16384, 40000, 200000, 1 << 20, 3 << 20]
 
@@ -36,7 +39,9 @@ def plan(rng, n):
     for _ in range(rng.randint(4, 24)):
         kind = rng.choice(["allreduce", "allreduce", "reducescatter", "reduce"])
         dt, tname = rng.choice(TYPES)
-        op = rng.choice([0, 0, 2, 3])
+        op = rng.choice([0, 0, 2, 3, PREMUL])
+        if op == PREMUL and tname not in ("float32", "int32", "int64"):
+            op = 0
         root = rng.randrange(n)
         if calls and rng.random() < 0.35:   # runs of one kind / type / op (/ root): what a group launch batches
             p = calls[-1]
@@ -46,7 +51,7 @@ def plan(rng, n):
             count = min(count, 40000)
         dep = False
         if (calls and calls[-1]["kind"] == "allreduce" and kind == "allreduce" and dt == calls[-1]["dt"] and
-                op == calls[-1]["op"] and (op in (2, 3) or tname in ("float32", "int32", "int64")) and
+                op == calls[-1]["op"] and op != PREMUL and (op in (2, 3) or tname in ("float32", "int32", "int64")) and
                 rng.random() < 0.5):
             # reads the previous call's output: a run must be cut before it
             dep, count = True, calls[-1]["count"]
@@ -95,13 +100,19 @@ def rank_main(rank, n, iters, seed, uid, q):
                     nbx.group_end()
                     in_group = False
                 s = streams[c["stream"]].cuda_stream
+                op = c["op"]
+                if op == PREMUL:   # the op's state is copied at enqueue: destroyed right after the call
+                    sc = torch.tensor([(rank % 3) + 1], dtype=x.dtype)
+                    op = comm.redop_create_premulsum(sc.data_ptr(), c["dt"])
                 if c["kind"] == "allreduce":
-                    comm.all_reduce(x.data_ptr(), y.data_ptr(), c["count"], c["dt"], c["op"], s)
+                    comm.all_reduce(x.data_ptr(), y.data_ptr(), c["count"], c["dt"], op, s)
                 elif c["kind"] == "reducescatter":
-                    comm.reduce_scatter(x.data_ptr(), y.data_ptr(), c["count"], c["dt"], c["op"], s)
+                    comm.reduce_scatter(x.data_ptr(), y.data_ptr(), c["count"], c["dt"], op, s)
                 else:
-                    comm.reduce(x.data_ptr(), y.data_ptr() if rank == c["root"] else 0, c["count"], c["dt"], c["op"],
+                    comm.reduce(x.data_ptr(), y.data_ptr() if rank == c["root"] else 0, c["count"], c["dt"], op,
                                 c["root"], s)
+                if c["op"] == PREMUL:
+                    comm.redop_destroy(op)
                 live.append((k, c, x, y))   # x too: a queued or in-flight call still reads it
             if in_group:
                 nbx.group_end()
@@ -115,7 +126,10 @@ def rank_main(rank, n, iters, seed, uid, q):
                 else:
                     xs = [_input(torch, c, r, it, k, n, dev) for r in range(n)]
                     st = torch.stack([t.to(torch.float64) for t in xs])
-                    ref = st.sum(0) if c["op"] == 0 else (st.amax(0) if c["op"] == 2 else st.amin(0))
+                    if c["op"] == PREMUL:
+                        st = st * torch.tensor([(r % 3) + 1 for r in range(n)], dtype=torch.float64,
+                                               device=dev).view(-1, 1)
+                    ref = st.sum(0) if c["op"] in (0, PREMUL) else (st.amax(0) if c["op"] == 2 else st.amin(0))
                     ref = ref.to(y.dtype)
                 refs.append(ref)
                 if c["kind"] == "reducescatter":
