@@ -5,7 +5,8 @@ LL128 transport forced on for ranks that share the one GPU of the test box
 (NBX_CLIQUE_LL=1; each rank's kernel waits for its peers', so every rank has
 its own streams, and GPU_MAX_HW_QUEUES gives every stream its own hardware
 queue — set here, before anything loads HIP). Same plans as mp_stress.py
-(AllReduce / ReduceScatter / Reduce, random dtype, op, size across LL, LL128
+(AllReduce / ReduceScatter / Reduce, random dtype, op — user PreMulSum with
+per-rank scalars included — size across LL, LL128
 one- and two-shot and the Simple-sized fold path, groups), plus stream switches
 and calls whose ranks all share one stream (those take the fold path), so the
 ordering between the two paths is exercised too.
@@ -31,7 +32,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
-from mp_stress import _input, plan  # noqa: E402
+from mp_stress import PREMUL, _input, plan  # noqa: E402
 
 
 def run(n: int, iters: int, seed: int, perf: bool) -> dict:
@@ -74,13 +75,19 @@ def run(n: int, iters: int, seed: int, perf: bool) -> dict:
                 nbx.group_start()
             for r in range(n):
                 s = (shared if c["shared"] else streams[r][c["stream"]]).cuda_stream
+                op = c["op"]
+                if op == PREMUL:   # rank r's own scalar (r % 3) + 1; state copied at enqueue
+                    sc = torch.tensor([(r % 3) + 1], dtype=xs[r].dtype)
+                    op = comms[r].redop_create_premulsum(sc.data_ptr(), c["dt"])
                 if c["kind"] == "allreduce":
-                    comms[r].all_reduce(xs[r].data_ptr(), ys[r].data_ptr(), c["count"], c["dt"], c["op"], s)
+                    comms[r].all_reduce(xs[r].data_ptr(), ys[r].data_ptr(), c["count"], c["dt"], op, s)
                 elif c["kind"] == "reducescatter":
-                    comms[r].reduce_scatter(xs[r].data_ptr(), ys[r].data_ptr(), c["count"], c["dt"], c["op"], s)
+                    comms[r].reduce_scatter(xs[r].data_ptr(), ys[r].data_ptr(), c["count"], c["dt"], op, s)
                 else:
                     comms[r].reduce(xs[r].data_ptr(), ys[r].data_ptr() if r == c["root"] else 0, c["count"],
-                                    c["dt"], c["op"], c["root"], s)
+                                    c["dt"], op, c["root"], s)
+                if c["op"] == PREMUL:
+                    comms[r].redop_destroy(op)
             if not in_group:
                 nbx.group_end()
             live.append((k, c, xs, ys))
@@ -98,7 +105,9 @@ def run(n: int, iters: int, seed: int, perf: bool) -> dict:
             return out
         for k, c, xs, ys in live:
             st = torch.stack([t.to(torch.float64) for t in xs])
-            ref = st.sum(0) if c["op"] == 0 else (st.amax(0) if c["op"] == 2 else st.amin(0))
+            if c["op"] == PREMUL:
+                st = st * torch.tensor([(r % 3) + 1 for r in range(n)], dtype=torch.float64, device=dev).view(-1, 1)
+            ref = st.sum(0) if c["op"] in (0, PREMUL) else (st.amax(0) if c["op"] == 2 else st.amin(0))
             ref = ref.to(ys[0].dtype)
             for r in range(n):
                 if c["kind"] == "reduce" and r != c["root"]:
