@@ -205,3 +205,15 @@ def test_vs_rccl_ratios_include_the_curve():
     assert v["allreduce_curve"] == [0.5, 1.0]
     assert v["sweep_best_protocol"] == [0.5, 1.0]
     assert bench.vs_rccl(coll, {"ok": False}) is None
+
+
+def test_fabric_fields_absent_without_probe_numbers():
+    """A leg that never reached the link probe (or a rank without it) leaves
+    the fabric fields out instead of reporting a rate from partial data."""
+    out = {"allreduce_direct": {"ms": 10.0}}
+    bench.add_fabric_rates(out, [{"link_push_ms": 2.0, "link_bytes_per_peer": 1 << 20}, {}], 2, 1 << 30)
+    assert "fabric" not in out and "fabric_floor_ms" not in out["allreduce_direct"]
+    out = {"allreduce_direct": {"ms": 10.0}, "allreduce_ring": None}
+    bench.add_fabric_rates(out, [{"link_push_ms": 2.0, "link_bytes_per_peer": 1 << 20}] * 2, 2, 1 << 30)
+    assert out["fabric"]["push_GBs_per_link"] == round((1 << 20) / 2e-3 / 1e9, 2) and out["fabric"]["pull_GBs_per_link"] is None
+    assert out["allreduce_direct"]["fabric_link_bytes"] == (1 << 30) and out["allreduce_ring"] is None

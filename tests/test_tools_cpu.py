@@ -132,3 +132,16 @@ def test_set_thresholds_cli(tmp_path):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "set_thresholds.py"), str(p), "--shared-gpu"],
                          capture_output=True, text=True, check=True).stdout
     assert "export NBX_LL_MAX_BYTES=1048576" in out and "unset NBX_LL128_ACROSS_GPUS" in out
+
+
+def test_set_thresholds_on_the_r5_rehearsal_with_knobs():
+    """The committed N = 4 shared-GPU line with the Simple-knob sweep (r5z): the
+    default knobs win there, so every knob stays unset; the line parses with
+    every round-5 field present."""
+    st = _thr()
+    b = st.last_collective_line(os.path.join(ROOT, "profiles", "r5", "bench_n4_shared_r5z.json"))
+    assert set(b["collective"]["simple_knobs"]) == {"slice256K", "grid64", "slots4", "default"}
+    r = st.thresholds(b)
+    env = r["env"]
+    assert env["NBX_SIMPLE_SLICE_BYTES"] == "" and env["NBX_SIMPLE_MAX_GRID"] == "" and env["NBX_SIMPLE_SLOTS"] == ""
+    assert env["NBX_LL128_ACROSS_GPUS"] == ""   # ranks shared one GPU
