@@ -210,16 +210,32 @@ class Emitter:
             print(json.dumps(line), flush=True)
 
 
+# Exit status of a run whose N > 1 legs were cut off (a leg gave no result in
+# its time, or the watchdog ended the run): the final line is printed first and
+# keeps the headline value, but the status tells a harness that checks it
+# that a leg hung. A complete run exits 0.
+EXIT_LEG_CUT_OFF = 3
+
+
+def legs_cut_off(coll) -> bool:
+    """True when any N > 1 leg of the final line ended without its result."""
+    if not isinstance(coll, dict):
+        return False
+    if coll.get("incomplete"):
+        return True
+    return any(isinstance(v, dict) and v.get("incomplete") for v in coll.values())
+
+
 class Watchdog:
     """Ends this rank when the leg budget (+ grace) is spent: rank 0 prints the
     final line with what the legs produced so far and the reason, every rank
-    kills its own leg children (by PID) and exits 0 — the headline value
-    stands; `collective.ok` is false."""
+    kills its own leg children (by PID) and exits EXIT_LEG_CUT_OFF — the
+    headline value stands in the line; `collective.ok` is false."""
 
     def __init__(self, seconds: float, emitter: Emitter, children, exit_fn=None):
         self.emitter = emitter
         self.children = [c for c in children if c is not None]
-        self.exit_fn = exit_fn or (lambda: os._exit(0))
+        self.exit_fn = exit_fn or (lambda: os._exit(EXIT_LEG_CUT_OFF))
         self.cancelled = threading.Event()
         self.seconds = seconds
         self.thread = threading.Thread(target=self._run, daemon=True)
@@ -643,6 +659,8 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0, 
     errs = [f"rank {r.get('rank')}: {e}" for r in allres for e in r.get("errors", [])]
     if errs:
         out["errors"] = errs[:8]
+    if any(r.get("incomplete") for r in allres):
+        out["incomplete"] = True   # a rank's leg gave no final result (exit status EXIT_LEG_CUT_OFF)
 
     def agg(key, busfac, alg_bytes):
         vals = [r.get(key) for r in allres]
@@ -1116,7 +1134,8 @@ def main(argv=None):
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    return EXIT_LEG_CUT_OFF if rank == 0 and legs_cut_off(result.get("collective")) else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

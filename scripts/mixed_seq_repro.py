@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""mixed_seq_repro.py — replay test_multiprocess_ll_protocol's mixed sequence
+(LL, LL128 one- and two-shot and Simple direct calls, back to back with no
+host synchronisation) at N ranks sharing GPU 0, many iterations, and describe
+every wrong output (tests/mp_diag.py): wrong-element count, their (block,
+round, workgroup) cells, and what the wrong values equal — zero, a peer's raw
+input, the fold without one source, or the previous iteration's output of that
+call in that buffer position.
+
+GPUTEST_r05: case 36 (int32 max, 1,000,003 elements, Simple direct) at 8
+ranks returned wrong data on rank 0 with no error.
+
+usage: mixed_seq_repro.py [--ranks 8] [--iters 10] [--cases 30:41] [--jitter]
+Prints one JSON line: {"ranks", "iters", "calls", "mismatches": [...], "errors"}.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _cases():
+    from tests.test_multiprocess_gpu import LL_CASES
+    return LL_CASES
+
+
+def _expected(oracle, case, i, n):
+    """rank -> expected output (storage dtype), and the fold order per block."""
+    import numpy as np
+    from tests.test_multiprocess_gpu import _blocks, _ll_input, _ll_root
+    kind, dtype, op, count, _ = case
+    xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
+    devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+    st = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st).itemsize
+    kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+    exp = {}
+    if kind == "ar":
+        full = np.empty(count, dtype=st)
+        for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+            if hi > lo:
+                order = [(c + 1 + k) % n for k in range(n)]
+                full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg, **kw)[0]
+        exp = {r: full for r in range(n)}
+    elif kind == "rs":
+        for r in range(n):
+            order = [(r + 1 + k) % n for k in range(n)]
+            exp[r] = oracle.reduce_multi([xs[j][r * count:(r + 1) * count] for j in order], dtype, devop, arg,
+                                         **kw)[0]
+    else:
+        root = _ll_root(i, n)
+        order = [(root + 1 + k) % n for k in range(n)]
+        exp[root] = oracle.reduce_multi([xs[j] for j in order], dtype, devop, arg, **kw)[0]
+    return exp, xs
+
+
+def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q):
+    try:
+        import random
+
+        import numpy as np
+        import torch
+        from oracle import oracle
+        from tests.conftest import load_package
+        from tests.test_multiprocess_gpu import _ll_input, _ll_root
+        cases = _cases()
+        nbx = load_package()
+        nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        settings = comm_settings(nbx, comm)
+        st = torch.cuda.current_stream().cuda_stream
+        exp = {}
+        for i in case_ids:
+            e, _ = _expected(oracle, cases[i], i, n)
+            if rank in e:
+                exp[i] = np.ascontiguousarray(e[rank]).view(np.uint8)
+        rng = random.Random(1234 + rank)
+        bad = []
+        prev = {}
+        calls = 0
+        t0 = time.time()
+        for it in range(iters):
+            keep = []
+            for i in case_ids:
+                kind, dtype, op, count, shift = cases[i]
+                x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
+                tx = torch.zeros(x.size + 16, dtype=torch.uint8, device="cuda")
+                tx[shift:shift + x.size] = torch.from_numpy(x.copy()).cuda()
+                out_bytes = x.size // n if kind == "rs" else x.size
+                ty = torch.zeros(out_bytes + 16, dtype=torch.uint8, device="cuda")
+                sp, rp = tx.data_ptr() + shift, ty.data_ptr() + shift
+                if jitter and rng.random() < 0.3:
+                    time.sleep(rng.random() * 0.004)
+                if kind == "ar":
+                    comm.all_reduce(sp, rp, count, dtype, op, st)
+                elif kind == "rs":
+                    comm.reduce_scatter(sp, rp, count, dtype, op, st)
+                else:
+                    comm.reduce(sp, rp, count, dtype, op, _ll_root(i, n), st)
+                calls += 1
+                keep.append((i, ty, shift, out_bytes))
+            torch.cuda.synchronize()
+            for i, ty, shift, nb in keep:
+                if i not in exp:
+                    continue
+                got = ty[shift:shift + nb].cpu().numpy().copy()
+                if not np.array_equal(got, exp[i]):
+                    bad.append({"it": it, "case": i, "got": got, "prev": prev.get(i)})
+                prev[i] = got
+            if time.time() - t0 > 60 * (it + 1) / max(iters, 1) + 120:
+                break
+        err = comm.async_error()
+        comm.destroy()
+        q.put((rank, "ok", {"bad": bad, "calls": calls, "async_error": err, "settings": settings,
+                            "s": time.time() - t0}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def comm_settings(nbx, comm):
+    import ctypes
+    lib = nbx.load_library()
+    out = (ctypes.c_int64 * 10)()
+    k = lib.nbxDebugCommSettings(comm.handle, out, 10)
+    names = ["llMax", "l128Max", "sliceBytes", "slots", "simpleGrid", "llGridCap", "l128GridCap", "groupBatch",
+             "ipcRepairs", "checkPlans"]
+    return {names[j]: int(out[j]) for j in range(max(k, 0))}
+
+
+def diagnose(oracle, n, case_id, rank, got_u8, prev_u8, settings):
+    import numpy as np
+    from tests import mp_diag
+    cases = _cases()
+    kind, dtype, op, count, _ = cases[case_id]
+    exp, xs = _expected(oracle, cases[case_id], case_id, n)
+    st = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st).itemsize
+    e = np.ascontiguousarray(exp[rank])
+    got = got_u8.view(st)
+    base = rank * count if kind == "rs" else 0
+    cand = {}
+    devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+    kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+    # raw inputs of every rank (send side, at the output's positions)
+    for j in range(n):
+        cand[f"raw_input_rank{j}"] = np.ascontiguousarray(xs[j][base:base + e.size])
+    # the fold with one rank's source left out (AllReduce / ReduceScatter blocks in rank order b+1, ..., b)
+    if kind in ("ar", "rs") and n > 1:
+        from tests.test_multiprocess_gpu import _blocks
+        blocks = _blocks(count, eb, n) if kind == "ar" else [(b * count, (b + 1) * count) for b in range(n)]
+        for j in range(n):
+            alt = np.empty(e.size, dtype=st)
+            for b, (lo, hi) in enumerate(blocks):
+                olo, ohi = lo - base, hi - base
+                if ohi <= 0 or olo >= e.size or hi <= lo:
+                    continue
+                order = [(b + 1 + k) % n for k in range(n) if (b + 1 + k) % n != j]
+                alt[olo:ohi] = oracle.reduce_multi([xs[q][lo:hi] for q in order], dtype, devop, arg, **kw)[0]
+            cand[f"without_rank{j}"] = alt
+    if prev_u8 is not None and prev_u8.size == got_u8.size:
+        cand["prev_iteration_output"] = prev_u8.view(st)
+    geom = None
+    if settings:
+        geom = mp_diag.simple_geometry(kind, count, eb, n, settings.get("simpleGrid", 32),
+                                       settings.get("sliceBytes", 65536))
+    d = mp_diag.describe_mismatch(got, e, geom, base, cand)
+    d["explained_by"] = {k: v for k, v in d.get("explained_by", {}).items() if v}
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cases", default="0:41")
+    ap.add_argument("--jitter", action="store_true")
+    args = ap.parse_args()
+    lo, hi = (int(x) for x in args.cases.split(":"))
+    case_ids = list(range(lo, min(hi, len(_cases()))))
+    os.environ.setdefault("NBX_BOOTSTRAP_TIMEOUT", "60")
+    os.environ.setdefault("NBX_TIMEOUT_SEC", "60")
+    os.environ.setdefault("NBX_LL128_MAX_GRID", "16")
+    from oracle import oracle
+    oracle.build()
+    from tests.conftest import load_package
+    nbx = load_package()
+    nbx.load_library()
+    n = args.ranks
+    uid = nbx.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=rank_main, args=(bytes(uid), r, n, args.iters, case_ids, args.jitter, q), daemon=True)
+             for r in range(n)]
+    for p in procs:
+        p.start()
+    res, errors = {}, []
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=600)
+            if status != "ok":
+                errors.append({"rank": rank, "error": payload[-3000:]})
+            else:
+                res[rank] = payload
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.terminate()
+    mism = []
+    for r, pl in sorted(res.items()):
+        for b in pl["bad"][:6]:
+            d = diagnose(oracle, n, b["case"], r, b["got"], b["prev"], pl["settings"])
+            mism.append({"rank": r, "it": b["it"], "case": b["case"], "call": list(_cases()[b["case"]]), **d})
+    out = {"ranks": n, "iters": args.iters, "cases": args.cases, "jitter": args.jitter,
+           "env": {k: v for k, v in os.environ.items() if k.startswith(("NBX_", "NCCL_"))},
+           "calls": sum(pl["calls"] for pl in res.values()),
+           "bad_calls": sum(len(pl["bad"]) for pl in res.values()),
+           "bad_per_rank": {r: len(pl["bad"]) for r, pl in res.items()},
+           "async_errors": {r: pl["async_error"] for r, pl in res.items() if pl["async_error"]},
+           "settings": res[min(res)]["settings"] if res else None,
+           "seconds": max((pl["s"] for pl in res.values()), default=None),
+           "mismatches": mism, "errors": errors}
+    print(json.dumps(out, default=str), flush=True)
+    return 1 if (mism or errors) else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

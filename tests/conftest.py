@@ -16,6 +16,37 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu on the GPU box")
 
 
+# Run order of the GPU suite: the single-GPU parity core first —
+# every type x op vs the oracle, config B at full size, config A, the API
+# entry points, config C — then the multi-process transport and the stress
+# files, so that `-x` can never hide the core oracle checks behind a
+# transport failure. Tests inside a file keep their order; files not listed
+# run between the core and the transport group.
+GPU_FILE_ORDER = [
+    "test_reduce_gpu.py", "test_config_a.py", "test_nccl_api_gpu.py", "test_rccl_corroboration_gpu.py",
+    "test_c_perf_gpu.py", "test_bench_rccl_gpu.py",
+    None,   # everything else
+    "test_configs_gpu.py", "test_clique_transport_gpu.py", "test_multiprocess_gpu.py",
+    "test_multiprocess_churn_gpu.py", "test_multiprocess_stress_gpu.py", "test_sched_stress_gpu.py",
+]
+
+
+def gpu_order_key(item_path: str, test_name: str = "") -> tuple:
+    base = os.path.basename(item_path)
+    rank = GPU_FILE_ORDER.index(base) if base in GPU_FILE_ORDER else GPU_FILE_ORDER.index(None)
+    # test_configs_gpu.py: config C (one GPU) before configs D / E (8 ranks)
+    sub = 1 if base == "test_configs_gpu.py" and "8_ranks" in test_name else 0
+    if base == "test_configs_gpu.py" and not sub:
+        rank = GPU_FILE_ORDER.index("test_bench_rccl_gpu.py")
+    return (rank, sub)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    keyed = [(gpu_order_key(str(it.fspath), it.name), i, it) for i, it in enumerate(items)]
+    keyed.sort(key=lambda t: (t[0], t[1]))
+    items[:] = [t[2] for t in keyed]
+
+
 def load_package():
     """Import neuronabox-nccl_amd (hyphenated directory) as `neuronabox_nccl_amd`."""
     name = "neuronabox_nccl_amd"

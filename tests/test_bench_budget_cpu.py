@@ -3,7 +3,8 @@ run bench.main under torch.distributed.run with the GPU headline replaced by a
 stub and every leg hanging — the multi-process collective child after one
 partial result, the clique child, and the RCCL leg inside the bench process —
 at the legs' DEFAULT timeouts (400 s each). The run must end inside the leg
-budget (+ the watchdog's grace), exit 0, and leave the headline value on
+budget (+ the watchdog's grace), exit non-zero (rank 0's status
+bench.EXIT_LEG_CUT_OFF: a leg was cut off), and leave the headline value on
 stdout twice: once before the legs, and last with `collective.ok` false and
 the reason, carrying what the collective child reported before it hung."""
 import json
@@ -71,7 +72,7 @@ if os.environ.get("STUB_MODE") == "hang":
     def hanging_rccl(world):
         time.sleep(3600)
     bench.rccl_leg = hanging_rccl
-bench.main(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+sys.exit(bench.main(["--gpus", "2", "--steps", "1", "--warmup", "0"]))
 '''
 
 
@@ -117,7 +118,10 @@ def test_skipped_leg_names_the_budget():
 def test_every_leg_hangs_the_run_ends_inside_the_budget(tmp_path):
     budget, leg_min, grace = 12.0, 3.0, 3.0
     p, el, lines = _run(tmp_path, "hang", budget, leg_min, grace)
-    assert p.returncode == 0, p.stderr[-3000:]
+    # the run says a leg was cut off: rank 0 exits EXIT_LEG_CUT_OFF, torchrun fails the job
+    assert p.returncode != 0, p.stderr[-3000:]
+    assert f"exitcode  : {bench.EXIT_LEG_CUT_OFF}" in p.stderr or f"exitcode: {bench.EXIT_LEG_CUT_OFF}" in p.stderr \
+        or "ChildFailedError" in p.stderr, p.stderr[-3000:]
     # bounded by the budget + grace (+ process start-up and torch import), far below the legs' 400 s defaults
     assert el < budget + grace + 60, el
     assert len(lines) == 2, p.stdout
@@ -142,7 +146,7 @@ def test_hang_inside_the_bench_process_ends_by_the_watchdog(tmp_path):
     budget, leg_min, grace = 10.0, 3.0, 3.0
     p, el, lines = _run(tmp_path, "hang", budget, leg_min, grace, NBX_BENCH_COLLECTIVE_STUB_OK="1",
                         NBX_BENCH_CLIQUE="0")
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode != 0, p.stderr[-3000:]   # the watchdog exits EXIT_LEG_CUT_OFF
     assert el < budget + grace + 60, el
     assert len(lines) == 2, p.stdout
     last = lines[-1]
@@ -192,6 +196,18 @@ def test_legs_finish_normally_inside_the_budget(tmp_path):
     assert abs(cu["busbw_GBs"][1] - round((256 << 20) / 3e-3 / 1e9, 2)) < 1e-9   # n = 2: busbw = algbw
     fa = coll["clique"]["fold_allreduce"]
     assert abs(fa["fabric_floor_ms"] - round(max(M // n / (pull * 1e9), M // n / (push * 1e9)) * 1e3, 4)) < 1e-9
+
+
+def test_exit_status_contract():
+    """0 for a complete run; EXIT_LEG_CUT_OFF when any leg ended without its result."""
+    assert bench.EXIT_LEG_CUT_OFF not in (0, 1, 2)
+    assert not bench.legs_cut_off(None) and not bench.legs_cut_off({"ok": True, "clique": {"ok": True}})
+    assert bench.legs_cut_off({"ok": False, "incomplete": "watchdog"})
+    assert bench.legs_cut_off({"ok": False, "clique": {"ok": False, "incomplete": True}})
+    fired = []
+    wd = bench.Watchdog(0.05, bench.Emitter(1), [], exit_fn=lambda: fired.append(1))
+    wd.thread.join(5)
+    assert fired == [1]
 
 
 def test_vs_rccl_ratios_include_the_curve():

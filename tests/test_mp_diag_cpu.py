@@ -1,0 +1,108 @@
+"""CPU tests of the GPU suite's diagnosis and ordering aids.
+
+* tests/mp_diag.py turns a wrong multi-process result into a description
+  (wrong-element count, first / last index, the Simple schedule's (block,
+  round, workgroup) cells, what the wrong values equal). A synthetic mismatch
+  is fed through it and the mapping checked against the host's cut
+  (comm_mp_launch.cc mpLaunchSimple).
+* conftest.py orders the GPU suite: the single-GPU parity core before the
+  multi-process transport files, so `-x` cannot hide config B's oracle check.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests import mp_diag
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_block_range_matches_host_rule():
+    # 1,000,003 int32 over 8 ranks: ceil(count / 8) rounded up to whole 16-B packs
+    assert mp_diag.block_range(1000003, 4, 8, 0) == (0, 125004)
+    assert mp_diag.block_range(1000003, 4, 8, 7) == (875028, 1000003)
+    assert mp_diag.block_range(5, 4, 8, 3) == (5, 5)   # empty trailing blocks
+
+
+def test_simple_geometry_gputest_r05_case():
+    """GPUTEST_r05's red case: 8 ranks, int32, 1,000,003 elements, 32-workgroup
+    Simple grid, 64 KiB staging slices -> one round of 32 slices of 3,908."""
+    g = mp_diag.simple_geometry("ar", 1000003, 4, 8, 32, 64 << 10)
+    assert (g.block_elts, g.grid, g.slice_elts, g.n_rounds) == (125004, 32, 3908, 1)
+    # more workgroups than 4 KiB pieces: the grid shrinks; a small slice: many rounds
+    g2 = mp_diag.simple_geometry("ar", 4096, 4, 2, 128, 64 << 10)
+    assert (g2.block_elts, g2.grid, g2.n_rounds) == (2048, 2, 1)
+    g3 = mp_diag.simple_geometry("rs", 100000, 4, 4, 2, 4096)
+    assert (g3.block_elts, g3.grid, g3.slice_elts, g3.n_rounds) == (100000, 2, 1024, 49)
+
+
+def test_describe_synthetic_mismatch_maps_cells_and_explanations():
+    g = mp_diag.simple_geometry("ar", 1000003, 4, 8, 32, 64 << 10)
+    rng = np.random.default_rng(1)
+    srcs = [rng.integers(-2**31, 2**31 - 1, 1000003, dtype=np.int32) for _ in range(8)]
+    exp = np.maximum.reduce(srcs)
+    got = exp.copy()
+    # block 3, workgroup 17: 40 elements lost rank 5's source; block 6, workgroup 2: 8 zeros
+    lo = 3 * 125004 + 17 * 3908 + 100
+    without5 = np.maximum.reduce([s for j, s in enumerate(srcs) if j != 5])
+    idx = np.arange(lo, lo + 40)
+    got[idx] = without5[idx]
+    changed = idx[without5[idx] != exp[idx]]
+    z0 = 6 * 125004 + 2 * 3908
+    got[z0:z0 + 8] = 0
+    d = mp_diag.describe_mismatch(got, exp, g, 0, {"without_rank5": without5, "raw_input_rank0": srcs[0]})
+    assert d["n_wrong"] == changed.size + 8
+    assert d["first"] == int(changed[0]) and d["last"] == z0 + 7
+    assert d["explained_by"]["zero"] == 8
+    assert d["explained_by"]["without_rank5"] == changed.size
+    cells = {(c["block"], c["round"], c["workgroup"]): c["wrong"] for c in d["cells"]}
+    assert cells == {(3, 0, 17): changed.size, (6, 0, 2): 8}
+    assert d["first_at"][:3] == [3, 0, 17] and d["last_at"] == [6, 0, 2, 7]
+    assert d["blocks"] == {3: changed.size, 6: 8}
+    # assert_same raises with the description, and passes on equal data
+    with pytest.raises(AssertionError, match=r"block.*workgroup"):
+        mp_diag.assert_same(got.view(np.uint8), exp, ("ar", 2, 2, 1000003, 0), g)
+    mp_diag.assert_same(exp.copy().view(np.uint8), exp, "equal")
+
+
+def test_describe_reduce_scatter_base_offset():
+    """ReduceScatter output of rank r starts at send-side element r * recvcount."""
+    g = mp_diag.simple_geometry("rs", 5000, 4, 4, 8, 4096)
+    exp = np.arange(5000, dtype=np.float32)
+    got = exp.copy()
+    got[1500] = -1
+    d = mp_diag.describe_mismatch(got, exp, g, base=2 * 5000)
+    assert d["n_wrong"] == 1
+    # 20,000-byte blocks: 5 workgroups of 1,000-element slices; offset 1500 -> workgroup 1, element 500
+    assert (g.grid, g.slice_elts) == (5, 1000)
+    assert d["first_at"] == [2, 0, 1, 500]
+
+
+def test_gpu_suite_runs_single_gpu_core_first():
+    out = subprocess.run([sys.executable, "-m", "pytest", "--collect-only", "-q", "-m", "gpu", "tests"], cwd=ROOT,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    files = []
+    names = []
+    for line in out.stdout.splitlines():
+        if "::" in line:
+            f = os.path.basename(line.split("::")[0])
+            names.append(line)
+            if not files or files[-1] != f:
+                files.append(f)
+    assert len(files) == len(set(files)), files   # each file in one contiguous run
+    core = ["test_reduce_gpu.py", "test_config_a.py", "test_nccl_api_gpu.py"]
+    assert files[:3] == core, files
+    transport = [f for f in files if "multiprocess" in f or "stress" in f or "clique" in f]
+    assert transport and min(files.index(f) for f in transport) > files.index("test_nccl_api_gpu.py")
+    # config B's full-size oracle check comes before any multi-process test
+    b = next(i for i, n in enumerate(names) if "test_config_b_full_size_bit_exact" in n)
+    mp_first = next(i for i, n in enumerate(names) if "multiprocess" in n or "8_ranks" in n)
+    assert b < mp_first
+    # config C (one GPU) before configs D / E (8 ranks)
+    c = max(i for i, n in enumerate(names) if "test_config_c" in n)
+    de = min(i for i, n in enumerate(names) if "test_configs_d_e" in n)
+    assert c < de
