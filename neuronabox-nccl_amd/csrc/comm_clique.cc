@@ -178,6 +178,7 @@ ncclResult_t runCliqueColl(Clique* c, const std::vector<PendingColl>& parts0) {
     for (int j = 0; j < n; j++)
       if (j != r) HIPCHECK(hipStreamWaitEvent(parts[r].stream, c->evDone[j], 0));
     NCCLCHECK(cliqueOrderAfter(c, r, parts[r].stream));
+    if (parts0[r].localPre) NCCLCHECK(preScratchDone(c->comms[r], c->devs[r], parts[r].stream));
   }
   return ncclSuccess;
 }

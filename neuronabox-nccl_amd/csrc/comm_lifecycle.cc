@@ -164,6 +164,10 @@ ncclResult_t commFree(ncclComm* comm) {
     if (comm->preScratch) (void)hipFree(comm->preScratch);
     for (void* p : comm->preScratchOld) (void)hipFree(p);
   }
+  if (comm->preScratchFree) {
+    DevGuard dg(comm->device);
+    (void)hipEventDestroy(comm->preScratchFree);
+  }
   if (c) {
     std::lock_guard<std::mutex> gp(g_pendMu);
     std::lock_guard<std::mutex> g(c->mu);

@@ -192,7 +192,9 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c0) {
     MpCall c = c0;   // after the cross-stream wait: the pre-pass reuses scratch an earlier call read
     if (c.localPre) NCCLCHECK(localPreOp(comm, comm->device, &c, comm->nRanks));
     const MpProto proto = mpProtoOf(comm, c);
-    return proto == kMpSimple ? mpLaunchSimple(comm, &c, 1) : mpLaunchLL(comm, c, proto);
+    NCCLCHECK(proto == kMpSimple ? mpLaunchSimple(comm, &c, 1) : mpLaunchLL(comm, c, proto));
+    // only this rank's kernel reads its scratch (peers see staging / lines)
+    return c0.localPre ? preScratchDone(comm, comm->device, c.stream) : ncclSuccess;
   });
 }
 

@@ -120,6 +120,12 @@ struct ncclComm {
   void* preScratch = nullptr;
   size_t preScratchBytes = 0;
   std::vector<void*> preScratchOld;
+  // recorded (on the call's stream) behind the last call that read preScratch:
+  // after the clique's leave step, every peer's fold of it is complete. The
+  // next pre-pass waits for it, whatever stream either call ran on (ADVICE r5:
+  // a clique without the in-kernel transport has no other cross-stream order)
+  hipEvent_t preScratchFree = nullptr;
+  bool preScratchPending = false;
   ~ncclComm() {
     if (hostWords) (void)hipHostFree(hostWords);
   }
@@ -313,6 +319,7 @@ ncclResult_t runMpColl(ncclComm* comm, const MpCall& c);
 // localPre calls: scratch = this rank's input x its own scalar (one pre-op
 // reduce on c.stream), then *c sums the scratch (op Sum, localPre cleared)
 ncclResult_t localPreOp(ncclComm* comm, int device, PendingColl* c, int nRanks);
+ncclResult_t preScratchDone(ncclComm* comm, int device, hipStream_t stream);
 ncclResult_t runMpGroup(ncclComm* comm);
 ncclResult_t flushMpGroups();
 

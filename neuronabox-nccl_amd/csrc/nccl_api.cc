@@ -207,18 +207,25 @@ ncclResult_t launchOneRank(void* dst, const void* src, size_t count, const nbxDe
 
 
 // localPre (PendingColl): scratch = x * s on c->stream, then the collective
-// sums the scratch. Scratch grows by doubling and is never freed while the
-// communicator lives (an earlier call, possibly on another stream, may still
-// read the old buffer); growing is refused inside a stream capture — one eager
-// call of the size first, as graph capture of NCCL calls expects anyway.
+// sums the scratch. Scratch grows by doubling (the exact size when the doubled
+// allocation fails) and superseded buffers are kept while the communicator
+// lives (an earlier call, possibly on another stream, may still read the old
+// buffer); growing is refused inside a stream capture — one eager call of the
+// size first, as graph capture of NCCL calls expects anyway. The pre-pass
+// first waits for the event recorded behind the last call that read the
+// scratch (preScratchDone): peers' folds of the previous PreMulSum may still
+// read it, on any stream. A captured pre-pass does not wait on that eager
+// event (the graph's own edges order captured calls): a graph holding a
+// PreMulSum must not be replayed while an eager PreMulSum of the same
+// communicator runs (the one scratch buffer is shared).
 ncclResult_t localPreOp(ncclComm* comm, int device, PendingColl* c, int nRanks) {
   const size_t eb = (size_t)typeSize(c->dt);
   const size_t elts = c->kind == kReduceScatter ? c->count * (size_t)nRanks : c->count;
   const size_t bytes = elts * eb;
   DevGuard g(device);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(c->stream, &cap));
   if (comm->preScratchBytes < bytes) {
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    HIPCHECK(hipStreamIsCapturing(c->stream, &cap));
     if (cap != hipStreamCaptureStatusNone) {
       warn("user PreMulSum of %zu bytes inside a stream capture needs its scratch first: run one eager call of "
            "that size on this communicator before capturing", bytes);
@@ -226,10 +233,16 @@ ncclResult_t localPreOp(ncclComm* comm, int device, PendingColl* c, int nRanks) 
     }
     size_t want = std::max<size_t>(bytes, std::max<size_t>(2 * comm->preScratchBytes, 1u << 20));
     void* p = nullptr;
-    HIPCHECK(hipMalloc(&p, want));
+    if (hipMalloc(&p, want) != hipSuccess) {
+      (void)hipGetLastError();
+      want = bytes;   // the doubled size does not fit: the exact one may
+      HIPCHECK(hipMalloc(&p, want));
+    }
     if (comm->preScratch) comm->preScratchOld.push_back(comm->preScratch);
     comm->preScratch = p;
     comm->preScratchBytes = want;
+  } else if (comm->preScratchPending && cap == hipStreamCaptureStatusNone) {
+    HIPCHECK(hipStreamWaitEvent(c->stream, comm->preScratchFree, 0));
   }
   void* dsts[1] = {comm->preScratch};
   const void* srcs[1] = {c->send};
@@ -238,6 +251,20 @@ ncclResult_t localPreOp(ncclComm* comm, int device, PendingColl* c, int nRanks) 
   c->send = comm->preScratch;
   c->op = nbxDevRedOpFull{nbxDevSum, 0, 0};
   c->localPre = false;
+  return ncclSuccess;
+}
+
+// Behind the last reader of the scratch a pre-pass filled (the collective's
+// own kernel, and on a clique every peer's fold: called after the leave step),
+// on that call's stream; eager calls only.
+ncclResult_t preScratchDone(ncclComm* comm, int device, hipStream_t stream) {
+  DevGuard g(device);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIPCHECK(hipStreamIsCapturing(stream, &cap));
+  if (cap != hipStreamCaptureStatusNone) return ncclSuccess;
+  if (comm->preScratchFree == nullptr) HIPCHECK(hipEventCreateWithFlags(&comm->preScratchFree, hipEventDisableTiming));
+  HIPCHECK(hipEventRecord(comm->preScratchFree, stream));
+  comm->preScratchPending = true;
   return ncclSuccess;
 }
 

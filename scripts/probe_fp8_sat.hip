@@ -7,7 +7,10 @@
 // scale 1.0; 1 = HIP's form (fmed3 clamp unless the exponent is all ones, then
 // v_cvt_pk_*); 2 = an unguarded fmed3 clamp, then v_cvt_pk_*; 3 = this
 // build's TyE4M3::narrow / TyE5M2::narrow (satE4M3 / satE5M2, nbx_functors.h);
-// 4 = its pair path, TyE*::narrow2 (satFinite2: packed fma), x in the high byte.
+// 4 = its pair path, TyE*::narrow2 (satFinite2: packed fma), x in the high byte;
+// 5 = v_cvt_pk_{fp8,bf8}_f32 with the VOP3 clamp bit (bit 15) set, hand-encoded:
+// the assembler rejects `clamp` on these opcodes (VERDICT r5 item 5 asks whether
+// the hardware honours it as SATFINITE anyway).
 // The specification is nbx_functors.h f32ToSmallSat. Mismatch classes as
 // probe_fp8_cvt.hip. Not part of the product.
 #include <hip/hip_runtime.h>
@@ -57,6 +60,18 @@ __global__ void probe(Res* r, int mode) {
     } else if (mode == 4) {   // the pair path (narrow2: packed fma), x in the high byte of the word
       hw4 = (TyE4M3::narrow2(1.0f, x, 0u, true) >> 24) & 0xff;
       hw5 = (TyE5M2::narrow2(1.0f, x, 0u, true) >> 24) & 0xff;
+    } else if (mode == 5) {
+      // v1 = x, v2 = 0; v_cvt_pk_fp8_f32 v1, v1, v2 clamp (0xd2a28001 0x00020501), then bf8 (0xd2a3....)
+      uint32_t r4, r5;
+      asm volatile(
+          "v_mov_b32 v1, %2\n\tv_mov_b32 v2, 0\n\ts_nop 1\n\t.long 0xd2a28001, 0x00020501\n\ts_nop 1\n\t"
+          "v_mov_b32 %0, v1\n\tv_mov_b32 v1, %2\n\ts_nop 1\n\t.long 0xd2a38001, 0x00020501\n\ts_nop 1\n\t"
+          "v_mov_b32 %1, v1"
+          : "=&v"(r4), "=&v"(r5)
+          : "v"(x)
+          : "v1", "v2");
+      hw4 = r4 & 0xff;
+      hw5 = r5 & 0xff;
     } else {
       hw4 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(x, 448.f, -448.f), 0.f, 0, false) & 0xff;
       hw5 = (uint32_t)__builtin_amdgcn_cvt_pk_bf8_f32(__builtin_amdgcn_fmed3f(x, 57344.f, -57344.f), 0.f, 0, false) &
@@ -80,11 +95,12 @@ __global__ void probe(Res* r, int mode) {
 int main() {
   Res* d;
   Res h;
-  const char* modes[5] = {"scalef32 scale 1.0", "HIP SATFINITE form (guarded fmed3)", "unguarded fmed3",
+  const char* modes[6] = {"scalef32 scale 1.0", "HIP SATFINITE form (guarded fmed3)", "unguarded fmed3",
                           "this build (satE4M3 / satE5M2 + v_cvt_pk)",
-                          "this build, pair path (narrow2: fmed3 x2 + v_pk_fma_f32)"};
+                          "this build, pair path (narrow2: fmed3 x2 + v_pk_fma_f32)",
+                          "v_cvt_pk with the VOP3 clamp bit (hand-encoded)"};
   const char* names[6] = {"nan-in", "inf-in", "overflow", "f32-denormal", "below-min-normal", "normal"};
-  for (int mode = 0; mode < 5; mode++) {
+  for (int mode = 0; mode < 6; mode++) {
     if (hipMalloc(&d, sizeof(Res)) != hipSuccess) return 2;
     if (hipMemset(d, 0, sizeof(Res)) != hipSuccess) return 2;
     probe<<<4096, 256>>>(d, mode);

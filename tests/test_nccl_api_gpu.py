@@ -202,6 +202,47 @@ def test_clique_counts_past_32_bits(nbx, torch_gpu):
             c.destroy()
 
 
+def test_clique_user_premulsum_alternating_streams_no_sync(nbx, oracle, torch_gpu):
+    """back-to-back per-rank PreMulSum AllReduces on a clique,
+    alternating each rank's stream between two streams with no host sync. Each
+    call's pre-pass rewrites the rank's one scratch buffer, which the peers'
+    folds of the previous call (on the other stream) read in place: the pre-pass
+    must wait for them (preScratchFree). 64 MiB per rank keeps the calls on the
+    fold path; every output is checked bit-exact."""
+    torch = torch_gpu
+    nranks, count, calls = 3, 16 << 20, 4
+    scal = (0.5, -1.25, 3.0)
+    comms = nbx.Communicator.init_all([0] * nranks)
+    streams = [[torch.cuda.Stream() for _ in range(2)] for _ in range(nranks)]
+    try:
+        hs = [np.array([s_], np.float32).view(np.uint32) for s_ in scal]
+        ops = [comms[r].redop_create_premulsum(hs[r].ctypes.data, F32) for r in range(nranks)]
+        ins, outs = [], []
+        for k in range(calls):
+            xs = oracle.random_inputs(F32, nranks, count, seed=300 + k)
+            ins.append((xs, [t_of(torch, x) for x in xs]))
+            outs.append([torch.zeros(count * 4, dtype=torch.uint8, device="cuda") for _ in range(nranks)])
+        torch.cuda.synchronize()
+        for k in range(calls):
+            nbx.group_start()
+            for r in range(nranks):
+                comms[r].all_reduce(ins[k][1][r].data_ptr(), outs[k][r].data_ptr(), count, F32, ops[r],
+                                    streams[r][k % 2].cuda_stream)
+            nbx.group_end()
+        torch.cuda.synchronize()
+        for r in range(nranks):
+            comms[r].redop_destroy(ops[r])
+        for k in range(calls):
+            xs = ins[k][0]
+            scaled = [oracle.reduce_multi([xs[r]], F32, 3, int(hs[r][0]), n_pre_op_srcs=1)[0] for r in range(nranks)]
+            exp = _ring_order_reduce(oracle, scaled, F32, 0, 0, False, nranks, _blocks(count, 4, nranks))
+            for r in range(nranks):
+                assert np.array_equal(outs[k][r].cpu().numpy(), np.ascontiguousarray(exp).view(np.uint8)), (k, r)
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def test_clique_user_premulsum_per_rank_scalars(nbx, oracle, torch_gpu):
     """A 3-rank clique with a different PreMulSum scalar per rank: sum_r s_r x_r
     (the reference's per-rank pre-op), AllReduce / ReduceScatter / Reduce on
