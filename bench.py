@@ -688,6 +688,13 @@ def collective_leg(child, world: int, rank: int, result_timeout: float = 400.0, 
     act = [r.get("ll128_active") for r in allres]
     out["ll128_active"] = None if any(a is None for a in act) else all(act)
     out["hbm_model"] = simple_hbm_model(world, S)
+    # LL_CASES back to back on the default protocols, every output exact
+    ms = [r.get("mixed_seq_mismatches") for r in allres]
+    mc = [r.get("mixed_seq_checked_calls") for r in allres]
+    out["mixed_seq"] = None if any(v is None for v in ms + mc) else {
+        "checked_calls": sum(mc), "mismatches_per_rank": ms,
+        "what": "tests' LL_CASES (LL / LL128 / Simple sizes, misaligned offsets) issued back to back without host "
+                "sync, 3 iterations, max / min on full-range values, sums on small integers: exact on the GPU"}
     out["transport_allreduce"] = agg("transport_allreduce_ms", 2 * (world - 1) / world, S)
     add_hbm_rates(out, world, S)
     add_fabric_rates(out, allres, world, S)

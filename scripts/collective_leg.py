@@ -235,6 +235,146 @@ def ll128_stress(c, rank, world, st, res):
     res["ll128_forced_mismatched_calls"] = bad
 
 
+# tests/test_multiprocess_gpu.py LL_CASES (kept equal by tests/test_tools_cpu.py):
+# (kind, ncclDataType, op, count, byte offset of send / recv). GPUTEST_r05 saw
+# this sequence, issued back to back on the default protocols, return wrong
+# data from the Simple direct path at 8 ranks sharing one GPU (case 36); the
+# node run replays it across the fabric.
+MIXED_CASES = [
+    ("ar", 7, 0, 1, 0), ("ar", 7, 0, 3, 0), ("ar", 7, 0, 1000, 0), ("ar", 7, 0, 16384, 0), ("ar", 6, 0, 17, 0),
+    ("ar", 9, 4, 4097, 0), ("ar", 2, 4, 999, 0), ("ar", 4, 2, 4096, 0), ("ar", 10, 0, 33, 0),
+    ("ar", 1, 3, 65536, 0), ("ar", 8, 1, 8191, 0), ("ar", 7, 0, 40000, 0), ("ar", 7, 0, 1001, 4),
+    ("ar", 0, 0, 77, 3), ("rs", 7, 0, 1000, 0), ("rs", 6, 4, 333, 2), ("rs", 0, 2, 5, 1), ("rs", 4, 4, 4096, 0),
+    ("rs", 7, 0, 20000, 0), ("red", 7, 0, 1000, 0), ("red", 9, 4, 777, 0), ("red", 2, 3, 64, 0),
+    ("red", 7, 0, 123, 4), ("red", 7, 1, 4096, 0), ("ar", 7, 0, 64, 0),
+    ("ar", 7, 0, 50003, 0), ("ar", 6, 4, 77777, 2), ("ar", 4, 2, 30000, 8), ("rs", 7, 0, 30001, 4),
+    ("rs", 2, 2, 131072, 0), ("red", 7, 0, 99999, 0), ("red", 8, 4, 100000, 8),
+    ("ar", 7, 4, 262144, 0), ("ar", 9, 0, 300001, 0), ("ar", 11, 0, 600001, 1), ("ar", 7, 0, 300000, 4),
+    ("ar", 2, 2, 1000003, 0), ("ar", 8, 0, 200001, 0), ("red", 7, 0, 300001, 0), ("red", 9, 4, 200003, 2),
+    ("red", 2, 3, 500000, 0),
+    ("ar", 7, 0, 1100000, 0), ("rs", 7, 4, 1048577, 0),
+]
+MIXED_ITERS = 3
+_EB = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
+
+
+def _mixed_op(op):
+    """The leg's op for a case: max / min kept, everything else a sum of small
+    integers (Prod -> max) — every fold order then gives the same bits, so a
+    GPU restatement checks the output exactly; the kinds, types, sizes and
+    offsets (hence protocols, grids and staging slices) are the case's own."""
+    return op if op in (2, 3) else (2 if op == 1 else 0)
+
+
+def _mixed_input(torch, dt, op, total, seed, device="cuda"):
+    """Raw bytes of one rank's input: full-range values for max / min (finite
+    floats, no zeros or NaN codes for fp8), small integers for sums."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    if op == 0:
+        v = torch.randint(0, 16 if dt not in (10, 11) else 2, (total,), generator=g, device=device)
+        if dt in (10, 11):
+            return v.to(torch.float32).to(torch.float8_e4m3fn if dt == 10 else torch.float8_e5m2).view(torch.uint8)
+        tdt = {0: torch.int8, 1: torch.uint8, 2: torch.int32, 3: torch.int32, 4: torch.int64, 5: torch.int64,
+               6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.bfloat16}[dt]
+        return v.to(tdt).view(torch.uint8)
+    if dt in (6, 7, 8, 9):
+        f = torch.randn(total, generator=g, device=device, dtype=torch.float64) * 1000
+        return f.to({6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.bfloat16}[dt]).view(torch.uint8)
+    c = torch.randint(0, 256, (total * _EB[dt],), generator=g, device=device, dtype=torch.int64).to(torch.uint8)
+    if dt == 10:
+        c[((c & 0x7f) == 0x7f) | (c == 0x80)] = 0x01
+    elif dt == 11:
+        c[((c & 0x7c) == 0x7c) | (c == 0x80)] = 0x01
+    return c
+
+
+def _mixed_expected(torch, dt, op, ins):
+    """The exact result of the leg's op over every rank's raw input bytes."""
+    if op == 0:
+        if dt in (10, 11):
+            f8 = torch.float8_e4m3fn if dt == 10 else torch.float8_e5m2
+            return sum(x.view(f8).float() for x in ins).to(f8).view(torch.uint8)
+        if dt in (6, 7, 8, 9):
+            tdt = {6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.bfloat16}[dt]
+            return sum(x.view(tdt).double() for x in ins).to(tdt).view(torch.uint8)
+        tdt = {0: torch.int8, 1: torch.uint8, 2: torch.int32, 3: torch.int32, 4: torch.int64, 5: torch.int64}[dt]
+        return sum(x.view(tdt).to(torch.int64) for x in ins).to(tdt).view(torch.uint8)
+    pick = torch.maximum if op == 2 else torch.minimum
+    if dt in (10, 11):
+        f8 = torch.float8_e4m3fn if dt == 10 else torch.float8_e5m2
+        acc = ins[0].view(f8).float()
+        for x in ins[1:]:
+            acc = pick(acc, x.view(f8).float())
+        return acc.to(f8).view(torch.uint8)
+    if dt in (6, 7, 8, 9):
+        tdt = {6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.bfloat16}[dt]
+        acc = ins[0].view(tdt).double()
+        for x in ins[1:]:
+            acc = pick(acc, x.view(tdt).double())
+        return acc.to(tdt).view(torch.uint8)
+    tdt = {0: torch.int8, 1: torch.uint8, 2: torch.int32, 3: torch.int32, 4: torch.int64, 5: torch.int64}[dt]
+    flip = {3: -(1 << 31), 5: -(1 << 63)}.get(dt)   # unsigned: compare with the sign bit flipped
+    vs = [x.view(tdt) if flip is None else (x.view(tdt) ^ flip) for x in ins]
+    acc = vs[0]
+    for v in vs[1:]:
+        acc = pick(acc, v)
+    return (acc if flip is None else acc ^ flip).view(torch.uint8)
+
+
+def mixed_sequence(comm, rank, world, st, res, iters=MIXED_ITERS):
+    """MIXED_CASES back to back on the default protocols (no host sync between
+    calls, inputs new every iteration, every rank's input regenerated on each
+    rank from its seed), every output checked exactly on the GPU; per-rank
+    counts of checked and wrong calls, and the first wrong call described."""
+    import torch
+    checked = bad = 0
+    first = None
+    for it in range(iters):
+        keep = []
+        for i, (kind, dt, op0, count, shift) in enumerate(MIXED_CASES):
+            op = _mixed_op(op0)
+            eb = _EB[dt]
+            total = count * world if kind == "rs" else count
+            x = _mixed_input(torch, dt, op, total, 50000 * it + 100 * i + rank)
+            tx = torch.zeros(total * eb + 16, dtype=torch.uint8, device="cuda")
+            tx[shift:shift + total * eb] = x
+            out_b = count * eb
+            ty = torch.full((out_b + 16,), 0xA5, dtype=torch.uint8, device="cuda")
+            root = (i * 3 + 1) % world
+            sp, rp = tx.data_ptr() + shift, ty.data_ptr() + shift
+            if kind == "ar":
+                comm.all_reduce(sp, rp, count, dt, op, st)
+            elif kind == "rs":
+                comm.reduce_scatter(sp, rp, count, dt, op, st)
+            else:
+                comm.reduce(sp, rp, count, dt, op, root, st)
+            keep.append((i, kind, dt, op, count, shift, root, tx, ty))
+        torch.cuda.synchronize()
+        for i, kind, dt, op, count, shift, root, tx, ty in keep:
+            if kind == "red" and rank != root:
+                continue
+            eb = _EB[dt]
+            total = count * world if kind == "rs" else count
+            ins = [_mixed_input(torch, dt, op, total, 50000 * it + 100 * i + r) for r in range(world)]
+            want = _mixed_expected(torch, dt, op, ins)
+            if kind == "rs":
+                want = want[rank * count * eb:(rank + 1) * count * eb]
+            got = ty[shift:shift + count * eb]
+            checked += 1
+            if not torch.equal(got, want):
+                bad += 1
+                if first is None:
+                    w = (got.view(-1, eb) != want.view(-1, eb)).any(dim=1).nonzero().flatten()
+                    first = (f"iteration {it} case {i} {MIXED_CASES[i]} (leg op {op}): {w.numel()} of {count} "
+                             f"elements wrong, first {int(w[0])} last {int(w[-1])}")
+        del keep
+    res["mixed_seq_checked_calls"] = checked
+    res["mixed_seq_mismatches"] = bad
+    if bad:
+        res["ok"] = False
+        res["errors"].append(f"mixed sequence: {bad} of {checked} calls wrong; {first}")
+
+
 LINK_PROBE_BYTES = 256 << 20   # per peer per launch
 
 
@@ -376,6 +516,8 @@ def run(ids, rank, world, dev):
     res["simple_stress_checked_calls"] = 2 * SIMPLE_STRESS_ITERS
     del xs_, es_, ys_
     _progress("config D done", res)
+    mixed_sequence(comm, rank, world, st, res)
+    _progress("mixed sequence done", res)
     # 1 MiB on the default protocol set (LL128 on one GPU; across GPUs LL128
     # is off by default, so Simple carries it there): exact on every one of
     # LL128_ITERS calls with inputs that change per call (a torn line or a

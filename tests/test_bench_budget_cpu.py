@@ -39,7 +39,8 @@ for line in sys.stdin:
                                       "simple_knobs_ms": {"slice256K": 9.0 + rank, "grid64": 12.0, "slots4": 10.0},
                                       "curve_allreduce_ms": [1.0 + rank, 3.0],
                                       "ipc_repairs": {"direct": rank, "ring": 0},
-                                      "ll128_forced_checked_calls": 2000, "ll128_forced_mismatched_calls": 0}),
+                                      "ll128_forced_checked_calls": 2000, "ll128_forced_mismatched_calls": 0,
+                                      "mixed_seq_checked_calls": 120 + rank, "mixed_seq_mismatches": rank}),
               flush=True)
         break
 '''
@@ -168,6 +169,7 @@ def test_legs_finish_normally_inside_the_budget(tmp_path):
     assert coll["rccl"] is None            # gloo: no RCCL leg
     assert coll["ipc_repairs"] == {"direct": 1, "ring": 0}
     assert coll["ll128_forced"]["checked_calls"] == 4000 and coll["ll128_forced"]["mismatched_calls"] == 0
+    assert coll["mixed_seq"]["checked_calls"] == 241 and coll["mixed_seq"]["mismatches_per_rank"] == [0, 1]
     tr = coll["transport_allreduce"]
     S = bench.COUNT_D * 4
     assert tr["ms"] == 6.0

@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MARKER = "void nbx::kReducePacks<nbx::FnSumF<nbx::TyF32>, 3, 1>(nbx::KArgs)"
 K16 = "void nbx::kReducePacks<nbx::FnSumF<nbx::TyF16>, 2, 1>(nbx::KArgs)"
@@ -145,3 +147,53 @@ def test_set_thresholds_on_the_r5_rehearsal_with_knobs():
     env = r["env"]
     assert env["NBX_SIMPLE_SLICE_BYTES"] == "" and env["NBX_SIMPLE_MAX_GRID"] == "" and env["NBX_SIMPLE_SLOTS"] == ""
     assert env["NBX_LL128_ACROSS_GPUS"] == ""   # ranks shared one GPU
+
+
+def test_collective_leg_mixed_cases_match_the_gpu_test_and_check_exactly():
+    """scripts/collective_leg.py replays the GPU suite's LL_CASES on the node
+    (VERDICT r5 item 4): the same list, and its torch restatement is exact for
+    every case's leg op (on the CPU here: inputs, the expected result, and a
+    wrong element detected)."""
+    import importlib.util
+    import torch
+    from tests.test_multiprocess_gpu import LL_CASES
+    spec = importlib.util.spec_from_file_location("collective_leg", os.path.join(ROOT, "scripts", "collective_leg.py"))
+    leg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(leg)
+    assert leg.MIXED_CASES == LL_CASES
+    world = 3
+    for i, (kind, dt, op0, count, shift) in enumerate(leg.MIXED_CASES):
+        op = leg._mixed_op(op0)
+        assert op in (0, 2, 3)
+        total = min(count * world if kind == "rs" else count, 5000)
+        ins = [leg._mixed_input(torch, dt, op, total, 100 * i + r, device="cpu") for r in range(world)]
+        assert all(x.dtype == torch.uint8 and x.numel() == total * leg._EB[dt] for x in ins)
+        want = leg._mixed_expected(torch, dt, op, ins)
+        assert want.numel() == total * leg._EB[dt]
+        # the restatement against a plain reference on a few elements
+        ref = _plain_fold(np, dt, op, [x.numpy() for x in ins])
+        assert np.array_equal(want.numpy(), ref), (i, dt, op)
+
+
+def _plain_fold(np_, dt, op, ins):
+    """numpy reference of the leg's op on raw bytes (floats through float64;
+    fp8 through the oracle's decoders)."""
+    from oracle import oracle as o
+    st = {0: np_.int8, 1: np_.uint8, 2: np_.int32, 3: np_.uint32, 4: np_.int64, 5: np_.uint64, 6: np_.float16,
+          7: np_.float32, 8: np_.float64}
+    if dt in (10, 11):
+        dec = o.e4m3_to_f32 if dt == 10 else o.e5m2_to_f32
+        enc = o.f32_to_e4m3 if dt == 10 else o.f32_to_e5m2
+        vals = [np_.array([dec(int(c)) for c in x], dtype=np_.float64) for x in ins]
+        acc = sum(vals) if op == 0 else (np_.maximum.reduce(vals) if op == 2 else np_.minimum.reduce(vals))
+        return np_.array([enc(float(v)) for v in acc], dtype=np_.uint8)
+    if dt == 9:
+        vals = [(x.view(np_.uint16).astype(np_.uint32) << 16).view(np_.float32).astype(np_.float64) for x in ins]
+        acc = sum(vals) if op == 0 else (np_.maximum.reduce(vals) if op == 2 else np_.minimum.reduce(vals))
+        return np_.array([o.f32_to_bf16(float(v)) for v in acc], dtype=np_.uint16).view(np_.uint8)
+    vals = [x.view(st[dt]) for x in ins]
+    if op == 0:
+        acc = sum(v.astype(np_.float64) if dt in (6, 7, 8) else v.astype(np_.int64) for v in vals)
+        return acc.astype(st[dt]).view(np_.uint8)
+    f = np_.maximum if op == 2 else np_.minimum
+    return f.reduce(vals).view(np_.uint8)
