@@ -62,7 +62,7 @@ def _expected(oracle, case, i, n):
     return exp, xs
 
 
-def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q):
+def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=False):
     try:
         import random
 
@@ -100,6 +100,8 @@ def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q):
                 sp, rp = tx.data_ptr() + shift, ty.data_ptr() + shift
                 if jitter and rng.random() < 0.3:
                     time.sleep(rng.random() * 0.004)
+                if skew and rng.random() < 0.02:   # a rank stalls (first-launch code loading on a fresh box)
+                    time.sleep(0.05 + rng.random() * 0.2)
                 if kind == "ar":
                     comm.all_reduce(sp, rp, count, dtype, op, st)
                 elif kind == "rs":
@@ -116,66 +118,33 @@ def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q):
                 if not np.array_equal(got, exp[i]):
                     bad.append({"it": it, "case": i, "got": got, "prev": prev.get(i)})
                 prev[i] = got
-            if time.time() - t0 > 60 * (it + 1) / max(iters, 1) + 120:
-                break
+            del keep
+            if rank == 0 and (it % 5 == 0 or it == iters - 1):   # progress (a silent GPU run is taken for hung)
+                print(f"[repro] iteration {it + 1}/{iters}, {time.time() - t0:.1f} s, rank 0 bad calls {len(bad)}",
+                      file=sys.stderr, flush=True)
+            if fresh:   # every buffer a fresh allocation next iteration (as iteration 0 of the GPU test)
+                torch.cuda.empty_cache()
         err = comm.async_error()
         comm.destroy()
         q.put((rank, "ok", {"bad": bad, "calls": calls, "async_error": err, "settings": settings,
-                            "s": time.time() - t0}))
+                            "s": time.time() - t0, "iters_done": it + 1}))
     except Exception:
         import traceback
         q.put((rank, "error", traceback.format_exc()))
 
 
 def comm_settings(nbx, comm):
-    import ctypes
-    lib = nbx.load_library()
-    out = (ctypes.c_int64 * 10)()
-    k = lib.nbxDebugCommSettings(comm.handle, out, 10)
-    names = ["llMax", "l128Max", "sliceBytes", "slots", "simpleGrid", "llGridCap", "l128GridCap", "groupBatch",
-             "ipcRepairs", "checkPlans"]
-    return {names[j]: int(out[j]) for j in range(max(k, 0))}
+    from tests import mp_diag
+    return mp_diag.comm_settings(nbx, comm)
 
 
 def diagnose(oracle, n, case_id, rank, got_u8, prev_u8, settings):
-    import numpy as np
     from tests import mp_diag
-    cases = _cases()
-    kind, dtype, op, count, _ = cases[case_id]
-    exp, xs = _expected(oracle, cases[case_id], case_id, n)
-    st = oracle.NP_STORAGE[dtype]
-    eb = np.dtype(st).itemsize
-    e = np.ascontiguousarray(exp[rank])
-    got = got_u8.view(st)
-    base = rank * count if kind == "rs" else 0
-    cand = {}
-    devop, arg = oracle.host_to_dev_redop(op, dtype, n)
-    kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
-    # raw inputs of every rank (send side, at the output's positions)
-    for j in range(n):
-        cand[f"raw_input_rank{j}"] = np.ascontiguousarray(xs[j][base:base + e.size])
-    # the fold with one rank's source left out (AllReduce / ReduceScatter blocks in rank order b+1, ..., b)
-    if kind in ("ar", "rs") and n > 1:
-        from tests.test_multiprocess_gpu import _blocks
-        blocks = _blocks(count, eb, n) if kind == "ar" else [(b * count, (b + 1) * count) for b in range(n)]
-        for j in range(n):
-            alt = np.empty(e.size, dtype=st)
-            for b, (lo, hi) in enumerate(blocks):
-                olo, ohi = lo - base, hi - base
-                if ohi <= 0 or olo >= e.size or hi <= lo:
-                    continue
-                order = [(b + 1 + k) % n for k in range(n) if (b + 1 + k) % n != j]
-                alt[olo:ohi] = oracle.reduce_multi([xs[q][lo:hi] for q in order], dtype, devop, arg, **kw)[0]
-            cand[f"without_rank{j}"] = alt
-    if prev_u8 is not None and prev_u8.size == got_u8.size:
-        cand["prev_iteration_output"] = prev_u8.view(st)
-    geom = None
-    if settings:
-        geom = mp_diag.simple_geometry(kind, count, eb, n, settings.get("simpleGrid", 32),
-                                       settings.get("sliceBytes", 65536))
-    d = mp_diag.describe_mismatch(got, e, geom, base, cand)
-    d["explained_by"] = {k: v for k, v in d.get("explained_by", {}).items() if v}
-    return d
+    from tests.test_multiprocess_gpu import _ll_input, _ll_root
+    kind, dtype, op, count, _ = _cases()[case_id]
+    xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
+    return mp_diag.diagnose_collective(oracle, kind, dtype, op, count, n, rank, got_u8, xs, settings, prev_u8,
+                                       root=_ll_root(case_id, n))
 
 
 def main():
@@ -184,6 +153,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--cases", default="0:41")
     ap.add_argument("--jitter", action="store_true")
+    ap.add_argument("--fresh", action="store_true", help="torch.cuda.empty_cache() after every iteration")
+    ap.add_argument("--skew", action="store_true", help="ranks stall 50-250 ms now and then")
     args = ap.parse_args()
     lo, hi = (int(x) for x in args.cases.split(":"))
     case_ids = list(range(lo, min(hi, len(_cases()))))
@@ -199,14 +170,24 @@ def main():
     uid = nbx.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=rank_main, args=(bytes(uid), r, n, args.iters, case_ids, args.jitter, q), daemon=True)
+    procs = [ctx.Process(target=rank_main, args=(bytes(uid), r, n, args.iters, case_ids, args.jitter, q, args.fresh,
+                                                     args.skew), daemon=True)
              for r in range(n)]
     for p in procs:
         p.start()
     res, errors = {}, []
+    import queue as _queue
+    t_start = time.time()
     try:
         for _ in range(n):
-            rank, status, payload = q.get(timeout=600)
+            while True:   # a heartbeat every 30 s (a fresh box's first torch import takes minutes)
+                try:
+                    rank, status, payload = q.get(timeout=30)
+                    break
+                except _queue.Empty:
+                    print(f"[repro] waiting for the ranks, {time.time() - t_start:.0f} s", file=sys.stderr, flush=True)
+                    if time.time() - t_start > 900:
+                        raise
             if status != "ok":
                 errors.append({"rank": rank, "error": payload[-3000:]})
             else:
@@ -222,7 +203,8 @@ def main():
         for b in pl["bad"][:6]:
             d = diagnose(oracle, n, b["case"], r, b["got"], b["prev"], pl["settings"])
             mism.append({"rank": r, "it": b["it"], "case": b["case"], "call": list(_cases()[b["case"]]), **d})
-    out = {"ranks": n, "iters": args.iters, "cases": args.cases, "jitter": args.jitter,
+    out = {"ranks": n, "iters": args.iters, "cases": args.cases, "jitter": args.jitter, "fresh": args.fresh,
+           "skew": args.skew, "iters_done": {r: pl.get("iters_done") for r, pl in res.items()},
            "env": {k: v for k, v in os.environ.items() if k.startswith(("NBX_", "NCCL_"))},
            "calls": sum(pl["calls"] for pl in res.values()),
            "bad_calls": sum(len(pl["bad"]) for pl in res.values()),

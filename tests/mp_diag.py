@@ -137,6 +137,8 @@ def format_mismatch(d: dict) -> str:
     if d.get("n_wrong") is None:
         return f"shape/dtype differ: {d}"
     s = [f"{d['n_wrong']} of {d['n']} elements wrong"]
+    if d.get("proto"):
+        s[0] = f"{d['proto']}: " + s[0]
     if d["n_wrong"]:
         s.append(f"first {d['first']} last {d['last']} runs {d['runs']}")
         s.append("explained by " + ", ".join(f"{k}={v}" for k, v in d["explained_by"].items()))
@@ -157,3 +159,124 @@ def assert_same(got: np.ndarray, exp: np.ndarray, ctx, geom: SimpleGeometry | No
     if got.shape == exp.shape and got.dtype == exp.dtype and np.array_equal(got.view(np.uint8), exp.view(np.uint8)):
         return
     raise AssertionError(f"{ctx}: " + format_mismatch(describe_mismatch(got, exp, geom, base, candidates)))
+
+
+# ---------------------------------------------------------------------------
+# Collective-level diagnosis (the multi-process tests and scripts/mixed_seq_repro.py)
+
+L128_DATA_BYTES = 48   # nbx_ll_args.h kL128DataBytesHost
+L128_MAX_RANKS = 8
+
+
+def l128_slot_lines(max_bytes: int) -> int:
+    half = (max_bytes + 1) // 2
+    return 2 * (-(-half // L128_DATA_BYTES))
+
+
+def proto_of(kind: str, count: int, eb: int, n: int, settings: dict, proto_mask: int = 7,
+             oneshot_max: int = 256 << 10) -> str:
+    """The protocol a call takes (comm_mp_init.cc chooseProtoFor), for the
+    description: "LL", "LL128", "LL128x2" or "Simple"."""
+    slot = count * eb
+    lo, hi = block_range(count, eb, n, 0)
+    block = (hi - lo) * eb
+    ll_max, l128_max = settings.get("llMax", 64 << 10), settings.get("l128Max", 1 << 20)
+    if slot == 0 or n > 64:
+        return "Simple"
+    if proto_mask & 1 and slot <= ll_max:
+        return "LL"
+    if proto_mask & 2 and l128_max and n <= L128_MAX_RANKS:
+        if kind == "rs" or n <= 2 or slot <= oneshot_max:
+            if slot <= l128_max:
+                return "LL128"
+        elif slot <= l128_max and block <= (l128_slot_lines(l128_max) // 2) * L128_DATA_BYTES:
+            return "LL128x2"
+    return "Simple"
+
+
+def diagnose_collective(oracle, kind: str, dtype: int, op: int, count: int, n: int, rank: int, got_u8, xs,
+                        settings: dict | None = None, prev_u8=None, root: int | None = None) -> dict:
+    """Describe rank `rank`'s wrong output of one multi-process collective.
+
+    xs: every rank's raw send buffer (oracle storage dtype, send-side length);
+    kind "ar" / "rs" / "red" (Reduce: the root's output, fold order root+1,
+    ..., root). Candidates: zero, each rank's raw input at the output's
+    positions, the fold with one rank's source left out (per block, in the
+    direct schedule's order), and `prev_u8` (this buffer position's output of
+    an earlier iteration). The Simple cut is added when the call took Simple."""
+    import numpy as np
+    st = oracle.NP_STORAGE[dtype]
+    eb = np.dtype(st).itemsize
+    devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+    kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+    if kind == "ar":
+        blocks = [block_range(count, eb, n, b) for b in range(n)]
+        firsts = [(b + 1) % n for b in range(n)]
+        base, out_n = 0, count
+    elif kind == "rs":
+        blocks = [(b * count, (b + 1) * count) for b in range(n)]
+        firsts = [(b + 1) % n for b in range(n)]
+        base, out_n = rank * count, count
+    else:
+        blocks = [(0, count)]
+        firsts = [((root if root is not None else 0) + 1) % n]
+        base, out_n = 0, count
+
+    def fold(skip=None):
+        out = np.empty(out_n, dtype=st)
+        for (lo, hi), first in zip(blocks, firsts):
+            olo, ohi = max(lo - base, 0), min(hi - base, out_n)
+            if ohi <= olo:
+                continue
+            order = [(first + k) % n for k in range(n) if (first + k) % n != skip]
+            if not order:
+                out[olo:ohi] = 0
+                continue
+            out[olo:ohi] = oracle.reduce_multi([xs[q][olo + base:ohi + base] for q in order], dtype, devop, arg,
+                                               **kw)[0]
+        return out
+
+    exp = fold()
+    got = np.ascontiguousarray(got_u8).view(np.uint8)[:out_n * eb].view(st)
+    cand = {f"raw_input_rank{j}": np.ascontiguousarray(xs[j][base:base + out_n]) for j in range(n)}
+    if n > 1:
+        for j in range(n):
+            cand[f"without_rank{j}"] = fold(skip=j)
+    if prev_u8 is not None and np.asarray(prev_u8).size == got.size * eb:
+        cand["earlier_iteration_output"] = np.ascontiguousarray(prev_u8).view(st)
+    proto = proto_of(kind, count, eb, n, settings or {})
+    geom = None
+    if proto == "Simple" and settings:
+        geom = simple_geometry(kind, count, eb, n, settings.get("simpleGrid", 32), settings.get("sliceBytes", 64 << 10),
+                               ring=bool(settings.get("ring")))
+    d = describe_mismatch(got, exp, geom, base, cand)
+    d["proto"] = proto
+    if "explained_by" in d:
+        d["explained_by"] = {k: v for k, v in d["explained_by"].items() if v}
+    return d
+
+
+def comm_settings(nbx, comm) -> dict:
+    """The communicator's transport settings (nbxDebugCommSettings) by name."""
+    import ctypes
+    lib = nbx.load_library()
+    out = (ctypes.c_int64 * 10)()
+    k = lib.nbxDebugCommSettings(comm.handle, out, 10)
+    names = ["llMax", "l128Max", "sliceBytes", "slots", "simpleGrid", "llGridCap", "l128GridCap", "groupBatch",
+             "ipcRepairs", "checkPlans"]
+    return {names[j]: int(out[j]) for j in range(max(k, 0))}
+
+
+def raise_collective_failures(oracle, failures, n, what="") -> None:
+    """failures: (label, kind, dtype, op, count, rank, got_u8, xs, settings, root)
+    tuples; raises one AssertionError that describes up to six of them."""
+    if not failures:
+        return
+    lines = []
+    for (label, kind, dtype, op, count, rank, got, xs, settings, root) in failures[:6]:
+        try:
+            d = diagnose_collective(oracle, kind, dtype, op, count, n, rank, got, xs, settings, root=root)
+            lines.append(f"{label} rank {rank}: {format_mismatch(d)}")
+        except Exception as e:   # the description must never hide the failure itself
+            lines.append(f"{label} rank {rank}: wrong output (diagnosis failed: {type(e).__name__}: {e})")
+    raise AssertionError(f"{what}{len(failures)} wrong output(s) at {n} ranks:\n" + "\n".join(lines))

@@ -106,3 +106,61 @@ def test_gpu_suite_runs_single_gpu_core_first():
     c = max(i for i, n in enumerate(names) if "test_config_c" in n)
     de = min(i for i, n in enumerate(names) if "test_configs_d_e" in n)
     assert c < de
+
+
+def test_diagnose_collective_names_the_missing_source_and_cell():
+    """GPUTEST_r05's case as a synthetic failure: 8 ranks, int32 max over
+    1,000,003 elements (Simple direct at the shared-GPU grid of 32); rank 0's
+    output has one workgroup's slice of block 6 folded without rank 3's source.
+    The description names the protocol, the cell and the missing source."""
+    from oracle import oracle
+    oracle.build()
+    n, count = 8, 1000003
+    xs = oracle.random_inputs(2, 8, count, seed=77 + 2 + count)
+    devop, arg = oracle.host_to_dev_redop(2, 2, n)
+    settings = {"llMax": 64 << 10, "l128Max": 1 << 20, "sliceBytes": 64 << 10, "simpleGrid": 32}
+    full = np.empty(count, dtype=np.int32)
+    for b in range(n):
+        lo, hi = mp_diag.block_range(count, 4, n, b)
+        order = [(b + 1 + k) % n for k in range(n)]
+        full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], 2, devop, arg, n_pre_op_srcs=n)[0]
+    lo = 6 * 125004 + 9 * 3908
+    idx = np.arange(lo, lo + 3908)
+    without3 = np.maximum.reduce([xs[j][idx] for j in range(n) if j != 3])
+    got = full.copy()
+    got[idx] = without3
+    changed = int((without3 != full[idx]).sum())
+    assert changed > 0
+    d = mp_diag.diagnose_collective(oracle, "ar", 2, 2, count, n, 0, got.view(np.uint8), xs, settings)
+    assert d["proto"] == "Simple" and d["n_wrong"] == changed
+    assert d["explained_by"]["without_rank3"] == changed
+    assert [(c["block"], c["round"], c["workgroup"]) for c in d["cells"]] == [(6, 0, 9)]
+    with pytest.raises(AssertionError, match=r"without_rank3=.*\(block, round, workgroup\)"):
+        mp_diag.raise_collective_failures(oracle, [("case 36", "ar", 2, 2, count, 0, got.view(np.uint8), xs,
+                                                    settings, 1)], n)
+    # protocol choice as comm_mp_init.cc chooseProtoFor at these settings
+    assert mp_diag.proto_of("ar", 1000, 4, 8, settings) == "LL"
+    assert mp_diag.proto_of("ar", 50003, 4, 8, settings) == "LL128"
+    assert mp_diag.proto_of("ar", 262144, 4, 8, settings) == "LL128x2"
+    assert mp_diag.proto_of("ar", 300000, 4, 8, settings) == "Simple"
+    assert mp_diag.proto_of("rs", 131072, 4, 8, settings) == "LL128"
+
+
+def test_proto_of_matches_the_library():
+    """mp_diag.proto_of restates comm_mp_init.cc chooseProtoFor: checked
+    against the library's own (nbxDebugChooseProto) over sizes, kinds, ranks."""
+    import ctypes
+    from tests.conftest import load_package
+    lib = load_package().load_library()
+    lib.nbxDebugChooseProto.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                        ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+    names = {0: "LL", 1: "LL128", 2: "Simple", 3: "LL128x2"}
+    settings = {"llMax": 64 << 10, "l128Max": 1 << 20}
+    for n in (2, 3, 5, 8, 9):
+        for kind in ("ar", "rs", "red"):
+            for eb in (1, 2, 4, 8):
+                for count in (1, 17, 4097, 16384, 50003, 65537, 200001, 262144, 300001, 1000003):
+                    lo, hi = mp_diag.block_range(count, eb, n, 0)
+                    lib_p = lib.nbxDebugChooseProto(7, int(kind != "rs"), count * eb, (hi - lo) * eb, n, 64 << 10,
+                                                    1 << 20, 256 << 10)
+                    assert mp_diag.proto_of(kind, count, eb, n, settings) == names[lib_p], (n, kind, eb, count)

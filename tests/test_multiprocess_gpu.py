@@ -9,6 +9,8 @@ import multiprocessing as mp
 import numpy as np
 import pytest
 
+from tests import mp_diag
+
 pytestmark = pytest.mark.gpu
 
 CASES = [  # (kind, dtype, op)
@@ -40,7 +42,7 @@ def _child(uid_bytes, rank, n, q, grouped=False):
         comm = nbx.Communicator.init_rank(n, uid, rank)
         assert comm.count() == n and comm.user_rank() == rank
         st = torch.cuda.Stream()
-        out = {}
+        out = {"settings": mp_diag.comm_settings(nbx, comm)}
         if grouped:
             for it in range(2):
                 live = []
@@ -183,6 +185,7 @@ def _run_ranks(nbx, n, target, *extra):
 
 
 def _check_cases(oracle, n, res):
+    failures = []
     for kind, dtype, op in CASES:
         xs = [_inputs(oracle, kind, dtype, n, r) for r in range(n)]
         devop, arg = oracle.host_to_dev_redop(op, dtype, n)
@@ -210,7 +213,11 @@ def _check_cases(oracle, n, res):
                     if r != 1 % n:
                         continue
                     exp = full
-                assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, kind, dtype, op, r)
+                if not np.array_equal(got.view(np.uint8), exp.view(np.uint8)):
+                    k = {"allreduce": "ar", "reducescatter": "rs", "reduce": "red"}[kind]
+                    failures.append((f"iteration {it} {kind} dtype {dtype} op {op}", k, dtype, op, COUNT, r,
+                                     got.view(np.uint8), xs, res[r].get("settings"), 1 % n))
+    mp_diag.raise_collective_failures(oracle, failures, n)
 
 
 # NCCL_ALGO=Ring ReduceScatter / Reduce through the Simple ring schedule
@@ -310,7 +317,12 @@ def test_multiprocess_ring_fifo_reduce_scatter_and_reduce(nbx, oracle, n, grid, 
         for it in range(2):
             for r, e in exp.items():
                 got = res[r][(it, i)]
-                assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (it, kind, dtype, op, count, r)
+                if not np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)):
+                    w = np.nonzero(got.reshape(-1, e.itemsize) != np.ascontiguousarray(e).view(np.uint8).reshape(
+                        -1, e.itemsize))[0] if got.size == e.nbytes else np.array([-1])
+                    raise AssertionError(f"ring FIFO iteration {it} {(kind, dtype, op, count, root)} rank {r}: "
+                                         f"{np.unique(w).size} of {e.size} elements wrong, first {int(w[0])} last "
+                                         f"{int(w[-1])} (fold order ring_chain; NCCL_ALGO=Ring, grid {grid or 32})")
 
 
 # config D at full size (8 ranks x 1 GiB, direct and ring) and config E:
@@ -367,6 +379,7 @@ def _child_ll(uid_bytes, rank, n, q, proto):
         nbx.load_library()
         torch.cuda.set_device(0)
         comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        settings = mp_diag.comm_settings(nbx, comm)
         st = torch.cuda.current_stream().cuda_stream
         out = {}
         for it in range(3):   # repeated: exercises both LL parities and LL/direct interleaving
@@ -401,7 +414,7 @@ def _child_ll(uid_bytes, rank, n, q, proto):
         us = (time.perf_counter() - t0) * 1e6 / 200
         assert comm.async_error() == 0
         comm.destroy()
-        q.put((rank, "ok", (out, us)))
+        q.put((rank, "ok", (out, us, settings)))
     except Exception:
         import traceback
         q.put((rank, "error", traceback.format_exc()))
@@ -438,6 +451,7 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
         for p in procs:
             if p.is_alive():
                 p.terminate()
+    failures = []   # every wrong output of every case, rank and iteration, described at the end
     for i, (kind, dtype, op, count, shift) in enumerate(LL_CASES):
         xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
         devop, arg = oracle.host_to_dev_redop(op, dtype, n)
@@ -464,7 +478,10 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
         for it in range(3):
             for r, e in exp.items():
                 got = res[r][0][(it, i)]
-                assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (it, kind, dtype, op, count, r)
+                if not np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)):
+                    failures.append((f"case {i} {LL_CASES[i]} iteration {it}", kind, dtype, op, count, r, got, xs,
+                                     res[r][2], _ll_root(i, n)))
+    mp_diag.raise_collective_failures(oracle, failures, n, what=f"NCCL_PROTO={proto or 'default'}: ")
     print(f"LL 4 KiB fp32 allreduce (NCCL_PROTO={proto or 'default'}), {n} ranks sharing one GPU: us/call =",
           [round(res[r][1], 1) for r in range(n)])
 
