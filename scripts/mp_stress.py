@@ -70,6 +70,26 @@ def _input(torch, c, r, it, k, n, dev):
     return v.to(getattr(torch, c["t"]))
 
 
+def _describe(torch, c, y, ref, rank, n, settings):
+    """mp_diag's description of a wrong output: count, first / last, runs, the
+    protocol, the Simple cells, and how many wrong values are zero or equal a
+    peer's raw input or the output of the call before (stale data)."""
+    from tests import mp_diag
+    kind = {"allreduce": "ar", "reducescatter": "rs", "reduce": "red"}[c["kind"]]
+    eb = y.element_size()
+    raw = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[eb]   # bf16 has no numpy type
+    got = y.contiguous().view(raw).cpu().numpy()
+    exp = ref.contiguous().view(raw).cpu().numpy()
+    geom = None
+    proto = mp_diag.proto_of(kind, c["count"], eb, n, settings)
+    if proto == "Simple":
+        geom = mp_diag.simple_geometry(kind, c["count"], eb, n, settings.get("simpleGrid", 32),
+                                       settings.get("sliceBytes", 64 << 10))
+    d = mp_diag.describe_mismatch(got, exp, geom, rank * c["count"] if kind == "rs" else 0)
+    d["proto"] = proto
+    return {"what": mp_diag.format_mismatch(d)}
+
+
 def rank_main(rank, n, iters, seed, uid, q):
     try:
         import random
@@ -81,6 +101,8 @@ def rank_main(rank, n, iters, seed, uid, q):
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid), rank)
+        from tests import mp_diag
+        settings = mp_diag.comm_settings(nbx, comm)
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
         bad, ncalls, errs = 0, 0, []
         for it in range(iters):
@@ -138,8 +160,8 @@ def rank_main(rank, n, iters, seed, uid, q):
                     continue
                 if not torch.equal(y, ref):
                     bad += 1
-                    if len(errs) < 5:
-                        errs.append({"it": it, "k": k, "call": c, "wrong": int((y != ref).sum())})
+                    if len(errs) < 5:   # self-describing (tests/mp_diag.py): where, which cells, what values
+                        errs.append({"it": it, "k": k, "call": c, **_describe(torch, c, y, ref, rank, n, settings)})
         ok = comm.async_error() == 0
         comm.destroy()
         q.put((rank, {"calls": ncalls, "mismatches": bad, "errors": errs, "async_ok": ok}))

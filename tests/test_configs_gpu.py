@@ -132,9 +132,45 @@ def _digest_e4m3(a):
     """Digest with every NaN code made 0x7F: NaN is compared as NaN, not by
     sign (the repo's parity convention, tests/test_reduce_gpu.py assert_same —
     the GPU's fp32 add returns a NaN whose sign need not be the x86 one's)."""
+    return _digest(_canon_e4m3(a))
+
+
+def _canon_e4m3(a):
     a = np.array(a, dtype=np.uint8, copy=True)
     a[(a & 0x7F) == 0x7F] = 0x7F
-    return _digest(a)
+    return a
+
+
+CHUNK_BYTES = 1 << 20
+
+
+def _chunk_digests(a):
+    """Short digests of every 1 MiB of an output: a wrong output then says WHERE
+    it is wrong (mp_diag maps the chunks to the Simple schedule's cells)."""
+    b = memoryview(np.ascontiguousarray(a)).cast("B")
+    return [hashlib.sha256(b[o:o + CHUNK_BYTES]).hexdigest()[:16] for o in range(0, len(b), CHUNK_BYTES)]
+
+
+def _describe_chunks(key, r, got, want, settings, algo):
+    """Which 1 MiB chunks differ, as element ranges and (block, round, workgroup) cells."""
+    from tests import mp_diag
+    eb = {"d_allreduce": 4, "d_reduce_scatter": 4, "e_i64_max": 8, "e_f8_sum": 1}[key]
+    bad = [i for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    if len(got) != len(want):
+        return f"{key} rank {r}: {len(got)} chunks vs {len(want)} expected"
+    msg = f"{key} rank {r}: {len(bad)} of {len(want)} 1 MiB chunks differ, first {bad[:6]}"
+    if settings and algo == "direct" and bad:
+        kind, count = {"d_allreduce": ("ar", COUNT_D), "d_reduce_scatter": ("rs", RC_D),
+                       "e_i64_max": ("ar", COUNT_E_I64), "e_f8_sum": ("ar", COUNT_E_F8)}[key]
+        g = mp_diag.simple_geometry(kind, count, eb, N_RANKS, settings.get("simpleGrid", 32),
+                                    settings.get("sliceBytes", 64 << 10))
+        base = r * count if kind == "rs" else 0
+        per = CHUNK_BYTES // eb
+        idx = np.concatenate([np.arange(i * per, (i + 1) * per, max(per // 64, 1)) for i in bad[:64]])
+        cells = np.unique(g.locate(idx + base)[:, :3], axis=0)
+        msg += (f"; geometry block {g.block_elts} grid {g.grid} slice {g.slice_elts} rounds {g.n_rounds}; "
+                f"{len(cells)} (block, round, workgroup) cells touched, e.g. {cells[:6].tolist()}")
+    return msg
 
 
 def _child_de(uid_bytes, rank, n, q):
@@ -146,7 +182,8 @@ def _child_de(uid_bytes, rank, n, q):
         torch.cuda.set_device(0)
         comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
         st = torch.cuda.current_stream().cuda_stream
-        res = {}
+        from tests import mp_diag
+        res = {"settings": mp_diag.comm_settings(nbx, comm)}
 
         def timed(fn):
             torch.cuda.synchronize()
@@ -158,20 +195,25 @@ def _child_de(uid_bytes, rank, n, q):
         x = torch.from_numpy(_input_d(rank)).cuda()
         y = torch.empty_like(x)
         res["d_allreduce_ms"] = timed(lambda: comm.all_reduce(x.data_ptr(), y.data_ptr(), COUNT_D, F32, 0, st))
-        res["d_allreduce"] = _digest(y.cpu().numpy())
+        yh = y.cpu().numpy()
+        res["d_allreduce"], res["d_allreduce_chunks"] = _digest(yh), _chunk_digests(yh)
+        del yh
         print(f"rank {rank}: config D AllReduce done ({res['d_allreduce_ms']:.1f} ms)", flush=True)
         z = torch.empty(RC_D, dtype=torch.float32, device="cuda")
         res["d_reduce_scatter_ms"] = timed(lambda: comm.reduce_scatter(x.data_ptr(), z.data_ptr(), RC_D, F32, 0, st))
-        res["d_reduce_scatter"] = _digest(z.cpu().numpy())
+        zh = z.cpu().numpy()
+        res["d_reduce_scatter"], res["d_reduce_scatter_chunks"] = _digest(zh), _chunk_digests(zh)
         del x, y, z
         a = torch.from_numpy(_input_e_i64(rank).copy()).cuda()
         b = torch.empty_like(a)
         res["e_i64_max_ms"] = timed(lambda: comm.all_reduce(a.data_ptr(), b.data_ptr(), COUNT_E_I64, I64, 2, st))
-        res["e_i64_max"] = _digest(b.cpu().numpy())
+        bh = b.cpu().numpy()
+        res["e_i64_max"], res["e_i64_max_chunks"] = _digest(bh), _chunk_digests(bh)
         a = torch.from_numpy(_input_e_f8(rank)).cuda()
         b = torch.empty_like(a)
         res["e_f8_sum_ms"] = timed(lambda: comm.all_reduce(a.data_ptr(), b.data_ptr(), COUNT_E_F8, E4M3, 0, st))
-        res["e_f8_sum"] = _digest_e4m3(b.cpu().numpy())
+        bh = _canon_e4m3(b.cpu().numpy())
+        res["e_f8_sum"], res["e_f8_sum_chunks"] = _digest(bh), _chunk_digests(bh)
         print(f"rank {rank}: config E done", flush=True)
         assert comm.async_error() == 0
         comm.destroy()
@@ -206,15 +248,18 @@ def _expected_de(oracle):
     xs = [_input_d(r) for r in range(n)]
     _say("oracle: config D inputs regenerated")
     full = _ring_fold(oracle, xs, F32, 0, 0, _blocks(COUNT_D, 4, n), n)
-    exp["d_allreduce"] = [_digest(full)] * n
+    exp["d_allreduce"] = [(_digest(full), _chunk_digests(full))] * n
     rs = _ring_fold(oracle, xs, F32, 0, 0, [(c * RC_D, (c + 1) * RC_D) for c in range(n)], n)
-    exp["d_reduce_scatter"] = [_digest(rs[r * RC_D:(r + 1) * RC_D]) for r in range(n)]
+    exp["d_reduce_scatter"] = [(_digest(rs[r * RC_D:(r + 1) * RC_D]), _chunk_digests(rs[r * RC_D:(r + 1) * RC_D]))
+                               for r in range(n)]
     del xs, full, rs
     devop, arg = oracle.host_to_dev_redop(2, I64, n)   # ncclMax
     xs = [_input_e_i64(r) for r in range(n)]
-    exp["e_i64_max"] = [_digest(_ring_fold(oracle, xs, I64, devop, arg, _blocks(COUNT_E_I64, 8, n), n))] * n
+    e = _ring_fold(oracle, xs, I64, devop, arg, _blocks(COUNT_E_I64, 8, n), n)
+    exp["e_i64_max"] = [(_digest(e), _chunk_digests(e))] * n
     xs = [_input_e_f8(r) for r in range(n)]
-    exp["e_f8_sum"] = [_digest_e4m3(_ring_fold(oracle, xs, E4M3, 0, 0, _blocks(COUNT_E_F8, 1, n), n))] * n
+    e = _canon_e4m3(_ring_fold(oracle, xs, E4M3, 0, 0, _blocks(COUNT_E_F8, 1, n), n))
+    exp["e_f8_sum"] = [(_digest(e), _chunk_digests(e))] * n
     _say("oracle: configs D and E expected digests ready")
     return exp
 
@@ -255,8 +300,12 @@ def test_configs_d_e_8_ranks_full_size(nbx, oracle, monkeypatch, algo):
         for p in procs:
             if p.is_alive():
                 p.terminate()
+    wrong = []
     for key, digests in exp.items():
         for r in range(n):
-            assert res[r][key] == digests[r], f"{key} rank {r}"
-    times = {k: round(max(res[r][k] for r in range(n)), 2) for k in res[0] if k.endswith("_ms")}
+            if res[r][key] != digests[r][0]:
+                wrong.append(_describe_chunks(key, r, res[r][key + "_chunks"], digests[r][1], res[r].get("settings"),
+                                              algo))
+    assert not wrong, f"configs D/E ({algo}): {len(wrong)} wrong output(s):\n" + "\n".join(wrong[:8])
+    times = {k: round(max(res[r][k] for r in range(n)), 2) for k in res[0] if isinstance(k, str) and k.endswith("_ms")}
     print(f"configs D/E ({algo}, 8 ranks sharing one GPU), max ms over ranks: {times}", file=sys.stderr)

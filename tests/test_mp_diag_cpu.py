@@ -164,3 +164,32 @@ def test_proto_of_matches_the_library():
                     lib_p = lib.nbxDebugChooseProto(7, int(kind != "rs"), count * eb, (hi - lo) * eb, n, 64 << 10,
                                                     1 << 20, 256 << 10)
                     assert mp_diag.proto_of(kind, count, eb, n, settings) == names[lib_p], (n, kind, eb, count)
+
+
+def test_configs_d_e_chunk_description():
+    """The 8-rank config D / E test compares 1 MiB chunk digests on a mismatch
+    and maps the differing chunks to the Simple schedule's cells."""
+    from tests import test_configs_gpu as t
+    a = np.arange(4 * t.CHUNK_BYTES // 4, dtype=np.float32)
+    want = t._chunk_digests(a)
+    b = a.copy()
+    b[t.CHUNK_BYTES // 4 * 2 + 5] = -1   # chunk 2
+    got = t._chunk_digests(b)
+    msg = t._describe_chunks("d_allreduce", 0, got, want, {"simpleGrid": 32, "sliceBytes": 64 << 10}, "direct")
+    assert "1 of 4 1 MiB chunks differ, first [2]" in msg and "(block, round, workgroup) cells" in msg
+
+
+def test_mp_stress_describes_a_wrong_output():
+    """scripts/mp_stress.py records what a wrong output looks like (bf16 too)."""
+    import importlib.util
+    import torch
+    spec = importlib.util.spec_from_file_location("mp_stress", os.path.join(ROOT, "scripts", "mp_stress.py"))
+    ms = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ms)
+    ref = torch.arange(1, 1000001, dtype=torch.float32).to(torch.bfloat16)
+    y = ref.clone()
+    y[1000:1010] = 0
+    c = {"kind": "allreduce", "count": 1000000}
+    out = ms._describe(torch, c, y, ref, 0, 4, {"llMax": 64 << 10, "l128Max": 1 << 20, "simpleGrid": 64,
+                                                 "sliceBytes": 64 << 10})
+    assert out["what"].startswith("Simple: 10 of 1000000 elements wrong") and "zero=10" in out["what"]
