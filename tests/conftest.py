@@ -42,6 +42,8 @@ def gpu_order_key(item_path: str, test_name: str = "") -> tuple:
 
 
 def pytest_collection_modifyitems(session, config, items):
+    if os.environ.get("NBX_GPU_TEST_ORDER") == "files":   # collection order (replays an earlier run's order)
+        return
     keyed = [(gpu_order_key(str(it.fspath), it.name), i, it) for i, it in enumerate(items)]
     keyed.sort(key=lambda t: (t[0], t[1]))
     items[:] = [t[2] for t in keyed]
