@@ -62,7 +62,10 @@ def _expected(oracle, case, i, n):
     return exp, xs
 
 
-def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=False):
+GUARD = 4096
+
+
+def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=False, guard=False):
     try:
         import random
 
@@ -85,6 +88,7 @@ def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=
                 exp[i] = np.ascontiguousarray(e[rank]).view(np.uint8)
         rng = random.Random(1234 + rank)
         bad = []
+        guard_hits = []
         prev = {}
         calls = 0
         t0 = time.time()
@@ -93,11 +97,14 @@ def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=
             for i in case_ids:
                 kind, dtype, op, count, shift = cases[i]
                 x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
-                tx = torch.zeros(x.size + 16, dtype=torch.uint8, device="cuda")
-                tx[shift:shift + x.size] = torch.from_numpy(x.copy()).cuda()
+                G = GUARD if guard else 0   # guard bytes before and after (0xA5), checked after the iteration
+                tx = torch.full((x.size + 16 + 2 * G,), 0xA5, dtype=torch.uint8, device="cuda")
+                tx[G:G + x.size + 16] = 0
+                tx[G + shift:G + shift + x.size] = torch.from_numpy(x.copy()).cuda()
                 out_bytes = x.size // n if kind == "rs" else x.size
-                ty = torch.zeros(out_bytes + 16, dtype=torch.uint8, device="cuda")
-                sp, rp = tx.data_ptr() + shift, ty.data_ptr() + shift
+                ty = torch.full((out_bytes + 16 + 2 * G,), 0xA5, dtype=torch.uint8, device="cuda")
+                ty[G:G + out_bytes + 16] = 0
+                sp, rp = tx.data_ptr() + G + shift, ty.data_ptr() + G + shift
                 if jitter and rng.random() < 0.3:
                     time.sleep(rng.random() * 0.004)
                 if skew and rng.random() < 0.02:   # a rank stalls (first-launch code loading on a fresh box)
@@ -109,12 +116,18 @@ def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=
                 else:
                     comm.reduce(sp, rp, count, dtype, op, _ll_root(i, n), st)
                 calls += 1
-                keep.append((i, ty, shift, out_bytes))
+                keep.append((i, ty, shift, out_bytes, tx, G))
             torch.cuda.synchronize()
-            for i, ty, shift, nb in keep:
+            for i, ty, shift, nb, tx_, G in keep:
+                if G:   # no byte outside [recv, recv + bytes) of the call's own slack may change
+                    for name, t_ in (("send", tx_), ("recv", ty)):
+                        lo, hi = t_[:G], t_[t_.numel() - G:]
+                        if not (bool((lo == 0xA5).all()) and bool((hi == 0xA5).all())):
+                            guard_hits.append({"it": it, "case": i, "buf": name,
+                                               "before": int((lo != 0xA5).sum()), "after": int((hi != 0xA5).sum())})
                 if i not in exp:
                     continue
-                got = ty[shift:shift + nb].cpu().numpy().copy()
+                got = ty[G + shift:G + shift + nb].cpu().numpy().copy()
                 if not np.array_equal(got, exp[i]):
                     bad.append({"it": it, "case": i, "got": got, "prev": prev.get(i)})
                 prev[i] = got
@@ -126,7 +139,8 @@ def rank_main(uid_bytes, rank, n, iters, case_ids, jitter, q, fresh=False, skew=
                 torch.cuda.empty_cache()
         err = comm.async_error()
         comm.destroy()
-        q.put((rank, "ok", {"bad": bad, "calls": calls, "async_error": err, "settings": settings,
+        q.put((rank, "ok", {"bad": bad, "guard_hits": guard_hits, "calls": calls, "async_error": err,
+                            "settings": settings,
                             "s": time.time() - t0, "iters_done": it + 1}))
     except Exception:
         import traceback
@@ -155,6 +169,7 @@ def main():
     ap.add_argument("--jitter", action="store_true")
     ap.add_argument("--fresh", action="store_true", help="torch.cuda.empty_cache() after every iteration")
     ap.add_argument("--skew", action="store_true", help="ranks stall 50-250 ms now and then")
+    ap.add_argument("--guard", action="store_true", help="4 KiB 0xA5 guards around every buffer, checked")
     args = ap.parse_args()
     lo, hi = (int(x) for x in args.cases.split(":"))
     case_ids = list(range(lo, min(hi, len(_cases()))))
@@ -171,7 +186,7 @@ def main():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=rank_main, args=(bytes(uid), r, n, args.iters, case_ids, args.jitter, q, args.fresh,
-                                                     args.skew), daemon=True)
+                                                     args.skew, args.guard), daemon=True)
              for r in range(n)]
     for p in procs:
         p.start()
@@ -209,12 +224,13 @@ def main():
            "calls": sum(pl["calls"] for pl in res.values()),
            "bad_calls": sum(len(pl["bad"]) for pl in res.values()),
            "bad_per_rank": {r: len(pl["bad"]) for r, pl in res.items()},
+           "guard_hits": {r: pl["guard_hits"][:4] for r, pl in res.items() if pl.get("guard_hits")},
            "async_errors": {r: pl["async_error"] for r, pl in res.items() if pl["async_error"]},
            "settings": res[min(res)]["settings"] if res else None,
            "seconds": max((pl["s"] for pl in res.values()), default=None),
            "mismatches": mism, "errors": errors}
     print(json.dumps(out, default=str), flush=True)
-    return 1 if (mism or errors) else 0
+    return 1 if (mism or errors or out["guard_hits"]) else 0
 
 
 if __name__ == "__main__":

@@ -24,10 +24,10 @@ def pytest_configure(config):
 # run between the core and the transport group.
 GPU_FILE_ORDER = [
     "test_reduce_gpu.py", "test_config_a.py", "test_nccl_api_gpu.py", "test_rccl_corroboration_gpu.py",
-    "test_c_perf_gpu.py", "test_bench_rccl_gpu.py",
+    "test_sched_stress_gpu.py", "test_c_perf_gpu.py", "test_bench_rccl_gpu.py",
     None,   # everything else
     "test_configs_gpu.py", "test_clique_transport_gpu.py", "test_multiprocess_gpu.py",
-    "test_multiprocess_churn_gpu.py", "test_multiprocess_stress_gpu.py", "test_sched_stress_gpu.py",
+    "test_multiprocess_churn_gpu.py", "test_multiprocess_stress_gpu.py",
 ]
 
 
