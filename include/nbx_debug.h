@@ -65,9 +65,9 @@ int nbxDebugCommProtoMask(ncclComm_t comm);
  * slots, [4] Simple grid, [5] LL grid cap, [6] LL128 grid cap, [7] group
  * batching, [8] connection buffers re-exported at creation because a peer's
  * IPC mapping of them showed other memory (verified before first use), [9]
- * plan checks on (NBX_CHECK_PLANS / NCCL_CHECK_POINTERS). Writes
- * min(nOut, 10) values and returns that count; -1 for a bad handle or a
- * communicator without a multi-rank transport. */
+ * plan checks on (NBX_CHECK_PLANS / NCCL_CHECK_POINTERS), [10] Simple slice
+ * checksums on (NBX_CHECK_SLICES). Writes min(nOut, 11) values and returns that
+ * count; -1 for a bad handle or a communicator without a multi-rank transport. */
 int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut);
 
 /* Config D's xGMI transport alone, on a multi-process

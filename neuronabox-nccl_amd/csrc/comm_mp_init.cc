@@ -56,6 +56,7 @@ struct MpInitInfo {
   int32_t simpleGrid;
   int32_t groupBatch;      // NBX_GROUP_BATCH: one launch per run of grouped calls, or one per call
   int32_t checkPlans;      // NBX_CHECK_PLANS: every launch stamps / checks its plan (or none does)
+  int32_t checkSlices;     // NBX_CHECK_SLICES: every Simple slice carries a checksum (or none does)
 };
 
 }  // namespace
@@ -236,6 +237,13 @@ void mpReportDeviceError(ncclComm* c) {
     warn("comm %p rank %d: a device wait was aborted (ncclCommAbort)", (void*)c, c->rank);
     return;
   }
+  if (rec[0] == nbx::kDiagSimpleSlice) {
+    warn("comm %p rank %d: device check failed: %s: from peer %lld, slot use %llu: the peer stamped sum %08llx, "
+         "this rank read sum %08llx (use %llu) (workgroup %llu)", (void*)c, c->rank, nbx::diagSiteName(rec[0]),
+         (long long)(int64_t)rec[1], (unsigned long long)(rec[2] >> 32), (unsigned long long)(rec[2] & 0xffffffffu),
+         (unsigned long long)(rec[3] & 0xffffffffu), (unsigned long long)(rec[3] >> 32), (unsigned long long)rec[4]);
+    return;
+  }
   if (nbx::diagIsPlanCheck(rec[0])) {
     warn("comm %p rank %d: device check failed after %.3f s: %s: peer %lld, our plan %llx, its plan %llx "
          "(workgroup %llu)", (void*)c, c->rank, (double)rec[5] * 1e-8, nbx::diagSiteName(rec[0]),
@@ -286,6 +294,13 @@ ncclResult_t mpAllocLL(MpState* mp, int n, bool ipc, const ncclComm* comm) {
   // knob NCCL_CHECK_POINTERS=1): they cost 0.7-1.9 us per small call on the
   // shared-GPU rig, and the reference does not check this either.
   mp->checkPlans = envLong("NBX_CHECK_PLANS", comm->checkPointers ? 1 : 0) != 0;
+  // Slice checksums (nbx_simple.h): every Simple staging slice carries a hash of
+  // its elements that the consumer recomputes from what it read; a difference
+  // (a slot read before its stores landed, a stale or misplaced slice) fails
+  // the launch naming the peer and slot use. A debug knob: the producer and
+  // consumer hash every element (off by default; equal on every rank).
+  mp->checkSlices = envLong("NBX_CHECK_SLICES", 0) != 0;
+  mp->sliceFaultRank = (int)envLong("NBX_DEBUG_SLICE_FAULT", -1);
   HIPCHECK(hipMalloc((void**)&mp->orderMem, 1024));
   HIPCHECK(hipMemset(mp->orderMem, 0, 1024));
   HIPCHECK(hipMalloc((void**)&mp->llState, sizeof(nbx::LLState)));
@@ -605,6 +620,7 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
   mine.simpleGrid = mp->simpleGrid;
   mine.groupBatch = mp->groupBatch;
   mine.checkPlans = mp->checkPlans;
+  mine.checkSlices = mp->checkSlices;
   mine.nonce = std::random_device{}() * 0x100000001ull ^ (uint64_t)std::random_device{}() ^
                ((uint64_t)getpid() << 20) ^ (uint64_t)(uintptr_t)mp;
   mine.llHandle = mp->llHandle;
@@ -636,6 +652,11 @@ ncclResult_t mpInit(ncclComm* c, const ncclUniqueId& id) {
     // a checking rank would wait for plan words a non-checking peer never stamps
     if (all[j].checkPlans != mine.checkPlans) {
       warn("ncclCommInitRank : NBX_CHECK_PLANS / NCCL_CHECK_POINTERS differ across ranks");
+      return ncclInvalidUsage;
+    }
+    // a checking consumer would compare against sums a non-checking producer never stamps
+    if (all[j].checkSlices != mine.checkSlices) {
+      warn("ncclCommInitRank : NBX_CHECK_SLICES differs across ranks");
       return ncclInvalidUsage;
     }
     if (j == me || all[j].device == c->device) continue;
@@ -875,11 +896,11 @@ NBX_EXPORT int nbxDebugCommSettings(ncclComm_t comm, int64_t* out, int nOut) {
   if (comm->asyncError.load() != ncclSuccess) return -1;
   const MpState* mp = mpOf(comm);
   if (mp == nullptr) return -1;
-  const int64_t v[10] = {(int64_t)mp->llMaxBytes, (int64_t)mp->l128MaxBytes, (int64_t)mp->sliceBytes, mp->slots,
+  const int64_t v[11] = {(int64_t)mp->llMaxBytes, (int64_t)mp->l128MaxBytes, (int64_t)mp->sliceBytes, mp->slots,
                          mp->simpleGrid,          (int64_t)mp->llGridCap,    (int64_t)mp->l128GridCap, mp->groupBatch,
-                         mp->ipcRepairs,          mp->checkPlans};
+                         mp->ipcRepairs,          mp->checkPlans,           mp->checkSlices};
   int k = 0;
-  for (; k < nOut && k < 10; k++) out[k] = v[k];
+  for (; k < nOut && k < 11; k++) out[k] = v[k];
   return k;
 }
 

@@ -182,6 +182,7 @@ ncclResult_t mpLaunchSimple(ncclComm* comm, const MpCall* calls, int nc, bool tr
   sa.prefetch = mp->simplePrefetch;
   sa.hdrOff = mp->stageHdrOff;
   sa.planSig = mp->checkPlans ? nbx::simplePlanSig(sa, (uint32_t)grid, (int32_t)c.dt, c.op.op) : 0;
+  sa.checkSlices = mp->checkSlices ? (mp->sliceFaultRank == me ? 2 : 1) : 0;   // 2: test hook, a wrong stamp
   sa.order = mpOrderArgs(mp);
   return nbx::launchSimple(c.dt, c.op, sa, (unsigned)grid, mp->ring && !transport, c.stream);
 }

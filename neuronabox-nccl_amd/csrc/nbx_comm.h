@@ -279,6 +279,8 @@ struct MpState {
   std::vector<MpCall> group;        // calls queued inside ncclGroupStart/End (run at the outermost End)
   bool groupBatch = true;           // NBX_GROUP_BATCH=0: every grouped call its own kernel
   bool checkPlans = false;          // NBX_CHECK_PLANS (default NCCL_CHECK_POINTERS): plan words / headers
+  bool checkSlices = false;         // NBX_CHECK_SLICES: Simple slices carry a checksum the consumer verifies
+  int sliceFaultRank = -1;          // NBX_DEBUG_SLICE_FAULT (test hook): this rank's workgroup 0 stamps wrong sums
   std::vector<hipEvent_t> groupEvents;   // fan-in / fan-out of a group launch over several streams
   // clique ranks only: the previous call ran on the event-ordered fold path
   // (runCliqueColl / runCliqueBatch) on extStream; it is complete once every

@@ -32,12 +32,13 @@ enum DiagSite : uint64_t {
   kDiagSimplePlan = 13,  // Simple: a peer's slice was cut by another plan (mismatched calls or group runs)
   kDiagLLPlan = 14,      // LL family: a peer at the same call runs another plan
   kDiagLLPlanWord = 15,  // LL family: a peer's plan word for this call (its lines had arrived)
+  kDiagSimpleSlice = 16, // Simple (NBX_CHECK_SLICES): a slice read differs from what its producer wrote
 };
 constexpr int kDiagWords = 6;
 constexpr int kDiagByteOffset = 16;   // from the start of the host words
 
 // a site that records a failed consistency check, not a wait that gave up
-constexpr bool diagIsPlanCheck(uint64_t s) { return s == kDiagSimplePlan || s == kDiagLLPlan; }
+constexpr bool diagIsPlanCheck(uint64_t s) { return s == kDiagSimplePlan || s == kDiagLLPlan || s == kDiagSimpleSlice; }
 
 inline const char* diagSiteName(uint64_t s) {
   switch (s) {
@@ -56,6 +57,7 @@ inline const char* diagSiteName(uint64_t s) {
     case kDiagSimplePlan: return "Simple slice from a peer running a different plan (mismatched call or group cut)";
     case kDiagLLPlan: return "LL / LL128 lines from a peer running a different plan (mismatched call or group cut)";
     case kDiagLLPlanWord: return "LL / LL128 plan word of a peer";
+    case kDiagSimpleSlice: return "Simple slice checksum (the bytes read differ from the bytes the peer wrote)";
     default: return "unknown";
   }
 }

@@ -198,6 +198,8 @@ struct SimpleArgs {
   int32_t gridMax;
   int32_t prefetch;            // direct: push round k+1 before folding round k (a rank-local choice)
   int32_t nSegs;               // group launch: segments in seg[] (0: one message)
+  int32_t checkSlices;         // NBX_CHECK_SLICES: producers stamp, consumers verify every slice's checksum
+  int32_t pad0;
   MpDone order;
   SimpleSeg seg[kSimpleMaxSegs];
 };

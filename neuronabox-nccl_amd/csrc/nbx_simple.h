@@ -183,6 +183,66 @@ __device__ __forceinline__ bool simpleWaitSlice(const uint64_t* w, uint64_t targ
   return false;
 }
 
+// Slice checksums (NBX_CHECK_SLICES, SimpleArgs.checkSlices): the producer of
+// a staging slice sums a hash of every element it stores there (position-mixed,
+// order-free: a 32-bit sum over the workgroup, LDS atomics) and stamps {use
+// count, sum} into the second word of the slice's header cell before the drain
+// that publishes the slice; the consumer sums the same hash over every element
+// it loads and, after its drain, compares with the header. A mismatch means the
+// bytes read are not the bytes written — a stale slot, a store not yet landed,
+// a misplaced copy — and fails the launch naming the peer, the slot use and both
+// sums (kDiagSimpleSlice) instead of returning a silently wrong result. The hash
+// is defined per element (index e within the slice, raw bits zero-extended), so
+// the 16-B pack path and the element path of either side agree.
+__device__ __forceinline__ uint32_t sliceMix(uint32_t lo, uint32_t hi, uint32_t e) {
+  const uint32_t t = lo * 0x9E3779B1u ^ hi * 0x85EBCA77u ^ (e + 1u) * 0xC2B2AE3Du;
+  return t ^ (t >> 15);
+}
+template <class E>
+__device__ __forceinline__ uint32_t sliceEltHash(E v, uint64_t e) {
+  uint64_t bits = 0;
+  __builtin_memcpy(&bits, &v, sizeof(E));
+  return sliceMix((uint32_t)bits, (uint32_t)(bits >> 32), (uint32_t)e);
+}
+// the sum of sliceEltHash over the 16 / sizeof(E) elements of pack v, the first at e0
+template <class E>
+__device__ __forceinline__ uint32_t slicePackHash(u32x4 v, uint64_t e0) {
+  constexpr int EB = (int)sizeof(E);
+  const uint32_t e = (uint32_t)e0;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t h = 0;
+  if constexpr (EB == 8) {
+    h = sliceMix(v.x, v.y, e) + sliceMix(v.z, v.w, e + 1);
+  } else if constexpr (EB == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) h += sliceMix(w[i], 0, e + i);
+  } else if constexpr (EB == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) h += sliceMix(w[i] & 0xffffu, 0, e + 2 * i) + sliceMix(w[i] >> 16, 0, e + 2 * i + 1);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; i++) h += sliceMix((w[i / 4] >> (8 * (i % 4))) & 0xffu, 0, e + i);
+  }
+  return h;
+}
+// checkSlices == 2 (the test hook NBX_DEBUG_SLICE_FAULT=<this rank>): workgroup
+// 0 stamps a wrong sum, so its consumers must fail the launch.
+__device__ __forceinline__ void simpleStampSum(uint64_t* h, const SimpleArgs& a, int g, uint64_t count,
+                                               uint32_t sum) {
+  if (a.checkSlices == 2 && g == 0) sum ^= 1u;
+  __hip_atomic_store(h + 1, ((uint64_t)(uint32_t)count << 32) | sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// After the consumer's drain: the header's {count, sum} against what was read.
+__device__ __forceinline__ bool simpleCheckSum(const SimpleArgs& a, const uint64_t* h, uint64_t count, uint32_t got,
+                                               int peer) {
+  const uint64_t want = __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t seen = ((uint64_t)(uint32_t)count << 32) | got;
+  if (want == seen) return true;
+  diagTimeout(a.errWord, kDiagSimpleSlice, peer, want, seen, 0);
+  *a.errWord = 1;
+  return false;
+}
+
 // What workgroup g (of `grid`) moves of block b in round k: elements
 // [off, off + cnt) of the message whose send / recv buffers are given (a
 // group launch's segment, or the launch's one message), and that message's
@@ -228,9 +288,14 @@ __device__ __forceinline__ SimpleSpan simpleSlice(const SimpleArgs& a, const Sim
 // 16-B packs when every pointer is 16-B aligned). sys0 / sys1: the
 // destination is staging (write-through stores), else a caller buffer; sysSrc:
 // the source is staging (system-scope loads).
+// sum (NBX_CHECK_SLICES, else nullptr): an LDS word that receives the slice
+// hash of the elements copied (the staging source read, or the staging
+// destination written: the same bytes).
 template <class E>
 __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool sys1, const void* src, bool sysSrc,
-                                           uint64_t nElts) {
+                                           uint64_t nElts, uint32_t* sum = nullptr) {
+  constexpr int EPP = 16 / (int)sizeof(E);
+  uint32_t h = 0;
   uint64_t done = 0;
   if (((((uintptr_t)d0) | ((uintptr_t)src) | (d1 ? (uintptr_t)d1 : 0)) & 15u) == 0) {
     const uint64_t nPk = nElts * sizeof(E) / 16;
@@ -248,6 +313,7 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
       for (int u = 0; u < U; u++) {
         if (p + (uint64_t)u * kBlock < nPk) {
           const uint64_t q = p + (uint64_t)u * kBlock;
+          if (sum) h += slicePackHash<E>(v[u], q * EPP);
           if (sys0) stSys(rd0, q, v[u]);
           else stPack((u32x4*)d0 + q, v[u]);
           if (d1) {
@@ -261,6 +327,7 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
   }
   for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
     const E v = sysSrc ? ldSysElt((const E*)src + e) : ldElt((const E*)src + e);
+    if (sum) h += sliceEltHash(v, e);
     if (sys0) stSysElt((E*)d0 + e, v);
     else ((E*)d0)[e] = v;
     if (d1) {
@@ -268,6 +335,7 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
       else ((E*)d1)[e] = v;
     }
   }
+  if (sum) atomicAdd(sum, h);
 }
 
 // Workgroup fold of nElts elements: acc = pre?(src[0]); acc = Fn(acc, pre?(src[q]))
@@ -278,13 +346,18 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
 // U packs per lane per source, G = 32 / U sources' loads in flight together
 // (32 packs = 512 B per lane, as the 8-source big tile): deep unrolling for
 // the 2-source ring hops and small rank counts, source groups for many ranks.
+// srcSums / dstSum (NBX_CHECK_SLICES, else nullptr): LDS words that receive
+// the slice hash of each staging source read (indexed by fold position) and
+// of the result stored into the staging destinations.
 template <class Fn, int U>
 __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t sysSrcMask,
                                             uint64_t preMask, bool doPost, char* const* dsts, int nDsts,
-                                            uint64_t sysMask, uint64_t nElts, bool aligned) {
+                                            uint64_t sysMask, uint64_t nElts, bool aligned, uint32_t* srcSums,
+                                            uint32_t* dstSum) {
   using E = typename Fn::Elt;
   constexpr int EPP = 16 / (int)sizeof(E);
   constexpr int G = 32 / U;
+  uint32_t hd = 0;
   uint64_t done = 0;
   if (aligned) {
     const uint64_t nPk = nElts / EPP;
@@ -305,6 +378,18 @@ __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* src
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        if (srcSums) {
+#pragma unroll
+          for (int s = 0; s < G; s++) {
+            if (q0 + s < nSrcs && ((sysSrcMask >> (q0 + s)) & 1u)) {
+              uint32_t hs = 0;
+#pragma unroll
+              for (int u = 0; u < U; u++)
+                if (p + (uint64_t)u * kBlock < nPk) hs += slicePackHash<E>(v[s][u], (p + (uint64_t)u * kBlock) * EPP);
+              atomicAdd(&srcSums[q0 + s], hs);
+            }
+          }
+        }
 #pragma unroll
         for (int s = 0; s < G; s++) {
           if (q0 + s < nSrcs) {
@@ -322,6 +407,7 @@ __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* src
         if (p + (uint64_t)u * kBlock < nPk) {
           u32x4 r = acc[u];
           if constexpr (Fn::kHasPost) if (doPost) r = fn.postPack(r);
+          if (dstSum) hd += slicePackHash<E>(r, (p + (uint64_t)u * kBlock) * EPP);
           for (int d = 0; d < nDsts; d++) {
             const uint64_t q = p + (uint64_t)u * kBlock;
             if ((sysMask >> d) & 1u) stSys(sysRsrc(dsts[d], nElts * sizeof(E)), q, r);
@@ -334,27 +420,38 @@ __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* src
   }
   for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
     E acc = (sysSrcMask & 1u) ? ldSysElt((const E*)srcs[0] + e) : ldElt((const E*)srcs[0] + e);
+    if (srcSums && (sysSrcMask & 1u)) atomicAdd(&srcSums[0], sliceEltHash(acc, e));
     if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.pre(acc);
     for (int q = 1; q < nSrcs; q++) {
       E x = ((sysSrcMask >> q) & 1u) ? ldSysElt((const E*)srcs[q] + e) : ldElt((const E*)srcs[q] + e);
+      if (srcSums && ((sysSrcMask >> q) & 1u)) atomicAdd(&srcSums[q], sliceEltHash(x, e));
       if constexpr (Fn::kHasPre) if ((preMask >> q) & 1u) x = fn.pre(x);
       acc = fn.red(acc, x);
     }
     if constexpr (Fn::kHasPost) if (doPost) acc = fn.post(acc);
+    if (dstSum) hd += sliceEltHash(acc, e);
     for (int d = 0; d < nDsts; d++) {
       if ((sysMask >> d) & 1u) stSysElt((E*)dsts[d] + e, acc);
       else ((E*)dsts[d])[e] = acc;
     }
   }
+  if (dstSum) atomicAdd(dstSum, hd);
 }
 
 template <class Fn>
 __device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t sysSrcMask,
                                            uint64_t preMask, bool doPost, char* const* dsts, int nDsts,
-                                           uint64_t sysMask, uint64_t nElts, bool aligned) {
-  if (nSrcs <= 2) simpleFoldU<Fn, 16>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned);
-  else if (nSrcs <= 4) simpleFoldU<Fn, 8>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned);
-  else simpleFoldU<Fn, 4>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned);
+                                           uint64_t sysMask, uint64_t nElts, bool aligned,
+                                           uint32_t* srcSums = nullptr, uint32_t* dstSum = nullptr) {
+  if (nSrcs <= 2)
+    simpleFoldU<Fn, 16>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
+                        dstSum);
+  else if (nSrcs <= 4)
+    simpleFoldU<Fn, 8>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
+                       dstSum);
+  else
+    simpleFoldU<Fn, 4>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
+                       dstSum);
 }
 
 __device__ __forceinline__ bool simpleAligned(const void* p) { return (((uintptr_t)p) & 15u) == 0; }
@@ -364,6 +461,8 @@ struct SimpleShared {
   uint64_t cnt[4][kSimpleMaxRanks];   // SimpleCounter x peer
   const char* src[kSimpleMaxRanks];
   char* dst[kSimpleMaxRanks];
+  uint32_t sumIn[kSimpleMaxRanks];    // NBX_CHECK_SLICES: hash of what was read (per source / peer)
+  uint32_t sumOut[kSimpleMaxRanks];   // ... and of what was written (per target / one for all)
   int fail;
 };
 
@@ -405,6 +504,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
   const bool gathers = ar || (red && me == a.root);    // C runs here
   const int first = ((red ? a.root : me) + 1) % n;      // fold order of block `me`
   auto pushTarget = [&](int p) { return p != me && (ar || (red && p == a.root)); };
+  const bool chk = a.checkSlices != 0;                  // NBX_CHECK_SLICES (uniform)
 
   auto phaseA = [&](uint64_t k) -> bool {
     // ---- A: slice g of block j into rank j's RS region, slot rsSent[j] % slots
@@ -414,16 +514,21 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
           !simpleWait(simpleFlag(myFlags, kFlRsCredit, n, tid, gm, g), sent + 1 - slots, a, tid, kDiagSimpleRsCredit))
         sh.fail = 1;
     }
+    if (chk && tid < n) sh.sumOut[tid] = 0;
     __syncthreads();
     if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
       const SimpleSpan sp = simpleSlice<E>(a, segs, j, k, g, grid);
       if (sp.cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
-                                sp.send + sp.off * sizeof(E), false, sp.cnt);
+                                sp.send + sp.off * sizeof(E), false, sp.cnt, chk ? &sh.sumOut[j] : nullptr);
     }
-    if (tid < n && tid != me)
-      simpleStamp(simpleHdr(a, tid, 0, sh.cnt[kCtRsSent][tid] % slots, me, g), a, sh.cnt[kCtRsSent][tid] + 1);
+    if (chk) __syncthreads();   // every lane's hash is in
+    if (tid < n && tid != me) {
+      uint64_t* h = simpleHdr(a, tid, 0, sh.cnt[kCtRsSent][tid] % slots, me, g);
+      simpleStamp(h, a, sh.cnt[kCtRsSent][tid] + 1);
+      if (chk) simpleStampSum(h, a, g, sh.cnt[kCtRsSent][tid] + 1, sh.sumOut[tid]);
+    }
     simpleDrain();
     if (tid < n && tid != me) simplePost(simpleFlag(a.peerFlags[tid], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][tid]);
     __syncthreads();
@@ -454,6 +559,10 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
         if (ar) sh.dst[tid] = simpleStage(a, p, 1, sh.cnt[kCtAgSent][p] % slots, me, g);
         else if (red && p == a.root) sh.dst[0] = simpleStage(a, p, 1, sh.cnt[kCtAgSent][p] % slots, me, g);
       }
+      if (chk) {
+        sh.sumIn[tid] = 0;
+        if (tid == 0) sh.sumOut[0] = 0;
+      }
     }
     __syncthreads();
     if (sh.fail) return false;
@@ -466,11 +575,25 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
       // every source but the own input (at fold position (me - first) mod n) is staging
       const int ownPos = (me - first + n) % n;
       const uint64_t sysSrc = ~(1ull << ownPos);
-      if (xport) simpleFold<Fn>(fn, sh.src + ownPos, 1, 0ull, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
-      else simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned);
+      if (xport)
+        simpleFold<Fn>(fn, sh.src + ownPos, 1, 0ull, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned, nullptr,
+                       chk ? &sh.sumOut[0] : nullptr);
+      else
+        simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned,
+                       chk ? sh.sumIn : nullptr, chk ? &sh.sumOut[0] : nullptr);
     }
-    if (tid < n && pushTarget(tid))
-      simpleStamp(simpleHdr(a, tid, 1, sh.cnt[kCtAgSent][tid] % slots, me, g), a, sh.cnt[kCtAgSent][tid] + 1);
+    if (chk) {
+      __syncthreads();   // every lane's hashes are in (sources read, result pushed)
+      // the n-1 slots folded: what each peer stamped (a transport-only call reads none)
+      if (!xport && tid < n && tid != me)
+        simpleCheckSum(a, simpleHdr(a, me, 0, sh.cnt[kCtRsRecv][tid] % slots, tid, g), sh.cnt[kCtRsRecv][tid] + 1,
+                       sh.sumIn[(tid - first + n) % n], tid);
+    }
+    if (tid < n && pushTarget(tid)) {
+      uint64_t* h = simpleHdr(a, tid, 1, sh.cnt[kCtAgSent][tid] % slots, me, g);
+      simpleStamp(h, a, sh.cnt[kCtAgSent][tid] + 1);
+      if (chk) simpleStampSum(h, a, g, sh.cnt[kCtAgSent][tid] + 1, sh.sumOut[0]);
+    }
     simpleDrain();
     if (tid < n && tid != me) {
       simplePost(simpleFlag(a.peerFlags[tid], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][tid]);
@@ -485,16 +608,21 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
         !simpleWaitSlice(simpleFlag(myFlags, kFlAgReady, n, tid, gm, g), sh.cnt[kCtAgRecv][tid] + 1,
                          simpleHdr(a, me, 1, sh.cnt[kCtAgRecv][tid] % slots, tid, g), a, tid, kDiagSimpleAg))
       sh.fail = 1;
+    if (chk && tid < n) sh.sumIn[tid] = 0;
     __syncthreads();
     if (sh.fail) return false;
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
       const SimpleSpan sp = simpleSlice<E>(a, segs, j, k, g, grid);
       if (sp.cnt) simpleCopy<E>(sp.recv + sp.off * sizeof(E), false, nullptr, false,
-                                simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, sp.cnt);
+                                simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, sp.cnt,
+                                chk ? &sh.sumIn[j] : nullptr);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slots are read: they may be refilled
     __syncthreads();
+    if (chk && tid < n && tid != me)
+      simpleCheckSum(a, simpleHdr(a, me, 1, sh.cnt[kCtAgRecv][tid] % slots, tid, g), sh.cnt[kCtAgRecv][tid] + 1,
+                     sh.sumIn[tid], tid);
     if (tid < n && tid != me)
       simplePost(simpleFlag(a.peerFlags[tid], kFlAgCredit, n, me, gm, g), ++sh.cnt[kCtAgRecv][tid]);
     __syncthreads();
@@ -545,10 +673,12 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
   simpleLoadCounters(a, sh, g);
   uint64_t* const myFlags = a.peerFlags[me];
   const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
+  const bool chk = a.checkSlices != 0;   // NBX_CHECK_SLICES: per hop, sumIn[1] = read, sumOut[0] = pushed
   // thread 0 waits for what a hop needs: the left neighbour's slice (recvFrom)
   // and free slots at the right neighbour (RS region: pushRs, AG region: pushAg)
   auto hopWait = [&](int recvRegion, bool pushRs, bool pushAg) {
     if (tid == 0) {
+      if (chk) sh.sumIn[1] = sh.sumOut[0] = 0;
       if (recvRegion >= 0) {
         const int fl = recvRegion == 0 ? kFlRsReady : kFlAgReady;
         const int ct = recvRegion == 0 ? kCtRsRecv : kCtAgRecv;
@@ -568,17 +698,29 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
     __syncthreads();
     return sh.fail == 0;
   };
-  // the plan headers of this hop's pushes, before the drain that publishes them
+  // the plan headers (and slice sums) of this hop's pushes, before the drain that publishes them
   auto hopStamp = [&](bool pushRs, bool pushAg) {
+    if (chk) __syncthreads();   // every lane's hash is in
     if (tid == 0) {
-      if (pushRs)
-        simpleStamp(simpleHdr(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), a, sh.cnt[kCtRsSent][right] + 1);
-      if (pushAg)
-        simpleStamp(simpleHdr(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g), a, sh.cnt[kCtAgSent][right] + 1);
+      if (pushRs) {
+        uint64_t* h = simpleHdr(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g);
+        simpleStamp(h, a, sh.cnt[kCtRsSent][right] + 1);
+        if (chk) simpleStampSum(h, a, g, sh.cnt[kCtRsSent][right] + 1, sh.sumOut[0]);
+      }
+      if (pushAg) {
+        uint64_t* h = simpleHdr(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g);
+        simpleStamp(h, a, sh.cnt[kCtAgSent][right] + 1);
+        if (chk) simpleStampSum(h, a, g, sh.cnt[kCtAgSent][right] + 1, sh.sumOut[0]);
+      }
     }
   };
   auto hopPost = [&](int recvRegion, bool pushRs, bool pushAg) {
     if (tid == 0) {
+      if (chk && recvRegion >= 0) {   // after the drain: the slot read is what the left neighbour stamped
+        const int ct = recvRegion == 0 ? kCtRsRecv : kCtAgRecv;
+        simpleCheckSum(a, simpleHdr(a, me, recvRegion, sh.cnt[ct][left] % slots, left, g), sh.cnt[ct][left] + 1,
+                       sh.sumIn[1], left);
+      }
       if (recvRegion == 0) simplePost(simpleFlag(a.peerFlags[left], kFlRsCredit, n, me, gm, g), ++sh.cnt[kCtRsRecv][left]);
       if (recvRegion == 1) simplePost(simpleFlag(a.peerFlags[left], kFlAgCredit, n, me, gm, g), ++sh.cnt[kCtAgRecv][left]);
       if (pushRs) simplePost(simpleFlag(a.peerFlags[right], kFlRsReady, n, me, gm, g), ++sh.cnt[kCtRsSent][right]);
@@ -597,7 +739,8 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
       char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : sp.recv + off * sizeof(E);
       if (pos == 0) {
-        if (cnt) simpleCopy<E>(out, push, nullptr, false, sp.send + off * sizeof(E), false, cnt);
+        if (cnt) simpleCopy<E>(out, push, nullptr, false, sp.send + off * sizeof(E), false, cnt,
+                               chk ? &sh.sumOut[0] : nullptr);
       } else if (cnt) {
         if (tid == 0) {
           sh.src[0] = sp.send + off * sizeof(E);
@@ -606,7 +749,8 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
         }
         __syncthreads();
         const bool aligned = simpleAligned(sp.send + off * sizeof(E)) && simpleAligned(out);
-        simpleFold<Fn>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned);
+        simpleFold<Fn>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned,
+                       chk ? sh.sumIn : nullptr, chk ? &sh.sumOut[0] : nullptr);
       }
       hopStamp(push, false);
       simpleDrain();
@@ -618,7 +762,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       const SimpleSpan sp = simpleSlice<E>(a, segs, left, k, g, grid);
       if (!hopWait(-1, true, false)) return;
       if (sp.cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr,
-                                false, sp.send + sp.off * sizeof(E), false, sp.cnt);
+                                false, sp.send + sp.off * sizeof(E), false, sp.cnt, chk ? &sh.sumOut[0] : nullptr);
       hopStamp(true, false);
       simpleDrain();
       hopPost(-1, true, false);
@@ -643,7 +787,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
         const bool aligned = simpleAligned(sh.src[0]) && simpleAligned(sh.dst[0]);
         // the last hop stores the caller's output (and pushes the AG start); others push the partial
         simpleFold<Fn>(fn, sh.src, 2, 2ull, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, last ? 2ull : 1ull,
-                       cnt, aligned);
+                       cnt, aligned, chk ? sh.sumIn : nullptr, chk ? &sh.sumOut[0] : nullptr);
       }
       hopStamp(!last, last && ar);
       simpleDrain();
@@ -659,7 +803,12 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       if (sp.cnt)
         simpleCopy<E>(sp.recv + sp.off * sizeof(E), false,
                       fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr, true,
-                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, sp.cnt);
+                      simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, sp.cnt,
+                      chk ? &sh.sumIn[1] : nullptr);
+      if (chk) {   // the forwarded slice is the slice read
+        __syncthreads();
+        if (tid == 0) sh.sumOut[0] = sh.sumIn[1];
+      }
       hopStamp(false, fwd);
       simpleDrain();
       hopPost(1, false, fwd);

@@ -260,10 +260,10 @@ def comm_settings(nbx, comm) -> dict:
     """The communicator's transport settings (nbxDebugCommSettings) by name."""
     import ctypes
     lib = nbx.load_library()
-    out = (ctypes.c_int64 * 10)()
-    k = lib.nbxDebugCommSettings(comm.handle, out, 10)
+    out = (ctypes.c_int64 * 11)()
+    k = lib.nbxDebugCommSettings(comm.handle, out, 11)
     names = ["llMax", "l128Max", "sliceBytes", "slots", "simpleGrid", "llGridCap", "l128GridCap", "groupBatch",
-             "ipcRepairs", "checkPlans"]
+             "ipcRepairs", "checkPlans", "checkSlices"]
     return {names[j]: int(out[j]) for j in range(max(k, 0))}
 
 

@@ -2129,3 +2129,125 @@ def test_multiprocess_ll_plan_mismatch_fails_loudly(nbx, monkeypatch, proto, cnt
     remote = int(nbx.ncclResult.ncclRemoteError)
     assert all(res[r]["err"] == remote for r in range(2)), res
     assert all("different plan" in res[r]["msg"] for r in range(2)), res
+
+
+# ---------------------------------------------------------------------------
+# Simple slice checksums (NBX_CHECK_SLICES): every staging slice carries a hash
+# of its elements that the consumer recomputes from what it read.
+
+SLICE_CASES = [  # (kind, dtype, op, count, byte offset): pack and element paths, fold and copy, every kind
+    ("ar", 7, 0, 1100000, 0), ("ar", 2, 2, 1000003, 0), ("ar", 7, 0, 300000, 4), ("ar", 6, 4, 700001, 2),
+    ("ar", 9, 0, 650000, 0), ("ar", 0, 3, 2500001, 1), ("ar", 8, 1, 200001, 0), ("ar", 11, 0, 1300001, 0),
+    ("rs", 7, 4, 1048577, 0), ("rs", 4, 2, 150000, 8), ("red", 7, 0, 300001, 0), ("red", 2, 3, 500000, 4),
+]
+
+
+def _child_slices(uid_bytes, rank, n, q, iters=2):
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        settings = mp_diag.comm_settings(nbx, comm)
+        st = torch.cuda.current_stream().cuda_stream
+        out = {}
+        for it in range(iters):
+            keep = []
+            for i, (kind, dtype, op, count, shift) in enumerate(SLICE_CASES):
+                x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
+                tx = torch.zeros(x.size + 16, dtype=torch.uint8, device="cuda")
+                tx[shift:shift + x.size] = torch.from_numpy(x.copy()).cuda()
+                out_bytes = x.size // n if kind == "rs" else x.size
+                ty = torch.zeros(out_bytes + 16, dtype=torch.uint8, device="cuda")
+                sp, rp = tx.data_ptr() + shift, ty.data_ptr() + shift
+                if kind == "ar":
+                    comm.all_reduce(sp, rp, count, dtype, op, st)
+                elif kind == "rs":
+                    comm.reduce_scatter(sp, rp, count, dtype, op, st)
+                else:
+                    comm.reduce(sp, rp, count, dtype, op, _ll_root(i, n), st)
+                keep.append((i, ty, tx, shift, out_bytes))   # no host sync between calls
+            torch.cuda.synchronize()
+            for i, ty, _tx, shift, nb in keep:
+                out[(it, i)] = ty[shift:shift + nb].cpu().numpy().copy()
+        err = comm.async_error()
+        msg = (lib.ncclGetLastError(None) or b"").decode(errors="replace")
+        comm.abort() if err else comm.destroy()
+        q.put((rank, "ok", {"out": out, "err": err, "msg": msg, "settings": settings}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("n,algo", [(3, ""), (4, "Ring"), (8, "")])
+def test_multiprocess_simple_slice_checksums(nbx, oracle, monkeypatch, n, algo):
+    """NBX_CHECK_SLICES=1 on the Simple direct and ring schedules: every
+    producer's stamped sum equals what its consumers recompute (no false
+    alarm on any path — 16-B packs, element tails, misaligned buffers, every
+    element width, fold and copy hops), and the outputs stay bit-exact."""
+    monkeypatch.setenv("NBX_CHECK_SLICES", "1")
+    monkeypatch.setenv("NCCL_PROTO", "Simple")
+    monkeypatch.setenv("NCCL_ALGO", algo)
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    res = _run_ranks(nbx, n, _child_slices)
+    for r in range(n):
+        assert res[r]["err"] == 0, (r, res[r]["msg"])
+        assert res[r]["settings"].get("checkSlices") == 1
+    failures = []
+    for i, (kind, dtype, op, count, shift) in enumerate(SLICE_CASES):
+        xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        st = oracle.NP_STORAGE[dtype]
+        eb = np.dtype(st).itemsize
+        kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+        root = _ll_root(i, n)
+        if algo == "Ring" and kind != "ar":
+            continue   # ring ReduceScatter / Reduce fold in NCCL's chain order: test_multiprocess_ring_fifo_*
+        exp = {}
+        if kind == "ar":
+            full = np.empty(count, dtype=st)
+            for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+                if hi > lo:
+                    order = [(c + 1 + k) % n for k in range(n)]
+                    full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg, **kw)[0]
+            exp = {r: full for r in range(n)}
+        elif kind == "rs":
+            for r in range(n):
+                order = [(r + 1 + k) % n for k in range(n)]
+                exp[r] = oracle.reduce_multi([xs[j][r * count:(r + 1) * count] for j in order], dtype, devop, arg,
+                                             **kw)[0]
+        else:
+            order = [(root + 1 + k) % n for k in range(n)]
+            exp[root] = oracle.reduce_multi([xs[j] for j in order], dtype, devop, arg, **kw)[0]
+        for it in range(2):
+            for r, e in exp.items():
+                got = res[r]["out"][(it, i)]
+                if not np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)):
+                    failures.append((f"slice-check case {i} {SLICE_CASES[i]} iteration {it}", kind, dtype, op, count,
+                                     r, got, xs, res[r]["settings"], root))
+    mp_diag.raise_collective_failures(oracle, failures, n, what=f"NBX_CHECK_SLICES=1 NCCL_ALGO={algo or 'direct'}: ")
+
+
+@pytest.mark.parametrize("algo", ["", "Ring"])
+def test_multiprocess_simple_slice_checksum_catches_a_wrong_slice(nbx, monkeypatch, algo):
+    """The negative case: rank 1's workgroup 0 stamps a wrong sum
+    (NBX_DEBUG_SLICE_FAULT=1), as a slice whose bytes changed between the
+    producer's stores and the consumer's loads would read. Its consumers fail
+    the call loudly — ncclRemoteError, the check named with the peer, the slot
+    use and both sums — instead of returning a result nobody verified."""
+    monkeypatch.setenv("NBX_CHECK_SLICES", "1")
+    monkeypatch.setenv("NBX_DEBUG_SLICE_FAULT", "1")
+    monkeypatch.setenv("NCCL_PROTO", "Simple")
+    monkeypatch.setenv("NCCL_ALGO", algo)
+    monkeypatch.setenv("NCCL_DEBUG", "WARN")
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "10")
+    res = _run_ranks(nbx, 3, _child_slices, 1)
+    remote = int(nbx.ncclResult.ncclRemoteError)
+    flagged = [r for r in range(3) if res[r]["err"] == remote]
+    assert flagged, {r: (res[r]["err"], res[r]["msg"]) for r in range(3)}
+    assert any("Simple slice checksum" in res[r]["msg"] and "from peer 1" in res[r]["msg"] for r in flagged), \
+        {r: res[r]["msg"] for r in range(3)}
