@@ -121,6 +121,8 @@ struct KernelSet {
   const void* ll128x2Chk;
   const void* simple;               // Simple protocol, direct schedule over init-mapped staging (nbx_simple.h)
   const void* simpleRing;           // Simple protocol, ring schedule over init-mapped staging (nbx_simple.h)
+  const void* simpleChk;            // the same two with slice checksums (NBX_CHECK_SLICES)
+  const void* simpleRingChk;
   const void* batch[kMaxKSrcs];     // batched buckets (kReduceBatch), [nSrcs-1]
   const void* batchList[kMaxKSrcs]; // batched buckets from a work-list table (kReduceBatchList), [nSrcs-1]
   int unroll[kMaxKSrcs];            // big-tile packs per lane per source

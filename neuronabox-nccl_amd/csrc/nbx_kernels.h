@@ -676,8 +676,10 @@ KernelSet makeKernelSetImpl(std::integer_sequence<int, I...>) {
   ks.llChk = (const void*)&kLLColl<Fn, true>;
   ks.ll128Chk = (const void*)&kLL128Coll<Fn, true>;
   ks.ll128x2Chk = (const void*)&kLL128AllReduce2<Fn, true>;
-  ks.simple = (const void*)&kSimpleColl<Fn>;
-  ks.simpleRing = (const void*)&kSimpleRing<Fn>;
+  ks.simple = (const void*)&kSimpleColl<Fn, false>;
+  ks.simpleRing = (const void*)&kSimpleRing<Fn, false>;
+  ks.simpleChk = (const void*)&kSimpleColl<Fn, true>;
+  ks.simpleRingChk = (const void*)&kSimpleRing<Fn, true>;
   ks.eltBytes = (int)sizeof(typename Fn::Elt);
   ks.bigBlocksPerCU = Fn::kBigBlocksPerCU;
   ks.valid = 1;

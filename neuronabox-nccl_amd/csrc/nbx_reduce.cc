@@ -493,7 +493,7 @@ ncclResult_t launchSimple(ncclDataType_t dt, const nbxDevRedOpFull& op, SimpleAr
                           hipStream_t stream) {
   if ((int)dt < 0 || (int)dt >= kNumTypes || op.op < 0 || op.op >= kNumDevOps) return ncclInvalidArgument;
   const KernelSet& ks = table()[(int)dt][op.op];
-  const void* k = ring ? ks.simpleRing : ks.simple;
+  const void* k = a.checkSlices ? (ring ? ks.simpleRingChk : ks.simpleChk) : (ring ? ks.simpleRing : ks.simple);
   if (!ks.valid || k == nullptr || grid < 1 || grid > (unsigned)a.gridMax || a.gridMax > kSimpleMaxGrid ||
       a.nRanks < 2 || a.nRanks > kSimpleMaxRanks)
     return ncclInvalidArgument;

@@ -288,10 +288,10 @@ __device__ __forceinline__ SimpleSpan simpleSlice(const SimpleArgs& a, const Sim
 // 16-B packs when every pointer is 16-B aligned). sys0 / sys1: the
 // destination is staging (write-through stores), else a caller buffer; sysSrc:
 // the source is staging (system-scope loads).
-// sum (NBX_CHECK_SLICES, else nullptr): an LDS word that receives the slice
-// hash of the elements copied (the staging source read, or the staging
-// destination written: the same bytes).
-template <class E>
+// CHK (the NBX_CHECK_SLICES kernels): `sum` is an LDS word that receives the
+// slice hash of the elements copied (the staging source read, or the staging
+// destination written: the same bytes); the default kernels compile none of it.
+template <class E, bool CHK = false>
 __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool sys1, const void* src, bool sysSrc,
                                            uint64_t nElts, uint32_t* sum = nullptr) {
   constexpr int EPP = 16 / (int)sizeof(E);
@@ -313,7 +313,7 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
       for (int u = 0; u < U; u++) {
         if (p + (uint64_t)u * kBlock < nPk) {
           const uint64_t q = p + (uint64_t)u * kBlock;
-          if (sum) h += slicePackHash<E>(v[u], q * EPP);
+          if constexpr (CHK) h += slicePackHash<E>(v[u], q * EPP);
           if (sys0) stSys(rd0, q, v[u]);
           else stPack((u32x4*)d0 + q, v[u]);
           if (d1) {
@@ -327,7 +327,7 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
   }
   for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
     const E v = sysSrc ? ldSysElt((const E*)src + e) : ldElt((const E*)src + e);
-    if (sum) h += sliceEltHash(v, e);
+    if constexpr (CHK) h += sliceEltHash(v, e);
     if (sys0) stSysElt((E*)d0 + e, v);
     else ((E*)d0)[e] = v;
     if (d1) {
@@ -335,7 +335,7 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
       else ((E*)d1)[e] = v;
     }
   }
-  if (sum) atomicAdd(sum, h);
+  if constexpr (CHK) atomicAdd(sum, h);
 }
 
 // Workgroup fold of nElts elements: acc = pre?(src[0]); acc = Fn(acc, pre?(src[q]))
@@ -346,10 +346,11 @@ __device__ __forceinline__ void simpleCopy(void* d0, bool sys0, void* d1, bool s
 // U packs per lane per source, G = 32 / U sources' loads in flight together
 // (32 packs = 512 B per lane, as the 8-source big tile): deep unrolling for
 // the 2-source ring hops and small rank counts, source groups for many ranks.
-// srcSums / dstSum (NBX_CHECK_SLICES, else nullptr): LDS words that receive
-// the slice hash of each staging source read (indexed by fold position) and
-// of the result stored into the staging destinations.
-template <class Fn, int U>
+// CHK (the NBX_CHECK_SLICES kernels): srcSums / dstSum are LDS words that
+// receive the slice hash of each staging source read (indexed by fold
+// position; nullptr: none read) and of the result stored into the staging
+// destinations (nullptr: none written).
+template <class Fn, int U, bool CHK>
 __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t sysSrcMask,
                                             uint64_t preMask, bool doPost, char* const* dsts, int nDsts,
                                             uint64_t sysMask, uint64_t nElts, bool aligned, uint32_t* srcSums,
@@ -378,7 +379,7 @@ __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* src
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (srcSums) {
+        if (CHK && srcSums) {
 #pragma unroll
           for (int s = 0; s < G; s++) {
             if (q0 + s < nSrcs && ((sysSrcMask >> (q0 + s)) & 1u)) {
@@ -407,7 +408,7 @@ __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* src
         if (p + (uint64_t)u * kBlock < nPk) {
           u32x4 r = acc[u];
           if constexpr (Fn::kHasPost) if (doPost) r = fn.postPack(r);
-          if (dstSum) hd += slicePackHash<E>(r, (p + (uint64_t)u * kBlock) * EPP);
+          if constexpr (CHK) if (dstSum) hd += slicePackHash<E>(r, (p + (uint64_t)u * kBlock) * EPP);
           for (int d = 0; d < nDsts; d++) {
             const uint64_t q = p + (uint64_t)u * kBlock;
             if ((sysMask >> d) & 1u) stSys(sysRsrc(dsts[d], nElts * sizeof(E)), q, r);
@@ -420,37 +421,37 @@ __device__ __forceinline__ void simpleFoldU(const Fn& fn, const char* const* src
   }
   for (uint64_t e = done + threadIdx.x; e < nElts; e += kBlock) {
     E acc = (sysSrcMask & 1u) ? ldSysElt((const E*)srcs[0] + e) : ldElt((const E*)srcs[0] + e);
-    if (srcSums && (sysSrcMask & 1u)) atomicAdd(&srcSums[0], sliceEltHash(acc, e));
+    if constexpr (CHK) if (srcSums && (sysSrcMask & 1u)) atomicAdd(&srcSums[0], sliceEltHash(acc, e));
     if constexpr (Fn::kHasPre) if (preMask & 1u) acc = fn.pre(acc);
     for (int q = 1; q < nSrcs; q++) {
       E x = ((sysSrcMask >> q) & 1u) ? ldSysElt((const E*)srcs[q] + e) : ldElt((const E*)srcs[q] + e);
-      if (srcSums && ((sysSrcMask >> q) & 1u)) atomicAdd(&srcSums[q], sliceEltHash(x, e));
+      if constexpr (CHK) if (srcSums && ((sysSrcMask >> q) & 1u)) atomicAdd(&srcSums[q], sliceEltHash(x, e));
       if constexpr (Fn::kHasPre) if ((preMask >> q) & 1u) x = fn.pre(x);
       acc = fn.red(acc, x);
     }
     if constexpr (Fn::kHasPost) if (doPost) acc = fn.post(acc);
-    if (dstSum) hd += sliceEltHash(acc, e);
+    if constexpr (CHK) if (dstSum) hd += sliceEltHash(acc, e);
     for (int d = 0; d < nDsts; d++) {
       if ((sysMask >> d) & 1u) stSysElt((E*)dsts[d] + e, acc);
       else ((E*)dsts[d])[e] = acc;
     }
   }
-  if (dstSum) atomicAdd(dstSum, hd);
+  if constexpr (CHK) if (dstSum) atomicAdd(dstSum, hd);
 }
 
-template <class Fn>
+template <class Fn, bool CHK = false>
 __device__ __forceinline__ void simpleFold(const Fn& fn, const char* const* srcs, int nSrcs, uint64_t sysSrcMask,
                                            uint64_t preMask, bool doPost, char* const* dsts, int nDsts,
                                            uint64_t sysMask, uint64_t nElts, bool aligned,
                                            uint32_t* srcSums = nullptr, uint32_t* dstSum = nullptr) {
   if (nSrcs <= 2)
-    simpleFoldU<Fn, 16>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
+    simpleFoldU<Fn, 16, CHK>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
                         dstSum);
   else if (nSrcs <= 4)
-    simpleFoldU<Fn, 8>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
+    simpleFoldU<Fn, 8, CHK>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
                        dstSum);
   else
-    simpleFoldU<Fn, 4>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
+    simpleFoldU<Fn, 4, CHK>(fn, srcs, nSrcs, sysSrcMask, preMask, doPost, dsts, nDsts, sysMask, nElts, aligned, srcSums,
                        dstSum);
 }
 
@@ -488,7 +489,7 @@ __device__ __forceinline__ void simpleStoreCounters(const SimpleArgs& a, SimpleS
 // The direct schedule as run by workgroup g of a `grid`-workgroup launch
 // (kSimpleColl: the launch's own block index; kSimpleCollFused: one launch
 // running every rank of a one-process rig, for the PMC passes).
-template <class Fn>
+template <class Fn, bool CHK>
 __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const SimpleSeg* segs, int g, int grid) {
   using E = typename Fn::Elt;
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
@@ -504,7 +505,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
   const bool gathers = ar || (red && me == a.root);    // C runs here
   const int first = ((red ? a.root : me) + 1) % n;      // fold order of block `me`
   auto pushTarget = [&](int p) { return p != me && (ar || (red && p == a.root)); };
-  const bool chk = a.checkSlices != 0;                  // NBX_CHECK_SLICES (uniform)
+  constexpr bool chk = CHK;                             // the NBX_CHECK_SLICES kernel
 
   auto phaseA = [&](uint64_t k) -> bool {
     // ---- A: slice g of block j into rank j's RS region, slot rsSent[j] % slots
@@ -520,7 +521,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
       const SimpleSpan sp = simpleSlice<E>(a, segs, j, k, g, grid);
-      if (sp.cnt) simpleCopy<E>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
+      if (sp.cnt) simpleCopy<E, CHK>(simpleStage(a, j, 0, sh.cnt[kCtRsSent][j] % slots, me, g), true, nullptr, false,
                                 sp.send + sp.off * sizeof(E), false, sp.cnt, chk ? &sh.sumOut[j] : nullptr);
     }
     if (chk) __syncthreads();   // every lane's hash is in
@@ -576,10 +577,10 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
       const int ownPos = (me - first + n) % n;
       const uint64_t sysSrc = ~(1ull << ownPos);
       if (xport)
-        simpleFold<Fn>(fn, sh.src + ownPos, 1, 0ull, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned, nullptr,
+        simpleFold<Fn, CHK>(fn, sh.src + ownPos, 1, 0ull, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned, nullptr,
                        chk ? &sh.sumOut[0] : nullptr);
       else
-        simpleFold<Fn>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned,
+        simpleFold<Fn, CHK>(fn, sh.src, n, sysSrc, ~0ull, true, sh.dst, nDsts, sysMask, cnt, aligned,
                        chk ? sh.sumIn : nullptr, chk ? &sh.sumOut[0] : nullptr);
     }
     if (chk) {
@@ -614,7 +615,7 @@ __device__ __forceinline__ void simpleCollBody(const SimpleArgs& a, const Simple
     for (int q = 1; q < n; q++) {
       const int j = (me + q) % n;
       const SimpleSpan sp = simpleSlice<E>(a, segs, j, k, g, grid);
-      if (sp.cnt) simpleCopy<E>(sp.recv + sp.off * sizeof(E), false, nullptr, false,
+      if (sp.cnt) simpleCopy<E, CHK>(sp.recv + sp.off * sizeof(E), false, nullptr, false,
                                 simpleStage(a, me, 1, sh.cnt[kCtAgRecv][j] % slots, j, g), true, sp.cnt,
                                 chk ? &sh.sumIn[j] : nullptr);
     }
@@ -652,9 +653,9 @@ __device__ __forceinline__ const SimpleSeg* simpleKernargSegs() {
   return (const SimpleSeg*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(SimpleArgs, seg));
 }
 
-template <class Fn>
+template <class Fn, bool CHK>
 __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
-  simpleCollBody<Fn>(a, simpleKernargSegs(), (int)blockIdx.x, (int)gridDim.x);
+  simpleCollBody<Fn, CHK>(a, simpleKernargSegs(), (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Ring schedule through the right neighbour's staging. AllReduce /
@@ -662,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void kSimpleColl(SimpleArgs a) {
 // finished (PostOp) at c; AllReduce then forwards the finished chunk around
 // the ring (all_reduce.h:60-93). Reduce: the chain root+1 -> ... -> root over
 // the one block of the message (reduce.h:44-67).
-template <class Fn>
+template <class Fn, bool CHK>
 __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const SimpleSeg* segs, int g, int grid) {
   using E = typename Fn::Elt;
   const Fn fn(a.argPtr != nullptr ? (uint64_t) * (const E*)a.argPtr : a.arg);
@@ -673,7 +674,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
   simpleLoadCounters(a, sh, g);
   uint64_t* const myFlags = a.peerFlags[me];
   const bool ar = a.mode == kSimpleAllReduce, red = a.mode == kSimpleReduce;
-  const bool chk = a.checkSlices != 0;   // NBX_CHECK_SLICES: per hop, sumIn[1] = read, sumOut[0] = pushed
+  constexpr bool chk = CHK;   // the NBX_CHECK_SLICES kernel: per hop, sumIn[1] = read, sumOut[0] = pushed
   // thread 0 waits for what a hop needs: the left neighbour's slice (recvFrom)
   // and free slots at the right neighbour (RS region: pushRs, AG region: pushAg)
   auto hopWait = [&](int recvRegion, bool pushRs, bool pushAg) {
@@ -739,7 +740,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       if (!hopWait(pos == 0 ? -1 : 0, push, false)) return;
       char* out = push ? simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g) : sp.recv + off * sizeof(E);
       if (pos == 0) {
-        if (cnt) simpleCopy<E>(out, push, nullptr, false, sp.send + off * sizeof(E), false, cnt,
+        if (cnt) simpleCopy<E, CHK>(out, push, nullptr, false, sp.send + off * sizeof(E), false, cnt,
                                chk ? &sh.sumOut[0] : nullptr);
       } else if (cnt) {
         if (tid == 0) {
@@ -749,7 +750,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
         }
         __syncthreads();
         const bool aligned = simpleAligned(sp.send + off * sizeof(E)) && simpleAligned(out);
-        simpleFold<Fn>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned,
+        simpleFold<Fn, CHK>(fn, sh.src, 2, 2ull, pos == 1 ? 3u : 1u, !push, sh.dst, 1, push ? 1ull : 0ull, cnt, aligned,
                        chk ? sh.sumIn : nullptr, chk ? &sh.sumOut[0] : nullptr);
       }
       hopStamp(push, false);
@@ -761,7 +762,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
     {
       const SimpleSpan sp = simpleSlice<E>(a, segs, left, k, g, grid);
       if (!hopWait(-1, true, false)) return;
-      if (sp.cnt) simpleCopy<E>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr,
+      if (sp.cnt) simpleCopy<E, CHK>(simpleStage(a, right, 0, sh.cnt[kCtRsSent][right] % slots, me, g), true, nullptr,
                                 false, sp.send + sp.off * sizeof(E), false, sp.cnt, chk ? &sh.sumOut[0] : nullptr);
       hopStamp(true, false);
       simpleDrain();
@@ -786,7 +787,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       if (cnt) {
         const bool aligned = simpleAligned(sh.src[0]) && simpleAligned(sh.dst[0]);
         // the last hop stores the caller's output (and pushes the AG start); others push the partial
-        simpleFold<Fn>(fn, sh.src, 2, 2ull, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, last ? 2ull : 1ull,
+        simpleFold<Fn, CHK>(fn, sh.src, 2, 2ull, st == 0 ? 3u : 1u, last, sh.dst, last && ar ? 2 : 1, last ? 2ull : 1ull,
                        cnt, aligned, chk ? sh.sumIn : nullptr, chk ? &sh.sumOut[0] : nullptr);
       }
       hopStamp(!last, last && ar);
@@ -801,7 +802,7 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
       const SimpleSpan sp = simpleSlice<E>(a, segs, c, k, g, grid);
       if (!hopWait(1, false, fwd)) return;
       if (sp.cnt)
-        simpleCopy<E>(sp.recv + sp.off * sizeof(E), false,
+        simpleCopy<E, CHK>(sp.recv + sp.off * sizeof(E), false,
                       fwd ? simpleStage(a, right, 1, sh.cnt[kCtAgSent][right] % slots, me, g) : nullptr, true,
                       simpleStage(a, me, 1, sh.cnt[kCtAgRecv][left] % slots, left, g), true, sp.cnt,
                       chk ? &sh.sumIn[1] : nullptr);
@@ -818,9 +819,9 @@ __device__ __forceinline__ void simpleRingBody(const SimpleArgs& a, const Simple
   mpArrive(a.order);
 }
 
-template <class Fn>
+template <class Fn, bool CHK>
 __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
-  simpleRingBody<Fn>(a, simpleKernargSegs(), (int)blockIdx.x, (int)gridDim.x);
+  simpleRingBody<Fn, CHK>(a, simpleKernargSegs(), (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Every rank of a one-process rig in ONE launch (workgroup b runs rank
@@ -831,8 +832,8 @@ __global__ __launch_bounds__(kBlock) void kSimpleRing(SimpleArgs a) {
 template <class Fn, bool RING>
 __global__ __launch_bounds__(kBlock) void kSimpleFused(const SimpleArgs* __restrict__ as, int grid) {
   const int r = (int)blockIdx.x / grid, g = (int)blockIdx.x % grid;
-  if (RING) simpleRingBody<Fn>(as[r], as[r].seg, g, grid);
-  else simpleCollBody<Fn>(as[r], as[r].seg, g, grid);
+  if (RING) simpleRingBody<Fn, false>(as[r], as[r].seg, g, grid);
+  else simpleCollBody<Fn, false>(as[r], as[r].seg, g, grid);
 }
 
 }  // namespace nbx

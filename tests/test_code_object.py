@@ -52,7 +52,7 @@ def test_all_kernels_present(kernels):
     shifted = [n for n in names if "kReduceShifted" in n]
     assert len(shifted) == 42 * (1 + 8)    # realigning kernels: run-time count, and one per source count 1..8
     simple = [n for n in names if "kSimpleColl" in n or "kSimpleRing" in n]
-    assert len(simple) == 42 * 2           # Simple protocol: direct and ring schedule per functor
+    assert len(simple) == 42 * 4           # Simple protocol: direct and ring schedule, default and slice-checking
 
 
 def test_no_scratch_and_vgpr_budget(kernels):
