@@ -376,7 +376,7 @@ def _child_ll(uid_bytes, rank, n, q, proto):
         import torch
         from tests.conftest import load_package
         nbx = load_package()
-        nbx.load_library()
+        lib = nbx.load_library()
         torch.cuda.set_device(0)
         comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
         settings = mp_diag.comm_settings(nbx, comm)
@@ -412,7 +412,8 @@ def _child_ll(uid_bytes, rank, n, q, proto):
             comm.all_reduce(tx.data_ptr(), ty.data_ptr(), 1024, 7, 0, st)
         torch.cuda.synchronize()
         us = (time.perf_counter() - t0) * 1e6 / 200
-        assert comm.async_error() == 0
+        err = comm.async_error()   # a device check that failed (NBX_CHECK_SLICES / plans) names itself here
+        assert err == 0, (err, (lib.ncclGetLastError(None) or b"").decode(errors="replace"))
         comm.destroy()
         q.put((rank, "ok", (out, us, settings)))
     except Exception:
@@ -420,14 +421,18 @@ def _child_ll(uid_bytes, rank, n, q, proto):
         q.put((rank, "error", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("n,proto", [(2, ""), (3, ""), (5, ""), (2, "LL128"), (3, "LL128"), (8, "")])
-def test_multiprocess_ll_protocol(nbx, oracle, n, proto, monkeypatch):
+@pytest.mark.parametrize("n,proto,checks", [(2, "", ""), (3, "", ""), (5, "", ""), (2, "LL128", ""), (3, "LL128", ""),
+                                            (8, "", ""), (8, "", "slices")])
+def test_multiprocess_ll_protocol(nbx, oracle, n, proto, checks, monkeypatch):
     """LL protocol (one kernel, {data, flag} 8-byte lines, no host exchange) for
     small, LL128 (120 payload bytes + flag per 128-byte line) for medium
     AllReduce / ReduceScatter / Reduce messages, misaligned buffers included,
     issued back to back without host synchronisation and interleaved with each
     other and with direct-path messages; bitwise equal to the direct schedule's
-    fold order. NCCL_PROTO=LL128 routes every message that fits through LL128."""
+    fold order. NCCL_PROTO=LL128 routes every message that fits through LL128.
+    checks="slices": the 8-rank run of GPUTEST_r05's red record with every
+    Simple hand-off verified by its slice checksum (NBX_CHECK_SLICES=1)."""
+    monkeypatch.setenv("NBX_CHECK_SLICES", "1" if checks == "slices" else "")
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     # all ranks share the test box's one GPU: keep every rank's LL128 grid
