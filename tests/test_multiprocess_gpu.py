@@ -2256,3 +2256,89 @@ def test_multiprocess_simple_slice_checksum_catches_a_wrong_slice(nbx, monkeypat
     assert flagged, {r: (res[r]["err"], res[r]["msg"]) for r in range(3)}
     assert any("Simple slice checksum" in res[r]["msg"] and "from peer 1" in res[r]["msg"] for r in flagged), \
         {r: res[r]["msg"] for r in range(3)}
+
+
+def _child_replay(uid_bytes, rank, n, q, case_ids, iters):
+    """LL_CASES[case_ids] back to back (no host sync inside an iteration), the
+    send and recv buffers inside 4 KiB 0xA5 canaries checked after every
+    iteration; returns every output."""
+    try:
+        import torch
+        from tests.conftest import load_package
+        nbx = load_package()
+        lib = nbx.load_library()
+        torch.cuda.set_device(0)
+        comm = nbx.Communicator.init_rank(n, nbx.ncclUniqueId.from_buffer_copy(uid_bytes), rank)
+        settings = mp_diag.comm_settings(nbx, comm)
+        st = torch.cuda.current_stream().cuda_stream
+        G = 4096
+        out, canary = {}, []
+        for it in range(iters):
+            keep = []
+            for i in case_ids:
+                kind, dtype, op, count, shift = LL_CASES[i]
+                x = _ll_input(kind, dtype, count, n, rank).view(np.uint8)
+                tx = torch.full((x.size + 16 + 2 * G,), 0xA5, dtype=torch.uint8, device="cuda")
+                tx[G:G + x.size + 16] = 0
+                tx[G + shift:G + shift + x.size] = torch.from_numpy(x.copy()).cuda()
+                nb = x.size // n if kind == "rs" else x.size
+                ty = torch.full((nb + 16 + 2 * G,), 0xA5, dtype=torch.uint8, device="cuda")
+                ty[G:G + nb + 16] = 0
+                sp, rp = tx.data_ptr() + G + shift, ty.data_ptr() + G + shift
+                if kind == "ar":
+                    comm.all_reduce(sp, rp, count, dtype, op, st)
+                elif kind == "rs":
+                    comm.reduce_scatter(sp, rp, count, dtype, op, st)
+                else:
+                    comm.reduce(sp, rp, count, dtype, op, _ll_root(i, n), st)
+                keep.append((i, tx, ty, shift, nb))
+            torch.cuda.synchronize()
+            for i, tx, ty, shift, nb in keep:
+                out[(it, i)] = ty[G + shift:G + shift + nb].cpu().numpy().copy()
+                for name, t in (("send", tx), ("recv", ty)):
+                    if not (bool((t[:G] == 0xA5).all()) and bool((t[t.numel() - G:] == 0xA5).all())):
+                        canary.append((it, i, name))
+        err = comm.async_error()
+        assert err == 0, (err, (lib.ncclGetLastError(None) or b"").decode(errors="replace"))
+        comm.destroy()
+        q.put((rank, "ok", {"out": out, "canary": canary, "settings": settings}))
+    except Exception:
+        import traceback
+        q.put((rank, "error", traceback.format_exc()))
+
+
+def test_multiprocess_gputest_r05_replay_cases_32_37(nbx, oracle, monkeypatch):
+    """the calls around GPUTEST_r05's red record — LL128
+    two-shot cases 32-34, Simple case 35 (misaligned fp32), Simple case 36
+    (int32 max, 1,000,003 elements: the wrong one), Simple case 37 (fp64) —
+    at 8 ranks sharing the GPU, back to back, 12 iterations; every output of
+    every rank bit-exact vs the oracle (described if not), and no byte outside
+    a call's own buffers written."""
+    monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
+    monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
+    monkeypatch.setenv("NBX_LL128_MAX_GRID", "16")
+    n, cases, iters = 8, list(range(32, 38)), 12
+    res = _run_ranks(nbx, n, _child_replay, cases, iters)
+    assert not any(res[r]["canary"] for r in range(n)), {r: res[r]["canary"][:4] for r in range(n)}
+    failures = []
+    for i in cases:
+        kind, dtype, op, count, shift = LL_CASES[i]
+        xs = [_ll_input(kind, dtype, count, n, r) for r in range(n)]
+        devop, arg = oracle.host_to_dev_redop(op, dtype, n)
+        st = oracle.NP_STORAGE[dtype]
+        eb = np.dtype(st).itemsize
+        kw = dict(n_pre_op_srcs=n, post_op=devop == 4)
+        assert kind == "ar"
+        full = np.empty(count, dtype=st)
+        for c, (lo, hi) in enumerate(_blocks(count, eb, n)):
+            if hi > lo:
+                order = [(c + 1 + k) % n for k in range(n)]
+                full[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], dtype, devop, arg, **kw)[0]
+        want = np.ascontiguousarray(full).view(np.uint8)
+        for it in range(iters):
+            for r in range(n):
+                got = res[r]["out"][(it, i)]
+                if not np.array_equal(got, want):
+                    failures.append((f"replay case {i} {LL_CASES[i]} iteration {it}", kind, dtype, op, count, r,
+                                     got, xs, res[r]["settings"], None))
+    mp_diag.raise_collective_failures(oracle, failures, n, what="GPUTEST_r05 replay: ")
