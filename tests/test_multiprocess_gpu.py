@@ -422,7 +422,7 @@ def _child_ll(uid_bytes, rank, n, q, proto):
 
 
 @pytest.mark.parametrize("n,proto,checks", [(2, "", ""), (3, "", ""), (5, "", ""), (2, "LL128", ""), (3, "LL128", ""),
-                                            (8, "", ""), (8, "", "slices")])
+                                            (8, "", ""), (8, "", "slices"), (8, "", "ring")])
 def test_multiprocess_ll_protocol(nbx, oracle, n, proto, checks, monkeypatch):
     """LL protocol (one kernel, {data, flag} 8-byte lines, no host exchange) for
     small, LL128 (120 payload bytes + flag per 128-byte line) for medium
@@ -431,8 +431,12 @@ def test_multiprocess_ll_protocol(nbx, oracle, n, proto, checks, monkeypatch):
     other and with direct-path messages; bitwise equal to the direct schedule's
     fold order. NCCL_PROTO=LL128 routes every message that fits through LL128.
     checks="slices": the 8-rank run of GPUTEST_r05's red record with every
-    Simple hand-off verified by its slice checksum (NBX_CHECK_SLICES=1)."""
+    Simple hand-off verified by its slice checksum (NBX_CHECK_SLICES=1);
+    checks="ring": the same with the Simple-sized calls on the ring schedule
+    (NCCL_ALGO=Ring: for these commutative ops NCCL's ring chain gives the
+    direct schedule's bits)."""
     monkeypatch.setenv("NBX_CHECK_SLICES", "1" if checks == "slices" else "")
+    monkeypatch.setenv("NCCL_ALGO", "Ring" if checks == "ring" else "")
     monkeypatch.setenv("NBX_BOOTSTRAP_TIMEOUT", "60")
     monkeypatch.setenv("NBX_TIMEOUT_SEC", "60")
     # all ranks share the test box's one GPU: keep every rank's LL128 grid
