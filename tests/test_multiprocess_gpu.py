@@ -358,7 +358,8 @@ LL_CASES = [
 def _ll_input(kind, dtype, count, n, r):
     from oracle import oracle
     total = count * n if kind == "rs" else count
-    return oracle.random_inputs(dtype, 8, total, seed=77 + dtype + count)[r]
+    # source s is seeded by seed + s alone: ranks 0-7 get the same input at any n
+    return oracle.random_inputs(dtype, max(8, n), total, seed=77 + dtype + count)[r]
 
 
 def _ll_root(i, n):
