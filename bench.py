@@ -86,6 +86,16 @@ def _load_package():
     return lp()
 
 
+def _build_stamp(nbx) -> dict:
+    """Which build of libnbxccl.so produced the line (the stamp build() wrote,
+    neuronabox-nccl_amd/lib/build_info.json) and whether the library and the
+    sources on this box are still that build."""
+    bi = nbx.build_info()
+    rec = bi["recorded"] or {}
+    return {"sources_sha256": rec.get("sources_sha256"), "lib_sha256": rec.get("lib_sha256"),
+            "lib_matches": bi["lib_matches"], "sources_match": bi["sources_match"]}
+
+
 def _dist_init():
     """One process per GPU (torch.distributed.run env). The process group is the
     control plane only (barrier + max-over-ranks): RCCL ("nccl") by default,
@@ -1064,6 +1074,7 @@ def headline(args, world: int, rank: int, local: int) -> dict:
                      "alg_bytes_per_launch": ALG_BYTES},
         "cpu_baseline": None,
         "collective": None,
+        "build": _build_stamp(nbx),
     }
     if ceil:
         rf = result["roofline"]

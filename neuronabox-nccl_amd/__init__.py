@@ -217,6 +217,65 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     return lib
 
 
+# Build provenance: build() stamps lib/build_info.json with a digest of the
+# sources make built the library from and of the library itself; the bench
+# line and smoke() report whether the library on disk is still that build and
+# the sources beside it are still those sources (a stale or foreign .so shows).
+BUILD_INFO_PATH = os.path.join(_HERE, "lib", "build_info.json")
+INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
+_SOURCE_SUFFIXES = (".cc", ".h", ".hip", ".inc")
+
+
+def _file_sha256(path: str) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for block in iter(lambda: f.read(1 << 20), b""):
+            h.update(block)
+    return h.hexdigest()
+
+
+def source_digest(csrc_dir: str = CSRC_DIR, include_dir: str = INCLUDE_DIR) -> tuple:
+    """(sha256 over every library source by name and content, file count):
+    csrc/*.{cc,h,hip,inc}, csrc/Makefile and include/*.h."""
+    import hashlib
+    files = [("csrc", csrc_dir, f) for f in sorted(os.listdir(csrc_dir))
+             if f.endswith(_SOURCE_SUFFIXES) or f == "Makefile"]
+    files += [("include", include_dir, f) for f in sorted(os.listdir(include_dir)) if f.endswith(".h")]
+    h = hashlib.sha256()
+    for tag, d, f in files:
+        h.update(f"{tag}/{f}".encode() + b"\0")
+        h.update(_file_sha256(os.path.join(d, f)).encode() + b"\n")
+    return h.hexdigest(), len(files)
+
+
+def write_build_info(path: str = BUILD_INFO_PATH) -> dict:
+    """Record the digests after a successful make (called by build())."""
+    import json
+    src, nfiles = source_digest()
+    lib = library_path()
+    info = {"sources_sha256": src, "source_files": nfiles, "lib_sha256": _file_sha256(lib),
+            "lib_bytes": os.path.getsize(lib), "arch": "gfx950"}
+    with open(path, "w") as f:
+        json.dump(info, f, indent=1)
+    return info
+
+
+def build_info(path: str = BUILD_INFO_PATH) -> dict:
+    """The recorded stamp plus two live checks: `lib_matches` (the library on
+    disk is the stamped build) and `sources_match` (the sources beside it are
+    the ones it was built from). None when no stamp exists."""
+    import json
+    if not os.path.exists(path):
+        return {"recorded": None, "lib_matches": None, "sources_match": None}
+    with open(path) as f:
+        rec = json.load(f)
+    lib = library_path()
+    lib_ok = os.path.exists(lib) and _file_sha256(lib) == rec.get("lib_sha256")
+    src_ok = source_digest()[0] == rec.get("sources_sha256") if os.path.isdir(CSRC_DIR) else None
+    return {"recorded": rec, "lib_matches": lib_ok, "sources_match": src_ok}
+
+
 def _check(code: int, where: str) -> None:
     if code != ncclResult.ncclSuccess:
         lib = load_library()
