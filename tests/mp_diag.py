@@ -14,6 +14,7 @@ Pure numpy: the CPU suite tests the mapping with synthetic mismatches
 """
 from __future__ import annotations
 
+import sys
 from dataclasses import dataclass
 
 import numpy as np
@@ -149,6 +150,32 @@ def format_mismatch(d: dict) -> str:
     return "; ".join(s)
 
 
+def compact_mismatch(d: dict) -> str:
+    """One short line (<= ~160 chars) of a description: what survives a
+    truncated log tail (the round-end driver keeps the last 3,000 characters)."""
+    if d.get("n_wrong") is None:
+        return "shape/dtype differ"
+    s = f"{d.get('proto') or '?'} {d['n_wrong']}/{d['n']} wrong"
+    if d["n_wrong"]:
+        s += f" [{d['first']}..{d['last']}] {len(d['runs'])}{'+' if len(d['runs']) >= 8 else ''} runs"
+        expl = [f"{k}={v}" for k, v in sorted(d["explained_by"].items(), key=lambda kv: -kv[1])[:3] if v]
+        if expl:
+            s += " = " + ",".join(expl)
+        if d.get("cells"):
+            c = d["cells"][0]
+            s += f" cells {d['n_cells']} top b{c['block']}r{c['round']}w{c['workgroup']}:{c['wrong']}"
+    return s
+
+
+def emit_summary(lines) -> str:
+    """Print the compact lines to stderr (pytest shows captured stderr after the
+    assertion text, i.e. at the very end of the failure report) and return
+    them as the message's closing block."""
+    text = "SUMMARY " + " | ".join(lines)
+    print(text, file=sys.stderr, flush=True)
+    return text
+
+
 def assert_same(got: np.ndarray, exp: np.ndarray, ctx, geom: SimpleGeometry | None = None, base: int = 0,
                 candidates: dict | None = None) -> None:
     """Bitwise equality, or an AssertionError that says what is wrong."""
@@ -158,7 +185,21 @@ def assert_same(got: np.ndarray, exp: np.ndarray, ctx, geom: SimpleGeometry | No
         got = got.view(exp.dtype) if got.size * got.itemsize % exp.itemsize == 0 else got
     if got.shape == exp.shape and got.dtype == exp.dtype and np.array_equal(got.view(np.uint8), exp.view(np.uint8)):
         return
-    raise AssertionError(f"{ctx}: " + format_mismatch(describe_mismatch(got, exp, geom, base, candidates)))
+    d = describe_mismatch(got, exp, geom, base, candidates)
+    raise AssertionError(f"{ctx}: " + format_mismatch(d) + "\n" + emit_summary([f"{ctx}: {compact_mismatch(d)}"]))
+
+
+def check_equal(got, exp, ctx, geom: SimpleGeometry | None = None, base: int = 0,
+                candidates: dict | None = None) -> None:
+    """`assert np.array_equal(got, exp), ctx` (the same pass rule), with the
+    description and the compact summary when it fails."""
+    got, exp = np.ascontiguousarray(got), np.ascontiguousarray(exp)
+    if np.array_equal(got, exp):
+        return
+    if got.dtype != exp.dtype and got.shape == exp.shape:
+        exp = exp.astype(got.dtype)
+    d = describe_mismatch(got, exp, geom, base, candidates)
+    raise AssertionError(f"{ctx}: " + format_mismatch(d) + "\n" + emit_summary([f"{ctx}: {compact_mismatch(d)}"]))
 
 
 # ---------------------------------------------------------------------------
@@ -272,11 +313,15 @@ def raise_collective_failures(oracle, failures, n, what="") -> None:
     tuples; raises one AssertionError that describes up to six of them."""
     if not failures:
         return
-    lines = []
+    lines, short = [], []
     for (label, kind, dtype, op, count, rank, got, xs, settings, root) in failures[:6]:
         try:
             d = diagnose_collective(oracle, kind, dtype, op, count, n, rank, got, xs, settings, root=root)
             lines.append(f"{label} rank {rank}: {format_mismatch(d)}")
+            short.append(f"{label} r{rank}: {compact_mismatch(d)}")
         except Exception as e:   # the description must never hide the failure itself
             lines.append(f"{label} rank {rank}: wrong output (diagnosis failed: {type(e).__name__}: {e})")
-    raise AssertionError(f"{what}{len(failures)} wrong output(s) at {n} ranks:\n" + "\n".join(lines))
+            short.append(f"{label} r{rank}: wrong ({type(e).__name__} in diagnosis)")
+    head = f"{what}{len(failures)} wrong output(s) at {n} ranks"
+    tail = emit_summary([head] + short)
+    raise AssertionError(head + ":\n" + "\n".join(lines) + "\n" + tail)

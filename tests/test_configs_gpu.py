@@ -306,6 +306,10 @@ def test_configs_d_e_8_ranks_full_size(nbx, oracle, monkeypatch, algo):
             if res[r][key] != digests[r][0]:
                 wrong.append(_describe_chunks(key, r, res[r][key + "_chunks"], digests[r][1], res[r].get("settings"),
                                               algo))
-    assert not wrong, f"configs D/E ({algo}): {len(wrong)} wrong output(s):\n" + "\n".join(wrong[:8])
+    if wrong:
+        from tests import mp_diag
+        head = f"configs D/E ({algo}): {len(wrong)} wrong output(s)"
+        tail = mp_diag.emit_summary([head] + [w.split(";")[0] for w in wrong[:8]])
+        raise AssertionError(head + ":\n" + "\n".join(wrong[:8]) + "\n" + tail)
     times = {k: round(max(res[r][k] for r in range(n)), 2) for k in res[0] if isinstance(k, str) and k.endswith("_ms")}
     print(f"configs D/E ({algo}, 8 ranks sharing one GPU), max ms over ranks: {times}", file=sys.stderr)

@@ -68,6 +68,44 @@ def test_describe_synthetic_mismatch_maps_cells_and_explanations():
     mp_diag.assert_same(exp.copy().view(np.uint8), exp, "equal")
 
 
+def test_compact_summary_survives_a_3000_char_tail(capsys):
+    """The round-end driver keeps the last 3,000 characters of the suite's
+    output: the compact summary is printed last (captured stderr follows the
+    assertion text) and stays short even for six wrong outputs."""
+    g = mp_diag.simple_geometry("ar", 1000003, 4, 8, 32, 64 << 10)
+    rng = np.random.default_rng(2)
+    exp = rng.integers(-2**31, 2**31 - 1, 1000003, dtype=np.int32)
+    got = exp.copy()
+    got[500000:503908] = 0
+    d = mp_diag.describe_mismatch(got, exp, g, 0, {})
+    d["proto"] = "Simple"
+    line = mp_diag.compact_mismatch(d)
+    assert line.startswith("Simple 3908/1000003 wrong [500000..503907] 1 runs = zero=3908 cells")
+    assert len(line) <= 160
+    with pytest.raises(AssertionError) as ei:
+        mp_diag.assert_same(got.view(np.uint8), exp, ("ar", 2, 2, 1000003, 0), g)
+    err = capsys.readouterr().err
+    assert err.startswith("SUMMARY ('ar', 2, 2, 1000003, 0): ?") and "wrong [500000..503907]" in err
+    assert str(ei.value).rstrip().endswith(err.strip())
+    six = " | ".join(["('ar', 2, 2, 1000003, 0) r7: " + line] * 6)
+    assert len(six) < 1200
+
+
+def test_check_equal_keeps_array_equal_semantics(capsys):
+    """check_equal passes exactly when np.array_equal does (values, not dtypes)
+    and describes a failure with the compact summary last."""
+    a = np.arange(1000, dtype=np.int64)
+    mp_diag.check_equal(a.astype(np.int32), a, "same values")
+    mp_diag.check_equal(np.float32([0.0]), np.float32([-0.0]), "signed zero equal as values")
+    b = a.astype(np.int32).copy()
+    b[10:13] = -1
+    with pytest.raises(AssertionError) as ei:
+        mp_diag.check_equal(b, a, ("w0", 1000))
+    assert "3 of 1000 elements wrong; first 10 last 12" in str(ei.value)
+    assert str(ei.value).splitlines()[-1] == "SUMMARY ('w0', 1000): ? 3/1000 wrong [10..12] 1 runs"
+    assert capsys.readouterr().err.strip() == str(ei.value).splitlines()[-1]
+
+
 def test_describe_reduce_scatter_base_offset():
     """ReduceScatter output of rank r starts at send-side element r * recvcount."""
     g = mp_diag.simple_geometry("rs", 5000, 4, 4, 8, 4096)
@@ -108,7 +146,7 @@ def test_gpu_suite_runs_single_gpu_core_first():
     assert c < de
 
 
-def test_diagnose_collective_names_the_missing_source_and_cell():
+def test_diagnose_collective_names_the_missing_source_and_cell(capsys):
     """GPUTEST_r05's case as a synthetic failure: 8 ranks, int32 max over
     1,000,003 elements (Simple direct at the shared-GPU grid of 32); rank 0's
     output has one workgroup's slice of block 6 folded without rank 3's source.
@@ -135,9 +173,17 @@ def test_diagnose_collective_names_the_missing_source_and_cell():
     assert d["proto"] == "Simple" and d["n_wrong"] == changed
     assert d["explained_by"]["without_rank3"] == changed
     assert [(c["block"], c["round"], c["workgroup"]) for c in d["cells"]] == [(6, 0, 9)]
-    with pytest.raises(AssertionError, match=r"without_rank3=.*\(block, round, workgroup\)"):
+    with pytest.raises(AssertionError, match=r"without_rank3=.*\(block, round, workgroup\)") as ei:
         mp_diag.raise_collective_failures(oracle, [("case 36", "ar", 2, 2, count, 0, got.view(np.uint8), xs,
                                                     settings, 1)], n)
+    # the compact form closes the message and goes to stderr (the end of a truncated log)
+    summary = (f"SUMMARY 1 wrong output(s) at 8 ranks | case 36 r0: Simple {changed}/{count} wrong "
+               f"[{int(idx[without3 != full[idx]][0])}..")
+    assert str(ei.value).splitlines()[-1].startswith(summary)
+    last = str(ei.value).splitlines()[-1]
+    assert f" = without_rank3={changed}," in last and last.endswith(f" cells 1 top b6r0w9:{changed}")
+    assert len(last) < 250
+    assert capsys.readouterr().err.startswith(summary)
     # protocol choice as comm_mp_init.cc chooseProtoFor at these settings
     assert mp_diag.proto_of("ar", 1000, 4, 8, settings) == "LL"
     assert mp_diag.proto_of("ar", 50003, 4, 8, settings) == "LL128"

@@ -158,8 +158,8 @@ def test_multiprocess_grouped_collectives(nbx, oracle, n, proto, monkeypatch):
             exp2[lo:hi] = oracle.reduce_multi([exp[lo:hi]] * n, 7, 0, 0, n_pre_op_srcs=n)[0]
     for it in range(2):
         for r in range(n):
-            assert np.array_equal(res[r][(it, "dep")].view(np.float32), exp), (it, r)
-            assert np.array_equal(res[r][(it, "dep2")].view(np.float32), exp2), (it, r)
+            mp_diag.check_equal(res[r][(it, "dep")].view(np.float32), exp, ("dep", it, r))
+            mp_diag.check_equal(res[r][(it, "dep2")].view(np.float32), exp2, ("dep2", it, r))
 
 
 def _run_ranks(nbx, n, target, *extra):
@@ -922,7 +922,7 @@ def test_multiprocess_float_minmax_ties(nbx, oracle, n, monkeypatch):
                 exp[root] = fold([xs[(root + 1 + k) % n] for k in range(n)])
             for r, e in exp.items():
                 got = res[r][(algo, i)]
-                assert np.array_equal(got, np.ascontiguousarray(e).view(np.uint8)), (algo, kind, dt, op, r)
+                mp_diag.check_equal(got, np.ascontiguousarray(e).view(np.uint8), (algo, kind, dt, op, r))
 
 
 def _child_streams(uid_bytes, rank, n, q):
@@ -1173,7 +1173,7 @@ def test_multiprocess_grouped_small_calls_one_launch(nbx, oracle, n, batch, whic
                     continue
                 else:
                     exp = full
-                assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (it, k, kind, dtype, op, count, r)
+                mp_diag.check_equal(got.view(np.uint8), exp.view(np.uint8), (it, k, kind, dtype, op, count, r))
 
 
 REDUCE_CHAIN_COUNTS = (1000, 30000, 300000)   # LL, LL128 one-shot, Simple (defaults, one GPU)
@@ -1241,12 +1241,13 @@ def test_multiprocess_grouped_reduce_chain_root_and_nonroot(nbx, n, null_recv, m
         W1 = sum(ws)
         W2 = W1 + sum(ws[1:])
         y0, z0, w0 = res[0][count]
-        assert np.array_equal(y0, S.astype(np.int32)), count
-        assert np.array_equal(z0, Z.astype(np.int32)), count
-        assert np.array_equal(w0, W2.astype(np.int32)), count
+        mp_diag.check_equal(y0, S.astype(np.int32), ("y0", count))
+        mp_diag.check_equal(z0, Z.astype(np.int32), ("z0", count))
+        mp_diag.check_equal(w0, W2.astype(np.int32), ("w0", count))
         for r in range(1, n):
             yr, zr, wr = res[r][count]
-            assert np.array_equal(yr, ys[r].astype(np.int32)) and np.array_equal(wr, ws[r].astype(np.int32))
+            mp_diag.check_equal(yr, ys[r].astype(np.int32), ("y", count, r))
+            mp_diag.check_equal(wr, ws[r].astype(np.int32), ("w", count, r))
             assert (zr == -1).all()
 
 
@@ -1302,8 +1303,8 @@ def test_multiprocess_transport_only_call(nbx, monkeypatch, n, count):
         for r in range(n):
             rc, y = res[r]["xport"][it]
             assert rc == 0
-            assert np.array_equal(y, want_x), (r, it)
-            assert np.array_equal(res[r]["ar"][it], sum(xs)), (r, it)
+            mp_diag.check_equal(y, want_x, ("xport", r, it))
+            mp_diag.check_equal(res[r]["ar"][it], sum(xs), ("ar", r, it))
 
 
 def _child_link_probe(uid_bytes, rank, n, q):
@@ -1707,8 +1708,8 @@ def test_multiprocess_user_premulsum_per_rank_scalars(nbx, oracle, monkeypatch, 
         order = [(c + 1 + k) % n for k in range(n)]
         plain[lo:hi] = oracle.reduce_multi([xs[j][lo:hi] for j in order], 7, 0)[0]
     for r in range(n):
-        assert np.array_equal(res[r]["group_premul"], e.view(np.uint8)), r
-        assert np.array_equal(res[r]["group_sum"], plain.view(np.uint8)), r
+        mp_diag.check_equal(res[r]["group_premul"], e.view(np.uint8), ("group_premul", r))
+        mp_diag.check_equal(res[r]["group_sum"], plain.view(np.uint8), ("group_sum", r))
 
 
 def _child_split(uid_bytes, rank, n, q):
