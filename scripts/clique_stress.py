@@ -12,6 +12,15 @@ and calls whose ranks all share one stream (those take the fold path), so the
 ordering between the two paths is exercised too.
 Then, with --perf, times back-to-back 4 KiB fp32 AllReduces per call.
 Prints one JSON line per rank count.
+
+The rig needs one hardware queue per stream: with ranks sharing one GPU, a
+rank's kernel queued behind a waiting peer's kernel on a shared hardware queue
+never starts, and every rank's device wait times out. Each rank count creates
+n x streams + 1 streams and they are not returned, so the rank counts of one
+process must fit GPU_MAX_HW_QUEUES together (24 here by default,
+NBX_STRESS_HW_QUEUES up to 32): profiles/r6/clique_queues_r6x/ — 2,3,4,8 in
+one process (30 streams) times out at 24 queues and is exact at 32; 8,8,8 (27)
+times out at its third 8 at 24. The script refuses such a list up front.
 usage: clique_stress.py ranks_list iterations seed [--perf]
 """
 from __future__ import annotations
@@ -23,7 +32,7 @@ import time
 
 # assigned, not defaulted: the GPU box exports GPU_MAX_HW_QUEUES=4, and with fewer hardware
 # queues than streams one rank's kernel can queue behind a peer's waiting one
-os.environ["GPU_MAX_HW_QUEUES"] = "24"
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, int(os.environ.get("NBX_STRESS_HW_QUEUES", "24"))))
 os.environ.setdefault("NBX_CLIQUE_LL", "1")
 os.environ.setdefault("NBX_TIMEOUT_SEC", "5")
 
@@ -99,7 +108,8 @@ def run(n: int, iters: int, seed: int, perf: bool) -> dict:
               flush=True)
         if any(errs_now):   # a device wait gave up: later calls would each wait out the timeout too
             out = {"n": n, "iters": it + 1, "seed": seed, "in_kernel": in_kernel, "checked": ncalls,
-                   "mismatches": bad, "errors": errs, "async_ok": False}
+                   "mismatches": bad, "errors": errs, "async_ok": False,
+                   "last_error": (lib.ncclGetLastError(None) or b"").decode(errors="replace")}
             for c in comms:
                 c.destroy()
             return out
@@ -147,8 +157,17 @@ def run(n: int, iters: int, seed: int, perf: bool) -> dict:
     return out
 
 
+def streams_needed(ns) -> int:
+    """Streams run() creates over the rank counts `ns` in one process."""
+    return sum(n * (2 if n <= 4 else 1) + 1 for n in ns)
+
+
 def main():
     ns = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else [2, 3]
+    queues = int(os.environ["GPU_MAX_HW_QUEUES"])
+    if streams_needed(ns) > queues:
+        sys.exit(f"clique_stress: rank counts {ns} need {streams_needed(ns)} streams in one process, more than the "
+                 f"{queues} hardware queues (GPU_MAX_HW_QUEUES): run them in separate processes")
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     seed = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     perf = "--perf" in sys.argv

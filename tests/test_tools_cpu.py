@@ -197,3 +197,21 @@ def _plain_fold(np_, dt, op, ins):
         return acc.astype(st[dt]).view(np_.uint8)
     f = np_.maximum if op == 2 else np_.minimum
     return f.reduce(vals).view(np_.uint8)
+
+
+def test_clique_stress_refuses_more_streams_than_hardware_queues():
+    """scripts/clique_stress.py: the rank counts of one process must fit the
+    hardware queues (a shared queue deadlocks the in-kernel transport on the
+    one-GPU rig, profiles/r6/clique_queues_r6x/); refused before HIP loads."""
+    script = os.path.join(ROOT, "scripts", "clique_stress.py")
+    env = {k: v for k, v in os.environ.items() if k != "NBX_STRESS_HW_QUEUES"}
+    out = subprocess.run([sys.executable, script, "2,3,4,8", "1", "1"], capture_output=True, text=True,
+                         timeout=60, env=env)
+    assert out.returncode != 0 and "need 30 streams" in out.stderr and "24 hardware queues" in out.stderr
+    out = subprocess.run([sys.executable, script, "8,8,8,8", "1", "1"], capture_output=True, text=True,
+                         timeout=60, env=dict(env, NBX_STRESS_HW_QUEUES="40"))   # clamped to 32
+    assert out.returncode != 0 and "need 36 streams" in out.stderr and "32 hardware queues" in out.stderr
+    code = ("import sys; sys.path.insert(0, 'scripts'); import clique_stress as c; "
+            "print([c.streams_needed(ns) for ns in ([2, 3], [4], [2, 3, 4], [8, 8], [8, 8, 8])])")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
+    assert out.stdout.strip() == "[12, 9, 21, 18, 27]", out.stderr
